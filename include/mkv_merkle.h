@@ -1,0 +1,130 @@
+/*
+ * mkv_merkle.h — C ABI of the MI355X (gfx950) Merkle anti-entropy hot path.
+ *
+ * Drop-in boundary for MerkleKV's `crate::store::merkle::MerkleTree` (/root/reference/src/store/merkle.rs).
+ * The reference exposes a concrete Rust struct, no trait or plugin registry; its callers are
+ * SyncManager (src/sync.rs:104-143, :67) and the HASH command (src/server.rs:647-685). Each entry point
+ * below names the reference method it replaces. All functions are `extern "C"`, take plain pointers
+ * and sizes, and return mkv_status (0 = OK); on failure mkv_last_error() holds a thread-local message.
+ * There is no CPU fallback: without a HIP device every compute call fails with MKV_EHIP.
+ *
+ * Threading: a handle is not thread-safe (the reference mutates through &mut self, serialised by the
+ * callers' tokio Mutex, server.rs:386-390). Calls block until results are host-visible.
+ * Ownership: input blobs are borrowed for the duration of the call; outputs go to caller buffers or to
+ * library-owned mkv_keylist objects freed with mkv_keylist_free.
+ */
+#ifndef MKV_MERKLE_H
+#define MKV_MERKLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t mkv_status;
+#define MKV_OK 0
+#define MKV_EINVAL 1 /* bad argument */
+#define MKV_EHIP 2   /* HIP runtime / device error (includes "no GPU") */
+#define MKV_ENOMEM 3 /* device allocation failed */
+#define MKV_ESTATE 4 /* call not valid in the handle's current state */
+
+typedef struct mkv_tree mkv_tree;       /* opaque: device-resident sorted keys, leaf digests, all levels */
+typedef struct mkv_keylist mkv_keylist; /* opaque: packed key list returned by diff / leaves */
+
+/* Packed byte strings: item i is bytes[offsets[i] .. offsets[i+1]), offsets has n+1 entries.
+ * Host memory unless a function says "device". Keys/values are hashed as the bytes given (the
+ * reference takes &str, i.e. UTF-8; R1 length prefixes are u32, so each item must be < 4 GiB). */
+typedef struct {
+    const uint8_t *bytes;
+    const uint64_t *offsets;
+    uint64_t n;
+} mkv_blob;
+
+/* ---------------- MerkleTree API (merkle.rs) ---------------- */
+
+/* MerkleTree::new() — merkle.rs:36-41. Binds the handle to HIP device `hip_device`. */
+mkv_status mkv_tree_create(int hip_device, mkv_tree **out);
+void mkv_tree_destroy(mkv_tree *t);
+
+/* #[derive(Clone)] (merkle.rs:27): dst (an existing handle on the same device) becomes a deep copy of src. */
+mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst);
+
+/* new() + n x insert(k_i, v_i) in order — merkle.rs:52-56 called by sync.rs:110-115, :130-134 and
+ * server.rs:664-667. Replaces the tree's contents. Duplicate keys: last write wins (merkle.rs:54). */
+mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values);
+/* Same with device pointers (bytes/offsets already resident in HBM on the tree's device). */
+mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
+
+/* n x insert(k_i, v_i) on the existing contents — merkle.rs:52-56 (sequential semantics, one rebuild). */
+mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values);
+/* n x remove(k_i) — merkle.rs:59-62. Missing keys are ignored. */
+mkv_status mkv_tree_remove(mkv_tree *t, mkv_blob keys);
+/* Mixed batch: record i is remove(k_i) if is_remove[i] else insert(k_i, v_i), applied in order. values
+ * must have the same n as keys (the value of a remove record is ignored). */
+mkv_status mkv_tree_apply(mkv_tree *t, mkv_blob keys, mkv_blob values, const uint8_t *is_remove);
+
+/* get_root_hash() — merkle.rs:65-67. *has_root = 0 for the empty tree (R6: root None). */
+mkv_status mkv_tree_root(const mkv_tree *t, uint8_t out32[32], int *has_root);
+/* Number of leaves (leaf_map.len()). */
+mkv_status mkv_tree_len(const mkv_tree *t, uint64_t *n);
+/* node_count() — merkle.rs:156-163 (= 2n-1 for n>0: each pairing adds one node, promotion adds none). */
+mkv_status mkv_tree_node_count(const mkv_tree *t, uint64_t *count);
+/* Implicit level arrays (the reference's MerkleNode tree, merkle.rs:18-25, laid out per level):
+ * level 0 = leaf digests in key order, level nlevels-1 = root. out may be NULL to query *count. */
+mkv_status mkv_tree_level_count(const mkv_tree *t, uint32_t *nlevels);
+mkv_status mkv_tree_level(const mkv_tree *t, uint32_t level, uint64_t *count, uint8_t *out);
+/* leaves() / inorder_keys() — merkle.rs:126-138: sorted keys (library-owned list) and, if digests_out
+ * != NULL, the n*32 leaf digests in the same order. */
+mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *digests_out);
+/* diff_keys(&other) — merkle.rs:171-196: sorted unique keys missing on one side or with different leaf
+ * digests. diff_first_key (merkle.rs:199-204) is element 0. Both trees must be on the same device. */
+mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out);
+/* HASH <prefix> — server.rs:647-685: root of a fresh tree over the keys starting with prefix
+ * (*has_root = 0 when none: the server prints 64 zeros). plen = 0 gives the whole-tree root. */
+mkv_status mkv_tree_prefix_root(const mkv_tree *t, const uint8_t *prefix, uint64_t plen, uint8_t out32[32],
+                                int *has_root);
+
+mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets);
+void mkv_keylist_free(mkv_keylist *l);
+
+const char *mkv_last_error(void);
+
+/* ---------------- sharded build (one process per GPU, key-range shards) ----------------
+ * Shard g holds a contiguous key range; ranges are ordered by rank. Flow per rank:
+ *   mkv_shard_prepare(keys, values)          -> local leaf count n_g (hash + sort + dedup)
+ *   [host all-gathers n_g, computes o_g = sum_{h<g} n_h, N = sum n_h]
+ *   mkv_shard_reduce(o_g, N)                 -> every node whose leaf span lies inside [o_g, o_g+n_g)
+ *   mkv_shard_fringe(buf)                    -> the <= 2 owned nodes per level whose parent is not owned
+ *   [host all-gathers the fringe buffers over RCCL]
+ *   mkv_shard_combine(all, world, N)         -> global root, identical on every rank (seam nodes hashed
+ *                                               on the device). Bit-exact with the unsharded tree. */
+#define MKV_FRINGE_ENTRY_BYTES 48
+#define MKV_FRINGE_MAX_ENTRIES 130
+#define MKV_FRINGE_BYTES (MKV_FRINGE_ENTRY_BYTES * MKV_FRINGE_MAX_ENTRIES)
+mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on_device, uint64_t *n_local);
+mkv_status mkv_shard_reduce(mkv_tree *t, uint64_t global_offset, uint64_t global_n);
+mkv_status mkv_shard_fringe(const mkv_tree *t, uint8_t *out /* MKV_FRINGE_BYTES */);
+mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes /* world x MKV_FRINGE_BYTES */, uint32_t world,
+                             uint64_t global_n, uint8_t out32[32], int *has_root);
+
+/* ---------------- measurement / test utilities (not part of the reference API) ---------------- */
+/* Per-kernel-group device time accumulated with HIP events on the tree's stream when enabled.
+ * Groups: "leaf_hash", "sort", "gather", "reduce", "diff", "total_build". */
+mkv_status mkv_prof_enable(mkv_tree *t, int on);
+mkv_status mkv_prof_reset(mkv_tree *t);
+mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms, uint64_t *count);
+/* Synthetic records (same generator as oracle/merkle_oracle.c) written to device buffers:
+ * kb >= n*klen, vb >= n*vlen, koff/voff n+1 entries. Synchronous. */
+mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,
+                                  uint32_t vlen, uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb,
+                                  uint64_t *koff, uint8_t *vb, uint64_t *voff);
+/* Leaf digests only (Kernel A) over host records; out = n*32 bytes. */
+mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint8_t *out);
+/* Library version string. */
+const char *mkv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MKV_MERKLE_H */

@@ -1,0 +1,60 @@
+// common.hpp — shared host/device definitions for the MI355X (gfx950) Merkle hot path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include <stdexcept>
+#include <string>
+
+namespace mkv {
+
+// Error type carried from the runtime to the C ABI (mkv_status + thread-local message).
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+enum : int { ST_OK = 0, ST_EINVAL = 1, ST_EHIP = 2, ST_ENOMEM = 3, ST_ESTATE = 4 };
+
+#define MKV_HIP(expr)                                                                                  \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            throw ::mkv::Error(e_ == hipErrorOutOfMemory ? ::mkv::ST_ENOMEM : ::mkv::ST_EHIP,          \
+                               std::string(#expr " failed: ") + hipGetErrorString(e_));               \
+    } while (0)
+
+#define MKV_LAUNCH_CHECK() MKV_HIP(hipGetLastError())
+
+// Growable device buffer. Grows only; steady-state builds of the same size never re-allocate.
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) {
+            (void)hipDeviceSynchronize();  // growth is rare; never free under in-flight work
+            (void)hipFree(p);
+        }
+        p = nullptr;
+        cap = 0;
+    }
+    // Contents are NOT preserved on growth. 256 B of tail padding keeps wide over-reads in bounds.
+    void *ensure(size_t bytes) {
+        if (bytes <= cap && p) return p;
+        release();
+        size_t want = bytes + 256;
+        MKV_HIP(hipMalloc(&p, want));
+        cap = bytes;
+        return p;
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+
+}  // namespace mkv

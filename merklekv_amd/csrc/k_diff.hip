@@ -1,0 +1,312 @@
+// k_diff.hip — Kernel D: two-tree key diff (R7, merkle.rs:171-196) and prefix bounds (HASH <prefix>).
+//
+// The reference builds a BTreeSet over the union of both leaf maps and looks every key up in both
+// HashMaps. Both trees here already hold their leaves sorted by key (R3), so the same set is a
+// merge-join of two sorted (key, digest) arrays:
+//   pass 0  partition the merged sequence into 2048-output tiles (one merge-path binary search per tile);
+//   pass 1  each 256-thread workgroup stages its A and B prefix slices (u64 BE key prefixes) in LDS,
+//           every lane finds its 8-output diagonal in LDS and merges; an A key is divergent unless the
+//           B cursor holds the same key with the same leaf digest, a B key unless the previous A key is
+//           equal. Lane results are packed to one u32 (split, from-A bits, divergent bits) plus a
+//           per-tile count;
+//   scan    exclusive scan of tile counts;
+//   pass 2  ballot/LDS compaction writes (side, index) refs of divergent keys in merged = sorted order.
+// Ties on the 8-byte prefix fall back to a full-key compare in HBM (key_cmp), so any key set is exact.
+#include "common.hpp"
+#include "dev_util.hpp"
+#include "kernels.hpp"
+
+namespace mkv {
+
+namespace {
+
+constexpr int DT = DIFF_THREADS;
+constexpr int DI = DIFF_ITEMS;
+constexpr int DTILE = DT * DI;
+
+__device__ __forceinline__ int cmp_ab(const DiffSide &A, uint64_t i, uint64_t pa, const DiffSide &B, uint64_t j,
+                                      uint64_t pb) {
+    if (pa != pb) return pa < pb ? -1 : 1;
+    uint64_t a0 = A.koff[i], a1 = A.koff[i + 1], b0 = B.koff[j], b1 = B.koff[j + 1];
+    return key_cmp(A.kb + a0, a1 - a0, pa, B.kb + b0, b1 - b0, pb);
+}
+
+__device__ __forceinline__ bool digest_eq(const uint8_t *a, const uint8_t *b) {
+    const uint4 *x = reinterpret_cast<const uint4 *>(a);
+    const uint4 *y = reinterpret_cast<const uint4 *>(b);
+    uint4 x0 = x[0], x1 = x[1], y0 = y[0], y1 = y[1];
+    return x0.x == y0.x && x0.y == y0.y && x0.z == y0.z && x0.w == y0.w && x1.x == y1.x && x1.y == y1.y &&
+           x1.z == y1.z && x1.w == y1.w;
+}
+
+// Merge-path split of diagonal d over the full arrays: number of A elements among the first d outputs
+// (A before B on equal keys).
+__device__ uint64_t split_global(const DiffSide &A, const DiffSide &B, uint64_t d) {
+    uint64_t lo = d > B.n ? d - B.n : 0, hi = d < A.n ? d : A.n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        uint64_t jb = d - 1 - mid;
+        if (cmp_ab(A, mid, A.pfx[mid], B, jb, B.pfx[jb]) <= 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_diff_partition(DiffSide A, DiffSide B, uint64_t ntiles, uint64_t *__restrict__ split) {
+    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    uint64_t M = A.n + B.n;
+    uint64_t d = t * DTILE;
+    if (d > M) d = M;
+    split[t] = split_global(A, B, d);
+}
+
+struct TileCtx {
+    uint64_t a0, a1, b0, b1;  // this tile's A range [a0,a1) and B range [b0,b1)
+    uint64_t d0;              // first merged output of the tile
+};
+
+// LDS layout: pa[0] = A[a0-1] (if a0 > 0), pa[1 + x] = A[a0 + x]; pb[x] = B[b0 + x], pb[b1-b0] = B[b1].
+__device__ __forceinline__ void stage_tile(const DiffSide &A, const DiffSide &B, const TileCtx &c, uint64_t *pa,
+                                           uint64_t *pb) {
+    const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
+    for (uint64_t x = threadIdx.x; x < na + 1; x += DT) {
+        uint64_t g = c.a0 + x;  // pa[x+1] = A[a0+x], pa[0] = A[a0-1]
+        if (x < na) pa[x + 1] = A.pfx[g];
+    }
+    if (threadIdx.x == 0) pa[0] = c.a0 > 0 ? A.pfx[c.a0 - 1] : 0;
+    for (uint64_t x = threadIdx.x; x <= nb; x += DT) {
+        uint64_t g = c.b0 + x;
+        if (g < B.n) pb[x] = B.pfx[g];
+    }
+    __syncthreads();
+}
+
+// Runs one lane's merge; returns packed (isplit << 16) | (fromA << 8) | div and the div count.
+__device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide &B, const TileCtx &c,
+                                               const uint64_t *pa, const uint64_t *pb, uint32_t *ndiv) {
+    const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
+    const uint64_t M = A.n + B.n;
+    const uint64_t dl = (uint64_t)threadIdx.x * DI;  // local diagonal
+    if (c.d0 + dl >= M || dl >= na + nb) {
+        *ndiv = 0;
+        return 0;
+    }
+    // local merge-path search
+    uint64_t lo = dl > nb ? dl - nb : 0, hi = dl < na ? dl : na;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        uint64_t jb = dl - 1 - mid;
+        if (cmp_ab(A, c.a0 + mid, pa[1 + mid], B, c.b0 + jb, pb[jb]) <= 0) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint32_t isplit = (uint32_t)lo;
+    uint64_t i = c.a0 + lo, j = c.b0 + (dl - lo);
+    uint32_t fromA = 0, div = 0;
+#pragma unroll
+    for (int s = 0; s < DI; ++s) {
+        if (dl + s >= na + nb) break;
+        const uint64_t li = i - c.a0, lj = j - c.b0;
+        bool takeA;
+        int cab = 1;
+        if (i >= c.a1) takeA = false;
+        else if (j >= B.n) takeA = true;
+        else {
+            cab = cmp_ab(A, i, pa[1 + li], B, j, pb[lj]);
+            takeA = (j >= c.b1) ? true : (cab <= 0);
+            // j == b1 < B.n: the tile's B slice is exhausted, so A[i] < B[b1] or equal (then matched)
+        }
+        bool d;
+        if (takeA) {
+            bool matched = (j < B.n) && cab == 0;
+            d = !matched || !digest_eq(A.dig + 32 * i, B.dig + 32 * j);
+            fromA |= 1u << s;
+            ++i;
+        } else {
+            bool matched = false;
+            if (i > 0) {
+                const uint64_t pprev = pa[li];  // A[i-1]: li-1+1
+                matched = cmp_ab(A, i - 1, pprev, B, j, pb[lj]) == 0;
+            }
+            d = !matched;
+            ++j;
+        }
+        if (d) div |= 1u << s;
+    }
+    *ndiv = (uint32_t)__popc(div);
+    return (isplit << 16) | (fromA << 8) | div;
+}
+
+__device__ __forceinline__ TileCtx tile_ctx(const DiffSide &A, const DiffSide &B, const uint64_t *split) {
+    TileCtx c;
+    const uint64_t M = A.n + B.n;
+    const uint64_t t = blockIdx.x;
+    c.d0 = t * DTILE;
+    uint64_t d1 = c.d0 + DTILE;
+    if (d1 > M) d1 = M;
+    c.a0 = split[t];
+    c.a1 = split[t + 1];
+    c.b0 = c.d0 - c.a0;
+    c.b1 = d1 - c.a1;
+    return c;
+}
+
+__global__ __launch_bounds__(DT) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
+                                                   uint32_t *__restrict__ packed, uint32_t *__restrict__ tilecnt) {
+    __shared__ uint64_t pa[DTILE + 2];
+    __shared__ uint64_t pb[DTILE + 2];
+    __shared__ uint32_t wsum[DT / 64];
+    const TileCtx c = tile_ctx(A, B, split);
+    stage_tile(A, B, c, pa, pb);
+    uint32_t nd;
+    const uint32_t pk = merge_lane(A, B, c, pa, pb, &nd);
+    packed[(uint64_t)blockIdx.x * DT + threadIdx.x] = pk;
+    // tile total
+    uint32_t s = nd;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < DT / 64; ++w) tot += wsum[w];
+        tilecnt[blockIdx.x] = tot;
+    }
+}
+
+__global__ __launch_bounds__(DT) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
+                                                   const uint32_t *__restrict__ packed,
+                                                   const uint64_t *__restrict__ tileoff, uint64_t *__restrict__ refs) {
+    __shared__ uint64_t lds[16];
+    const TileCtx c = tile_ctx(A, B, split);
+    const uint32_t pk = packed[(uint64_t)blockIdx.x * DT + threadIdx.x];
+    const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
+    uint64_t off = block_excl_scan<uint64_t>((uint64_t)__popc(div), lds, nullptr) + tileoff[blockIdx.x];
+    if (!div) return;
+    const uint64_t dl = (uint64_t)threadIdx.x * DI;
+    uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
+    for (int s = 0; s < DI; ++s) {
+        const bool fa = (fromA >> s) & 1u;
+        const uint64_t ref = fa ? i : (j | (1ull << 63));
+        if (fa) ++i; else ++j;
+        if ((div >> s) & 1u) refs[off++] = ref;
+    }
+}
+
+__global__ void k_diff_keylens(const uint64_t *__restrict__ refs, uint64_t m, DiffSide A, DiffSide B,
+                               uint64_t *__restrict__ lens) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    uint64_t r = refs[k];
+    const DiffSide &S = (r >> 63) ? B : A;
+    uint64_t i = r & ~(1ull << 63);
+    lens[k] = S.koff[i + 1] - S.koff[i];
+}
+
+__global__ void k_diff_keys(const uint64_t *__restrict__ refs, uint64_t m, DiffSide A, DiffSide B,
+                            const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    uint64_t r = refs[k];
+    const DiffSide &S = (r >> 63) ? B : A;
+    uint64_t i = r & ~(1ull << 63);
+    uint64_t a = S.koff[i], len = S.koff[i + 1] - a;
+    const uint8_t *s = S.kb + a;
+    uint8_t *d = out + off[k];
+    for (uint64_t x = 0; x < len; ++x) d[x] = s[x];
+}
+
+// lohi[0] = lower_bound(prefix), lohi[1] = first index >= lo whose key does not start with prefix.
+__global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, uint32_t plen,
+                                uint64_t *__restrict__ lohi) {
+    if (threadIdx.x != 0) return;
+    const uint64_t pp = key_chunk(prefix, plen, 0);
+    uint64_t lo = 0, hi = A.n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        uint64_t a0 = A.koff[mid], a1 = A.koff[mid + 1];
+        if (key_cmp(A.kb + a0, a1 - a0, A.pfx[mid], prefix, plen, pp) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    // keys with the prefix are exactly those >= prefix that start with it: binary search on "starts with"
+    uint64_t l2 = lo, h2 = A.n;
+    while (l2 < h2) {
+        uint64_t mid = (l2 + h2) >> 1;
+        uint64_t a0 = A.koff[mid], a1 = A.koff[mid + 1];
+        bool starts = (a1 - a0) >= plen;
+        for (uint32_t x = 0; starts && x < plen; ++x) starts = A.kb[a0 + x] == prefix[x];
+        if (starts) l2 = mid + 1;
+        else h2 = mid;
+    }
+    lohi[0] = lo;
+    lohi[1] = l2;
+}
+
+__global__ void k_widen_u32(const uint32_t *__restrict__ c, uint64_t *__restrict__ o, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) o[i] = c[i];
+}
+
+inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_div(n ? n : 1, bs)); }
+
+}  // namespace
+
+size_t diff_scratch_bytes(uint64_t M) {
+    uint64_t nt = ceil_div(M ? M : 1, DTILE);
+    size_t b = 0;
+    b += (nt + 2) * sizeof(uint64_t);             // split
+    b += nt * DT * sizeof(uint32_t);              // packed
+    b += (nt + 2) * sizeof(uint32_t);             // tile counts
+    b += (nt + 2) * sizeof(uint64_t);             // tile offsets
+    b += scan_scratch_bytes(nt) + 1024;
+    return b;
+}
+
+void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
+                 hipStream_t st) {
+    const uint64_t M = A.n + B.n;
+    if (M == 0) {
+        MKV_HIP(hipMemsetAsync(count, 0, sizeof(uint64_t), st));
+        return;
+    }
+    const uint64_t nt = ceil_div(M, DTILE);
+    uint8_t *p = reinterpret_cast<uint8_t *>(scratch);
+    auto carve = [&](size_t bytes) {
+        uint8_t *r = p;
+        p += (bytes + 255) & ~size_t(255);
+        return r;
+    };
+    uint64_t *split = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
+    uint32_t *packed = reinterpret_cast<uint32_t *>(carve(nt * DT * sizeof(uint32_t)));
+    uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
+    uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
+    void *sc = carve(scan_scratch_bytes(nt));
+    hipLaunchKernelGGL(k_diff_partition, grid1d(nt + 1), dim3(256), 0, st, A, B, nt, split);
+    hipLaunchKernelGGL(k_diff_pass1, dim3((uint32_t)nt), dim3(DT), 0, st, A, B, split, packed, tilecnt);
+    MKV_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);
+    exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
+    hipLaunchKernelGGL(k_diff_pass2, dim3((uint32_t)nt), dim3(DT), 0, st, A, B, split, packed, tileoff, refs);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
+                         hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_diff_keylens, grid1d(m), dim3(256), 0, st, refs, m, A, B, lens);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,
+                      uint8_t *out, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_diff_keys, grid1d(m), dim3(256), 0, st, refs, m, A, B, off, out);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t plen, uint64_t *lohi, hipStream_t st) {
+    hipLaunchKernelGGL(k_prefix_bounds, dim3(1), dim3(64), 0, st, A, prefix, plen, lohi);
+    MKV_LAUNCH_CHECK();
+}
+
+}  // namespace mkv

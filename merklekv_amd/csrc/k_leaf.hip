@@ -1,0 +1,218 @@
+// k_leaf.hip — Kernel A: batched leaf hashing (R1 + R2).
+//
+// Restates merkle.rs:7-16 (encode_leaf) fused into merkle.rs:45-49 (compute_leaf_hash): the digest of
+// u32_be(|k|) || k || u32_be(|v|) || v, computed without ever materialising the encoding.
+//
+// Layout: records arrive as two packed blobs with u64 offsets (keys kb/koff, values vb/voff), exactly
+// the mkv_blob pair of the C ABI. One lane owns one record; one wave owns 64 consecutive records, so
+// the wave's key bytes and value bytes are each one contiguous span. The wave copies both spans into
+// its private LDS region with coalesced 16-byte loads, then every lane builds its message words from
+// LDS (ds_read_b32 + v_perm_b32 for the byte-swap / unaligned extract) and runs the compressions with
+// state and the rolling schedule in VGPRs.
+//
+// Paths (chosen per wave, uniformly):
+//   fast    — every record in the wave has the same |k| and |v|, both multiples of 4, 4-aligned in
+//             LDS: every message word is one whole LDS word or a constant (the bench/config path).
+//   generic — any lengths / alignments: words are assembled from byte-range masks.
+//   global  — the wave's spans do not fit its LDS region: generic assembly straight from HBM.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "sha256.hpp"
+
+namespace mkv {
+
+namespace {
+
+constexpr int LEAF_WAVES = 4;                 // waves per workgroup
+constexpr uint32_t LEAF_LDS_WAVE = 10240;     // bytes of LDS per wave (4 waves -> 40 KiB per WG)
+
+// Big-endian word of the 4 bytes at byte offset `off` of an LDS byte region starting at `base` (bytes).
+__device__ __forceinline__ uint32_t lds_be_word(const uint32_t *lds, uint32_t byte) {
+    uint32_t a = byte >> 2, sh = byte & 3;
+    uint32_t lo = lds[a], hi = lds[a + 1];
+    return __builtin_amdgcn_perm(hi, lo, 0x00010203u + sh * 0x01010101u);
+}
+
+// Same from global memory, never touching a 4-byte chunk that lies wholly past `end`.
+__device__ __forceinline__ uint32_t glb_be_word(const uint8_t *p, const uint8_t *end) {
+    uintptr_t ad = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *a = reinterpret_cast<const uint32_t *>(ad & ~uintptr_t(3));
+    uint32_t sh = (uint32_t)(ad & 3);
+    uint32_t lo = (reinterpret_cast<const uint8_t *>(a) < end) ? a[0] : 0u;
+    uint32_t hi = (reinterpret_cast<const uint8_t *>(a + 1) < end) ? a[1] : 0u;
+    return __builtin_amdgcn_perm(hi, lo, 0x00010203u + sh * 0x01010101u);
+}
+
+// Mask of the first n (0..4) bytes of a big-endian word.
+__device__ __forceinline__ uint32_t head_mask(int n) {
+    return n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : ~(0xFFFFFFFFu >> (8 * n)));
+}
+
+struct LdsSrc {
+    const uint32_t *lds;
+    uint32_t kbyte, vbyte;  // byte offsets of this lane's key / value inside the wave's region
+    __device__ __forceinline__ uint32_t key(uint32_t q, uint32_t) const { return lds_be_word(lds, kbyte + q); }
+    __device__ __forceinline__ uint32_t val(uint32_t q, uint32_t) const { return lds_be_word(lds, vbyte + q); }
+};
+
+struct GlbSrc {
+    const uint8_t *k, *v;
+    const uint8_t *kend, *vend;
+    __device__ __forceinline__ uint32_t key(uint32_t q, uint32_t) const { return glb_be_word(k + q, kend); }
+    __device__ __forceinline__ uint32_t val(uint32_t q, uint32_t) const { return glb_be_word(v + q, vend); }
+};
+
+// Generic message word at byte position p (multiple of 4) of the padded encoding.
+template <class Src>
+__device__ __forceinline__ uint32_t msg_word(const Src &src, uint32_t p, uint32_t klen, uint32_t vlen, uint32_t L) {
+    uint32_t w = 0;
+    if (p == 0) w = klen;  // u32_be(|k|), bytes [0,4)
+    // key bytes at [4, 4+klen): stream offset qk = p - 4 (multiple of 4, >= 0 once p >= 4)
+    if (p >= 4 && p - 4 < klen) {
+        uint32_t qk = p - 4;
+        w |= src.key(qk, klen) & head_mask((int)(klen - qk));
+    }
+    // u32_be(|v|) at [4+klen, 8+klen)
+    int d = (int)(4 + klen) - (int)p;
+    if (d >= 0 && d < 4) w |= vlen >> (8 * d);
+    else if (d < 0 && d > -4) w |= vlen << (8 * -d);
+    // value bytes at [8+klen, L)
+    int qv = (int)p - (int)(8 + klen);
+    if (qv > -4 && qv < (int)vlen) {
+        int s = qv < 0 ? -qv : 0;                     // first byte of the word that is value data
+        uint32_t raw = src.val((uint32_t)(qv < 0 ? 0 : qv), vlen);
+        raw = s ? (raw >> (8 * s)) : raw;
+        int e = (int)vlen - qv;                       // one past the last value byte, word-relative
+        uint32_t m = head_mask(e < 4 ? e : 4) & ~head_mask(s);
+        w |= raw & m;
+    }
+    // 0x80 terminator at L
+    int d2 = (int)L - (int)p;
+    if (d2 >= 0 && d2 < 4) w |= 0x80000000u >> (8 * d2);
+    return w;
+}
+
+template <class Src>
+__device__ __forceinline__ void hash_generic(const Src &src, uint32_t klen, uint32_t vlen, uint32_t out[8]) {
+    uint32_t L = 8 + klen + vlen;
+    uint32_t nb = (L + 9 + 63) >> 6;
+    uint64_t bits = (uint64_t)L * 8;
+    sha_init(out);
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = msg_word(src, blk * 64 + 4 * i, klen, vlen, L);
+        if (blk == nb - 1) {
+            w[14] |= (uint32_t)(bits >> 32);
+            w[15] |= (uint32_t)bits;
+        }
+        sha_compress(out, w);
+    }
+}
+
+// Fast path: K0 = |k|, V0 = |v| wave-uniform multiples of 4, data 4-aligned in LDS. Word g of the
+// message is: 0 -> K0 | 1..K0/4 -> key | K0/4+1 -> V0 | .. -> value | L/4 -> 0x80000000 | 0.
+__device__ __forceinline__ void hash_fast(const uint32_t *lds, uint32_t kword, uint32_t vword, uint32_t K0,
+                                          uint32_t V0, uint32_t out[8]) {
+    const uint32_t kw = K0 >> 2, vw = V0 >> 2;
+    const uint32_t vbeg = kw + 2, vend = kw + 2 + vw, lw = vend;  // L/4 == vend
+    const uint32_t L = 8 + K0 + V0;
+    const uint32_t nb = (L + 9 + 63) >> 6;
+    const uint64_t bits = (uint64_t)L * 8;
+    sha_init(out);
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint32_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t g = blk * 16 + i;
+            uint32_t x;
+            if (g == 0) x = K0;
+            else if (g <= kw) x = bswap32(lds[kword + g - 1]);
+            else if (g == kw + 1) x = V0;
+            else if (g < vend) x = bswap32(lds[vword + g - vbeg]);
+            else if (g == lw) x = 0x80000000u;
+            else x = 0;
+            w[i] = x;
+        }
+        if (blk == nb - 1) {
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+        sha_compress(out, w);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                  const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                  uint64_t n, uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t r0 = ((uint64_t)blockIdx.x * LEAF_WAVES + wave) * 64;
+    const bool wave_live = r0 < n;
+    const uint64_t r = r0 + lane;
+    const bool valid = r < n;
+    uint32_t *lds = lds_all + wave * (LEAF_LDS_WAVE / 4);
+
+    uint64_t k0 = 0, v0 = 0, k1 = 0, v1 = 0;
+    const uint8_t *kstart = kb, *vstart = vb;
+    uint32_t kspan = 0, vspan = 0;
+    bool staged = false;
+    if (wave_live) {
+        uint64_t rc = n - r0 < 64 ? n - r0 : 64;
+        k0 = koff[r0]; k1 = koff[r0 + rc];
+        v0 = voff[r0]; v1 = voff[r0 + rc];
+        kstart = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(kb + k0) & ~uintptr_t(15));
+        vstart = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(vb + v0) & ~uintptr_t(15));
+        uint64_t ks = (uint64_t)((kb + k1) - kstart), vs = (uint64_t)((vb + v1) - vstart);
+        ks = (ks + 15) & ~uint64_t(15);
+        vs = (vs + 15) & ~uint64_t(15);
+        staged = ks + vs + 32 <= LEAF_LDS_WAVE;
+        if (staged) {
+            kspan = (uint32_t)ks;
+            vspan = (uint32_t)vs;
+            const uint4 *gk = reinterpret_cast<const uint4 *>(kstart);
+            const uint4 *gv = reinterpret_cast<const uint4 *>(vstart);
+            uint4 *lk = reinterpret_cast<uint4 *>(lds);
+            uint4 *lv = reinterpret_cast<uint4 *>(lds + kspan / 4);
+            for (uint32_t i = lane; i < kspan / 16; i += 64) lk[i] = gk[i];
+            for (uint32_t i = lane; i < vspan / 16; i += 64) lv[i] = gv[i];
+        }
+    }
+    __syncthreads();
+    if (!valid) return;
+
+    const uint64_t kbeg = koff[r], kend = koff[r + 1], vbeg = voff[r], vend = voff[r + 1];
+    const uint32_t klen = (uint32_t)(kend - kbeg), vlen = (uint32_t)(vend - vbeg);
+    uint32_t st[8];
+    if (staged) {
+        const uint32_t kbyte = (uint32_t)((kb + kbeg) - kstart);
+        const uint32_t vbyte = kspan + (uint32_t)((vb + vbeg) - vstart);
+        // wave-uniform fast-path test over the live lanes
+        const uint32_t K0 = __shfl(klen, 0), V0 = __shfl(vlen, 0);
+        const bool mine = klen == K0 && vlen == V0 && ((K0 | V0 | kbyte | vbyte) & 3) == 0;
+        if (__all(mine)) {
+            hash_fast(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
+                      __builtin_amdgcn_readfirstlane(V0), st);
+        } else {
+            LdsSrc src{lds, kbyte, vbyte};
+            hash_generic(src, klen, vlen, st);
+        }
+    } else {
+        GlbSrc src{kb + kbeg, vb + vbeg, kb + kend, vb + vend};
+        hash_generic(src, klen, vlen, st);
+    }
+    store_digest(out + 32 * r, st);
+}
+
+}  // namespace
+
+void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                      uint8_t *out, hipStream_t st) {
+    if (n == 0) return;
+    uint64_t waves = ceil_div(n, 64);
+    uint64_t blocks = ceil_div(waves, LEAF_WAVES);
+    hipLaunchKernelGGL(k_leaf_hash, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff, n, out);
+    MKV_LAUNCH_CHECK();
+}
+
+}  // namespace mkv

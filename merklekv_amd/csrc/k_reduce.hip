@@ -1,0 +1,179 @@
+// k_reduce.hip — Kernel B: level-by-level internal-node reduction (R4/R5, merkle.rs:94-118).
+//
+// The reference materialises a pointer tree, deep-cloning both subtrees into every parent
+// (merkle.rs:107-108). Here the tree is implicit: level l is a dense array of 32-byte digests and
+// node (l, j) covers leaves [j*2^l, min((j+1)*2^l, n)). Parent j hashes children 2j and 2j+1; when
+// 2j+1 falls off the end of an odd level the child is promoted unchanged (R5), so level sizes are
+// n, ceil(n/2), ceil(n/4), ..., 1 and every level is kept in HBM (diff, level views, incremental).
+//
+// One launch fuses up to 4 levels (10 for the last, small launch): a 512-thread workgroup owns a
+// tile of 512 first-level parents (1024 children read coalesced from HBM, 64 B per lane), keeps each
+// produced level in LDS (BE words, ping-pong 2 x 16 KiB) and feeds the next level from there. Level k
+// of the tile has 512>>(k-1) parents, so with 4 fused levels every wave is fully busy: 8+4+2+1
+// wave-hashes for 960 hashes, no lane idles. The second compression of every node is the constant
+// padding block (sha_compress_pad64), so a node costs ~1.65 compressions of VALU work.
+//
+// Ownership (sharded trees): a launch computes only nodes whose leaf span lies inside the shard
+// [o, o+n); plan.a/plan.c give, per level, the owned global index range. With one shard this is the
+// whole tree.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "sha256.hpp"
+
+namespace mkv {
+
+namespace {
+
+constexpr int RD_THREADS = 512;
+constexpr int RD_TILE = 512;
+
+__global__ __launch_bounds__(RD_THREADS) void k_reduce_fused(FusePlan p) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
+    const uint64_t t = p.tile0 + blockIdx.x;
+    const uint32_t i = threadIdx.x;
+    for (int k = 1; k <= p.nl; ++k) {
+        const uint64_t Tk = (uint64_t)RD_TILE >> (k - 1);
+        const uint64_t j = t * Tk + i;
+        const bool own = i < Tk && j >= p.a[k] && j < p.a[k] + p.c[k];
+        if (own) {
+            uint32_t l[8], r[8], o[8];
+            const uint64_t c0 = 2 * j;
+            const bool pair = c0 + 1 < p.S[k - 1];
+            if (k == 1) {
+                const uint8_t *src = p.in + 32 * (c0 - p.a[0]);
+                load_digest(src, l);
+                if (pair) load_digest(src + 32, r);
+            } else {
+                const uint32_t *src = buf[(k - 1) & 1] + 16 * i;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    l[q] = src[q];
+                    r[q] = src[8 + q];
+                }
+            }
+            if (pair) {
+                sha_node(l, r, o);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) o[q] = l[q];  // R5: promote unchanged
+            }
+            uint32_t *dst = buf[k & 1] + 8 * i;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dst[q] = o[q];
+            store_digest(p.out[k - 1] + 32 * (j - p.a[k]), o);
+        }
+        __syncthreads();
+    }
+}
+
+// ---- seam combine ----
+struct SeamEntry {
+    uint32_t level;
+    uint32_t valid;
+    uint64_t idx;
+    uint8_t h[32];
+};
+static_assert(sizeof(SeamEntry) == 48, "seam entry layout");
+
+constexpr int SEAM_MAX = 64;
+
+// One wave. Loose nodes of level l (fringes handed over by the shards + seam nodes computed from
+// level l-1) are kept sorted by index in LDS; each lane hashes at most one parent per level.
+__global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict__ ent, uint32_t nent,
+                                                    const uint64_t *__restrict__ S, uint32_t L,
+                                                    uint8_t *__restrict__ root) {
+    __shared__ uint64_t cidx[SEAM_MAX];
+    __shared__ uint32_t ch[SEAM_MAX][8];
+    __shared__ uint64_t nidx[SEAM_MAX];
+    __shared__ uint32_t nh[SEAM_MAX][8];
+    __shared__ uint32_t ncnt, ccnt, epos;
+    const uint32_t lane = threadIdx.x;
+    if (lane == 0) {
+        ccnt = 0;
+        epos = 0;
+    }
+    __syncthreads();
+    for (uint32_t l = 0; l < L; ++l) {
+        // computed parents of level l come from cur (level l-1) -> nidx/nh (sorted by construction)
+        if (lane == 0) ncnt = 0;
+        __syncthreads();
+        if (l > 0) {
+            const uint32_t cc = ccnt;
+            bool act = false;
+            uint64_t x = 0;
+            uint32_t lw[8], rw[8], ow[8];
+            bool pair = false;
+            if (lane < cc) {
+                x = cidx[lane];
+                if ((x & 1) == 0) {
+                    act = true;
+                    pair = x + 1 < S[l - 1];
+                    for (int q = 0; q < 8; ++q) lw[q] = ch[lane][q];
+                    if (pair) {
+                        // sibling must be the next loose node
+                        for (int q = 0; q < 8; ++q) rw[q] = (lane + 1 < cc) ? ch[lane + 1][q] : 0u;
+                    }
+                }
+            }
+            const uint64_t m = __ballot(act);
+            if (act) {
+                if (pair) sha_node(lw, rw, ow);
+                else
+                    for (int q = 0; q < 8; ++q) ow[q] = lw[q];
+                const uint32_t slot = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                nidx[slot] = x >> 1;
+                for (int q = 0; q < 8; ++q) nh[slot][q] = ow[q];
+            }
+            if (lane == 0) ncnt = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        // merge computed (nidx) with this level's fringe entries into cur (single lane, tiny lists)
+        if (lane == 0) {
+            uint32_t a = 0, na = ncnt, e = epos, c = 0;
+            while (true) {
+                const bool hasE = e < nent && ent[e].level == l;
+                const bool hasA = a < na;
+                if (!hasE && !hasA) break;
+                bool takeE = hasE && (!hasA || ent[e].idx < nidx[a]);
+                if (c < SEAM_MAX) {
+                    if (takeE) {
+                        cidx[c] = ent[e].idx;
+                        const uint8_t *h = ent[e].h;
+                        for (int q = 0; q < 8; ++q)
+                            ch[c][q] = ((uint32_t)h[4 * q] << 24) | ((uint32_t)h[4 * q + 1] << 16) |
+                                       ((uint32_t)h[4 * q + 2] << 8) | (uint32_t)h[4 * q + 3];
+                    } else {
+                        cidx[c] = nidx[a];
+                        for (int q = 0; q < 8; ++q) ch[c][q] = nh[a][q];
+                    }
+                }
+                ++c;
+                if (takeE) ++e; else ++a;
+            }
+            ccnt = c < SEAM_MAX ? c : SEAM_MAX;
+            epos = e;
+        }
+        __syncthreads();
+    }
+    if (lane == 0) {
+        if (ccnt >= 1) store_digest(root, ch[0]);
+    }
+}
+
+}  // namespace
+
+void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
+    if (p.ntiles == 0) return;
+    hipLaunchKernelGGL(k_reduce_fused, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_seam_combine(const uint8_t *entries, uint32_t nent, const uint64_t *level_sizes, uint32_t nlevels,
+                         uint8_t *scratch, uint8_t *root_out, hipStream_t st) {
+    (void)scratch;
+    hipLaunchKernelGGL(k_seam_combine, dim3(1), dim3(64), 0, st, reinterpret_cast<const SeamEntry *>(entries), nent,
+                       level_sizes, nlevels, root_out);
+    MKV_LAUNCH_CHECK();
+}
+
+}  // namespace mkv

@@ -1,0 +1,488 @@
+// k_sort.hip — Kernel C: leaf ordering (R3, merkle.rs:80-81) plus the scans / compactions / gathers
+// the build needs.
+//
+// Ordering is Rust String Ord on raw key bytes. It is reproduced bit-exactly as:
+//   1. stable LSD radix sort of (u64 big-endian 8-byte key prefix, input index), 8-bit digits;
+//   2. for runs of equal prefix only: segmented refinement by the next 8-byte chunk (and finally by key
+//      length), each round a stable chunk sort followed by a stable group-id sort (tree.cpp);
+// zero padding + length tie-break == shorter-prefix-first. Stability keeps equal keys in insertion
+// order so dedup keeps the last write (merkle.rs:54).
+//
+// Radix sort: tile = 4096 pairs per 256-thread workgroup (1024 per wave, 16 per lane, striped so each
+// wave-load is 64 consecutive pairs). Pass = per-tile 256-bin histogram -> exclusive scan of the
+// digit-major count matrix -> stable scatter, with in-wave ranks from 8 ballots (peer mask of lanes
+// with the same digit) and per-wave LDS digit counters.
+#include "common.hpp"
+#include "dev_util.hpp"
+#include "kernels.hpp"
+
+namespace mkv {
+
+namespace {
+
+constexpr int RS_THREADS = 256;
+constexpr int RS_IPT = 16;
+constexpr int RS_TILE = RS_THREADS * RS_IPT;
+constexpr int RS_WAVE_ITEMS = 64 * RS_IPT;
+
+constexpr int SC_THREADS = 256;
+constexpr int SC_IPT = 8;
+constexpr int SC_TILE = SC_THREADS * SC_IPT;
+
+__global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                 uint64_t n, uint64_t *__restrict__ pfx, uint32_t *__restrict__ idx) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t a = koff[i], b = koff[i + 1];
+    pfx[i] = key_chunk(kb + a, b - a, 0);
+    idx[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const uint64_t *__restrict__ keys, uint64_t n, int shift,
+                                                       uint32_t *__restrict__ counts, uint32_t nblocks) {
+    __shared__ uint32_t h[4][256];
+    for (int i = threadIdx.x; i < 1024; i += RS_THREADS) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + threadIdx.x;
+#pragma unroll
+    for (int s = 0; s < RS_IPT; ++s) {
+        uint64_t i = base + (uint64_t)s * RS_THREADS;
+        if (i < n) atomicAdd(&h[w][(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const uint32_t d = threadIdx.x;
+    counts[(uint64_t)d * nblocks + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+}
+
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const uint64_t *__restrict__ kin,
+                                                          const uint32_t *__restrict__ vin,
+                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                          uint64_t n, int shift, const uint32_t *__restrict__ offs,
+                                                          uint32_t nblocks) {
+    __shared__ uint32_t wcnt[4][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 1024; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WAVE_ITEMS + lane;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint64_t key[RS_IPT];
+    uint32_t val[RS_IPT];
+    uint32_t rk[RS_IPT];
+#pragma unroll
+    for (int s = 0; s < RS_IPT; ++s) {
+        const uint64_t i = base + (uint64_t)s * 64;
+        const bool ok = i < n;
+        key[s] = ok ? kin[i] : 0ull;
+        val[s] = ok ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (int s = 0; s < RS_IPT; ++s) {
+        const uint64_t i = base + (uint64_t)s * 64;
+        const bool ok = i < n;
+        const uint32_t d = (uint32_t)(key[s] >> shift) & 255u;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t before = wcnt[w][d];
+        const uint32_t r = (uint32_t)__popcll(peers & lt);
+        __builtin_amdgcn_wave_barrier();
+        if (ok && r == 0) wcnt[w][d] = before + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        rk[s] = before + r;
+    }
+    __syncthreads();
+    {
+        const uint32_t d = threadIdx.x;
+        uint32_t run = offs[(uint64_t)d * nblocks + blockIdx.x];
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            uint32_t c = wcnt[ww][d];
+            wcnt[ww][d] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < RS_IPT; ++s) {
+        const uint64_t i = base + (uint64_t)s * 64;
+        if (i < n) {
+            const uint32_t d = (uint32_t)(key[s] >> shift) & 255u;
+            const uint32_t pos = wcnt[w][d] + rk[s];
+            kout[pos] = key[s];
+            vout[pos] = val[s];
+        }
+    }
+}
+
+// ---- exclusive scan (reduce-then-scan) ----
+template <class T>
+__global__ __launch_bounds__(SC_THREADS) void k_scan_reduce(const T *__restrict__ in, uint64_t n,
+                                                           T *__restrict__ partial) {
+    __shared__ T lds[16];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_IPT;
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_IPT; ++j)
+        if (base + j < n) s += in[base + j];
+    T tot;
+    block_excl_scan<T>(s, lds, &tot);
+    if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+template <class T>
+__global__ __launch_bounds__(1024) void k_scan_partials(T *__restrict__ partial, uint64_t nb, T *__restrict__ total) {
+    __shared__ T lds[16];
+    T carry = 0;
+    for (uint64_t base = 0; base < nb; base += 1024) {
+        uint64_t i = base + threadIdx.x;
+        T x = i < nb ? partial[i] : T(0);
+        T tot;
+        T ex = block_excl_scan<T>(x, lds, &tot);
+        if (i < nb) partial[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+template <class T>
+__global__ __launch_bounds__(SC_THREADS) void k_scan_down(const T *in, T *out, uint64_t n,
+                                                         const T *__restrict__ partial) {
+    __shared__ T lds[16];
+    const uint64_t base = (uint64_t)blockIdx.x * SC_TILE + (uint64_t)threadIdx.x * SC_IPT;
+    T v[SC_IPT];
+    T s = 0;
+#pragma unroll
+    for (int j = 0; j < SC_IPT; ++j) {
+        v[j] = (base + j < n) ? in[base + j] : T(0);
+        s += v[j];
+    }
+    T ex = block_excl_scan<T>(s, lds, nullptr) + partial[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < SC_IPT; ++j) {
+        if (base + j < n) out[base + j] = ex;
+        ex += v[j];
+    }
+}
+
+template <class T> void scan_impl(const T *in, T *out, uint64_t n, T *total, void *scratch, hipStream_t st) {
+    uint64_t nb = ceil_div(n ? n : 1, SC_TILE);
+    T *partial = reinterpret_cast<T *>(scratch);
+    if (n == 0) {
+        if (total) MKV_HIP(hipMemsetAsync(total, 0, sizeof(T), st));
+        return;
+    }
+    hipLaunchKernelGGL(k_scan_reduce<T>, dim3((uint32_t)nb), dim3(SC_THREADS), 0, st, in, n, partial);
+    hipLaunchKernelGGL(k_scan_partials<T>, dim3(1), dim3(1024), 0, st, partial, nb, total);
+    hipLaunchKernelGGL(k_scan_down<T>, dim3((uint32_t)nb), dim3(SC_THREADS), 0, st, in, out, n, partial);
+    MKV_LAUNCH_CHECK();
+}
+
+// ---- ties / refinement ----
+__global__ void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, uint8_t *__restrict__ tie,
+                            uint32_t *__restrict__ count) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool t = false;
+    if (i < n) {
+        t = i > 0 && pfx[i] == pfx[i - 1];
+        tie[i] = t;
+    } else if (i == n) {
+        tie[n] = 0;
+    }
+    uint64_t m = __ballot(t);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (uint32_t)__popcll(m));
+}
+
+__global__ void k_active_flags(const uint8_t *__restrict__ tie, uint64_t n, uint32_t *__restrict__ flags) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[i] = (tie[i] | tie[i + 1]) ? 1u : 0u;
+}
+
+__global__ void k_compact_positions(const uint32_t *__restrict__ flags, const uint32_t *__restrict__ scan, uint64_t n,
+                                    uint32_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flags[i]) out[scan[i]] = (uint32_t)i;
+}
+
+__global__ void k_max_keylen(const uint32_t *__restrict__ pos, uint64_t m, const uint32_t *__restrict__ perm,
+                             const uint64_t *__restrict__ koff, uint32_t *__restrict__ out) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    uint32_t o = perm[pos[k]];
+    uint64_t len = koff[o + 1] - koff[o];
+    atomicMax(out, (uint32_t)(len > 0xFFFFFFFFull ? 0xFFFFFFFFull : len));
+}
+
+__global__ void k_refine_keys(const uint32_t *__restrict__ pos, uint64_t m, const uint32_t *__restrict__ perm,
+                              const uint8_t *__restrict__ tie, const uint8_t *__restrict__ kb,
+                              const uint64_t *__restrict__ koff, uint32_t depth, int use_len,
+                              uint64_t *__restrict__ chunk, uint32_t *__restrict__ kidx,
+                              uint32_t *__restrict__ perm_act, uint32_t *__restrict__ headflag) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    uint32_t p = pos[k];
+    uint32_t o = perm[p];
+    uint64_t a = koff[o], len = koff[o + 1] - a;
+    uint64_t c = use_len ? len : key_chunk(kb + a, len, 8ull * depth);
+    chunk[k] = c;            // sort key (overwritten by the sort)
+    chunk[m + k] = c;        // kept copy, indexed by k
+    kidx[k] = (uint32_t)k;
+    perm_act[k] = o;
+    headflag[k] = tie[p] ? 0u : 1u;
+}
+
+// key2[k'] = group id of element kidx[k'] = inclusive scan of head flags - 1
+__global__ void k_gid_keys(const uint32_t *__restrict__ kidx, const uint32_t *__restrict__ excl,
+                           const uint32_t *__restrict__ head, uint64_t m, uint64_t *__restrict__ key2) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    uint32_t e = kidx[k];
+    key2[k] = (uint64_t)(excl[e] + head[e] - 1u);
+}
+
+__global__ void k_refine_apply(const uint32_t *__restrict__ pos, uint64_t m, const uint32_t *__restrict__ sorted_k,
+                               const uint32_t *__restrict__ perm_act, const uint64_t *__restrict__ chunk_keep,
+                               uint32_t *__restrict__ perm, uint8_t *__restrict__ tie, uint32_t *__restrict__ count) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool t = false;
+    if (k < m) {
+        uint32_t p = pos[k];
+        uint32_t e = sorted_k[k];
+        perm[p] = perm_act[e];
+        // same group as the previous position (old tie) and equal on this round's chunk
+        t = tie[p] && k > 0 && chunk_keep[e] == chunk_keep[sorted_k[k - 1]];
+        tie[p] = t ? 1 : 0;
+    }
+    uint64_t bm = __ballot(t);
+    if ((threadIdx.x & 63) == 0 && bm) atomicAdd(count, (uint32_t)__popcll(bm));
+}
+
+__global__ void k_keep_flags(const uint8_t *__restrict__ tie, const uint32_t *__restrict__ perm, uint64_t n,
+                             uint64_t n_live, uint32_t *__restrict__ flags) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) flags[i] = (!tie[i + 1] && perm[i] < n_live) ? 1u : 0u;
+}
+
+__global__ void k_compact_u32(const uint32_t *__restrict__ src, const uint32_t *__restrict__ flags,
+                              const uint32_t *__restrict__ scan, uint64_t n, uint32_t *__restrict__ dst) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flags[i]) dst[scan[i]] = src[i];
+}
+
+// ---- gathers ----
+__global__ void k_gather_digests(const uint32_t *__restrict__ perm, const uint8_t *__restrict__ dig, uint64_t n,
+                                 uint8_t *__restrict__ out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 *s = reinterpret_cast<const uint4 *>(dig + 32ull * perm[i]);
+    uint4 *d = reinterpret_cast<uint4 *>(out + 32ull * i);
+    uint4 x = s[0], y = s[1];
+    d[0] = x;
+    d[1] = y;
+}
+
+__global__ void k_gather_keylens(const uint32_t *__restrict__ perm, const uint64_t *__restrict__ koff, uint64_t n,
+                                 uint64_t *__restrict__ lens) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t o = perm[i];
+    lens[i] = koff[o + 1] - koff[o];
+}
+
+__global__ void k_gather_keys(const uint32_t *__restrict__ perm, const uint8_t *__restrict__ kb,
+                              const uint64_t *__restrict__ koff, const uint64_t *__restrict__ koff_out, uint64_t n,
+                              uint8_t *__restrict__ kb_out) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t o = perm[i];
+    uint64_t a = koff[o], len = koff[o + 1] - a;
+    const uint8_t *s = kb + a;
+    uint8_t *d = kb_out + koff_out[i];
+    uintptr_t al = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d) | (uintptr_t)len;
+    if ((al & 15) == 0) {
+        for (uint64_t j = 0; j < len; j += 16)
+            *reinterpret_cast<uint4 *>(d + j) = *reinterpret_cast<const uint4 *>(s + j);
+    } else if ((al & 3) == 0) {
+        for (uint64_t j = 0; j < len; j += 4)
+            *reinterpret_cast<uint32_t *>(d + j) = *reinterpret_cast<const uint32_t *>(s + j);
+    } else {
+        for (uint64_t j = 0; j < len; ++j) d[j] = s[j];
+    }
+}
+
+__global__ void k_gather_u64(const uint32_t *__restrict__ perm, const uint64_t *__restrict__ src, uint64_t n,
+                             uint64_t *__restrict__ dst) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[perm[i]];
+}
+
+__global__ void k_gather_u32_to_u64(const uint32_t *__restrict__ src, const uint32_t *__restrict__ idx, uint64_t m,
+                                    uint64_t *__restrict__ dst) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) dst[i] = src[idx[i]];
+}
+
+__global__ void k_gather_u64_by_u32(const uint64_t *__restrict__ src, const uint32_t *__restrict__ idx, uint64_t m,
+                                    uint64_t *__restrict__ dst) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) dst[i] = src[idx[i]];
+}
+
+__global__ void k_add_offset_u64(const uint64_t *__restrict__ src, uint64_t n, uint64_t add,
+                                 uint64_t *__restrict__ dst) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i] + add;
+}
+
+__global__ void k_iota_u32(uint32_t *__restrict__ dst, uint64_t n) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = (uint32_t)i;
+}
+
+inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_div(n ? n : 1, bs)); }
+
+}  // namespace
+
+void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, uint32_t *idx,
+                     hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_prefix64, grid1d(n), dim3(256), 0, st, kb, koff, n, pfx, idx);
+    MKV_LAUNCH_CHECK();
+}
+
+size_t scan_scratch_bytes(uint64_t n) { return (ceil_div(n ? n : 1, SC_TILE) + 16) * sizeof(uint64_t); }
+
+size_t radix_scratch_bytes(uint64_t n) {
+    uint64_t nb = ceil_div(n ? n : 1, RS_TILE);
+    return 256 * nb * sizeof(uint32_t) + 256 + scan_scratch_bytes(256 * nb);
+}
+
+bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, int bit0, int bit1,
+                      void *scratch, hipStream_t st) {
+    if (n <= 1 || bit1 <= bit0) return false;
+    uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
+    uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
+    void *sc = reinterpret_cast<uint8_t *>(scratch) + ((256ull * nb * sizeof(uint32_t) + 255) & ~255ull);
+    uint64_t *ki = k, *ko = k2;
+    uint32_t *vi = v, *vo = v2;
+    bool swapped = false;
+    for (int shift = bit0; shift < bit1; shift += 8) {
+        hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_THREADS), 0, st, ki, n, shift, counts, nb);
+        scan_impl<uint32_t>(counts, counts, 256ull * nb, nullptr, sc, st);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, shift, counts, nb);
+        MKV_LAUNCH_CHECK();
+        std::swap(ki, ko);
+        std::swap(vi, vo);
+        swapped = !swapped;
+    }
+    return swapped;
+}
+
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *scratch,
+                        hipStream_t st) {
+    scan_impl<uint32_t>(in, out, n, total, scratch, st);
+}
+void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total, void *scratch,
+                        hipStream_t st) {
+    scan_impl<uint64_t>(in, out, n, total, scratch, st);
+}
+
+void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st) {
+    hipLaunchKernelGGL(k_mark_ties, grid1d(n + 1), dim3(256), 0, st, pfx, n, tie, count);
+    MKV_LAUNCH_CHECK();
+}
+void launch_active_flags(const uint8_t *tie, uint64_t n, uint32_t *flags, hipStream_t st) {
+    hipLaunchKernelGGL(k_active_flags, grid1d(n), dim3(256), 0, st, tie, n, flags);
+    MKV_LAUNCH_CHECK();
+}
+void launch_compact_positions(const uint32_t *flags, const uint32_t *scan, uint64_t n, uint32_t *out,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_compact_positions, grid1d(n), dim3(256), 0, st, flags, scan, n, out);
+    MKV_LAUNCH_CHECK();
+}
+void launch_max_keylen(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint64_t *koff, uint32_t *out,
+                       hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_max_keylen, grid1d(m), dim3(256), 0, st, pos, m, perm, koff, out);
+    MKV_LAUNCH_CHECK();
+}
+void launch_refine_keys(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *tie, const uint8_t *kb,
+                        const uint64_t *koff, uint32_t depth, int use_len, uint64_t *chunk, uint32_t *kidx,
+                        uint32_t *perm_act, uint32_t *headflag, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_refine_keys, grid1d(m), dim3(256), 0, st, pos, m, perm, tie, kb, koff, depth, use_len, chunk,
+                       kidx, perm_act, headflag);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gid_keys(const uint32_t *kidx, const uint32_t *excl, const uint32_t *head, uint64_t m, uint64_t *key2,
+                     hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_gid_keys, grid1d(m), dim3(256), 0, st, kidx, excl, head, m, key2);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gather_u64_by_u32(const uint64_t *src, const uint32_t *idx, uint64_t m, uint64_t *dst, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_gather_u64_by_u32, grid1d(m), dim3(256), 0, st, src, idx, m, dst);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gather_u32_to_u64(const uint32_t *src, const uint32_t *idx, uint64_t m, uint64_t *dst, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_gather_u32_to_u64, grid1d(m), dim3(256), 0, st, src, idx, m, dst);
+    MKV_LAUNCH_CHECK();
+}
+void launch_refine_apply(const uint32_t *pos, uint64_t m, const uint32_t *sorted_k, const uint32_t *perm_act,
+                         const uint64_t *chunk, uint32_t *perm, uint8_t *tie, uint32_t *count, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_refine_apply, grid1d(m), dim3(256), 0, st, pos, m, sorted_k, perm_act, chunk, perm, tie,
+                       count);
+    MKV_LAUNCH_CHECK();
+}
+void launch_keep_flags(const uint8_t *tie, const uint32_t *perm, uint64_t n, uint64_t n_live, uint32_t *flags,
+                       hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_keep_flags, grid1d(n), dim3(256), 0, st, tie, perm, n, n_live, flags);
+    MKV_LAUNCH_CHECK();
+}
+void launch_compact_u32(const uint32_t *src, const uint32_t *flags, const uint32_t *scan, uint64_t n, uint32_t *dst,
+                        hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_compact_u32, grid1d(n), dim3(256), 0, st, src, flags, scan, n, dst);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gather_digests(const uint32_t *perm, const uint8_t *dig_in, uint64_t n, uint8_t *out, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_gather_digests, grid1d(n), dim3(256), 0, st, perm, dig_in, n, out);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gather_keylens(const uint32_t *perm, const uint64_t *koff, uint64_t n, uint64_t *lens, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_gather_keylens, grid1d(n), dim3(256), 0, st, perm, koff, n, lens);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gather_keys(const uint32_t *perm, const uint8_t *kb, const uint64_t *koff, const uint64_t *koff_out,
+                        uint64_t n, uint8_t *kb_out, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_gather_keys, grid1d(n), dim3(256), 0, st, perm, kb, koff, koff_out, n, kb_out);
+    MKV_LAUNCH_CHECK();
+}
+void launch_gather_u64(const uint32_t *perm, const uint64_t *src, uint64_t n, uint64_t *dst, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_gather_u64, grid1d(n), dim3(256), 0, st, perm, src, n, dst);
+    MKV_LAUNCH_CHECK();
+}
+void launch_add_offset_u64(const uint64_t *src, uint64_t n, uint64_t add, uint64_t *dst, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_add_offset_u64, grid1d(n), dim3(256), 0, st, src, n, add, dst);
+    MKV_LAUNCH_CHECK();
+}
+void launch_iota_u32(uint32_t *dst, uint64_t n, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_iota_u32, grid1d(n), dim3(256), 0, st, dst, n);
+    MKV_LAUNCH_CHECK();
+}
+
+}  // namespace mkv

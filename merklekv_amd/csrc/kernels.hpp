@@ -1,0 +1,109 @@
+// kernels.hpp — internal launcher API between the C-ABI runtime (tree.cpp) and the HIP kernels.
+// All launchers are asynchronous on `st`; none allocates or synchronises.
+#pragma once
+#include "common.hpp"
+
+namespace mkv {
+
+// ---- Kernel A: leaf hashing (k_leaf.hip) ----
+void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                      uint8_t *out_digests, hipStream_t st);
+
+// ---- Kernel C: ordering (k_sort.hip) ----
+// pfx[i] = big-endian first 8 key bytes, zero padded (key i of kb/koff); idx[i] = i
+void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, uint32_t *idx,
+                     hipStream_t st);
+// Scratch bytes needed by radix_sort_pairs / scans for n elements.
+size_t radix_scratch_bytes(uint64_t n);
+size_t scan_scratch_bytes(uint64_t n);
+// Stable LSD radix sort of (key, val) pairs on key bits [bit0, bit1). Ping-pongs between (k, v) and
+// (k2, v2); returns true if the result ended in (k2, v2).
+bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, int bit0, int bit1,
+                      void *scratch, hipStream_t st);
+// Exclusive scans (out may alias in). total (device, may be null) receives the sum.
+void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *total, void *scratch,
+                        hipStream_t st);
+void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total, void *scratch,
+                        hipStream_t st);
+
+// tie[i] = (pfx[i] == pfx[i-1]) for i>0, tie[0] = 0; *count += number of ties. tie has n+1 entries
+// (tie[n] = 0 sentinel).
+void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st);
+// Refinement helpers (see tree.cpp refine_ties for the algorithm).
+void launch_active_flags(const uint8_t *tie, uint64_t n, uint32_t *flags, hipStream_t st);
+void launch_compact_positions(const uint32_t *flags, const uint32_t *scan, uint64_t n, uint32_t *out, hipStream_t st);
+void launch_max_keylen(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint64_t *koff, uint32_t *out,
+                       hipStream_t st);
+void launch_refine_keys(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *tie, const uint8_t *kb,
+                        const uint64_t *koff, uint32_t depth, int use_len, uint64_t *chunk, uint32_t *kidx,
+                        uint32_t *perm_act, uint32_t *headflag, hipStream_t st);
+void launch_gid_keys(const uint32_t *kidx, const uint32_t *excl, const uint32_t *head, uint64_t m, uint64_t *key2,
+                     hipStream_t st);
+void launch_gather_u64_by_u32(const uint64_t *src, const uint32_t *idx, uint64_t m, uint64_t *dst, hipStream_t st);
+void launch_gather_u32_to_u64(const uint32_t *src, const uint32_t *idx, uint64_t m, uint64_t *dst, hipStream_t st);
+void launch_refine_apply(const uint32_t *pos, uint64_t m, const uint32_t *sorted_k, const uint32_t *perm_act,
+                         const uint64_t *chunk, uint32_t *perm, uint8_t *tie, uint32_t *count, hipStream_t st);
+// keep[i] = !tie[i+1] && perm[i] < n_live
+void launch_keep_flags(const uint8_t *tie, const uint32_t *perm, uint64_t n, uint64_t n_live, uint32_t *flags,
+                       hipStream_t st);
+void launch_compact_u32(const uint32_t *src, const uint32_t *flags, const uint32_t *scan, uint64_t n, uint32_t *dst,
+                        hipStream_t st);
+
+// ---- gathers into sorted order ----
+void launch_gather_digests(const uint32_t *perm, const uint8_t *dig_in, uint64_t n, uint8_t *out, hipStream_t st);
+void launch_gather_keylens(const uint32_t *perm, const uint64_t *koff, uint64_t n, uint64_t *lens, hipStream_t st);
+void launch_gather_keys(const uint32_t *perm, const uint8_t *kb, const uint64_t *koff, const uint64_t *koff_out,
+                        uint64_t n, uint8_t *kb_out, hipStream_t st);
+void launch_gather_u64(const uint32_t *perm, const uint64_t *src, uint64_t n, uint64_t *dst, hipStream_t st);
+void launch_add_offset_u64(const uint64_t *src, uint64_t n, uint64_t add, uint64_t *dst, hipStream_t st);
+void launch_iota_u32(uint32_t *dst, uint64_t n, hipStream_t st);
+
+// ---- Kernel B: level reduction (k_reduce.hip) ----
+// One fused launch produces up to MAX_FUSE levels. Level k (1-based within the launch) owns global
+// node indices [a[k], a[k]+c[k]); S[k-1] is the global size of its child level.
+constexpr int MAX_FUSE = 10;
+struct FusePlan {
+    const uint8_t *in;       // child level (local array; global index of in[0] is a[0])
+    uint8_t *out[MAX_FUSE];  // out[k-1] = level k's local array
+    uint64_t a[MAX_FUSE + 1];
+    uint64_t c[MAX_FUSE + 1];
+    uint64_t S[MAX_FUSE + 1];
+    int nl;
+    uint64_t tile0;  // first tile index (global, in units of 512 first-level parents)
+    uint64_t ntiles;
+};
+void launch_reduce_fused(const FusePlan &p, hipStream_t st);
+
+// Seam combine for sharded trees (k_reduce.hip). entries: (level, index, digest) records sorted by
+// (level, index); see tree.cpp. Writes the root.
+void launch_seam_combine(const uint8_t *entries, uint32_t nent, const uint64_t *level_sizes, uint32_t nlevels,
+                         uint8_t *scratch, uint8_t *root_out, hipStream_t st);
+
+// ---- Kernel D: diff (k_diff.hip) ----
+struct DiffSide {
+    const uint8_t *kb;
+    const uint64_t *koff;
+    const uint64_t *pfx;
+    const uint8_t *dig;
+    uint64_t n;
+};
+constexpr int DIFF_ITEMS = 8;     // merged outputs per thread
+constexpr int DIFF_THREADS = 256;
+size_t diff_scratch_bytes(uint64_t nmerged);
+// Pass 1 + scan + pass 2: writes refs (bit 63 = side B, low bits = sorted index) of the divergent keys
+// in sorted order; *count (device) receives the number. Returns nothing; host reads count.
+void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
+                 hipStream_t st);
+void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
+                         hipStream_t st);
+void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,
+                      uint8_t *out, hipStream_t st);
+// Prefix range [lo, hi) of sorted keys starting with prefix (single-thread binary search).
+void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t plen, uint64_t *lohi, hipStream_t st);
+
+// ---- synthetic generator (k_gen.hip) — bench/test utility, not part of the reference API ----
+void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
+                        uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb, uint64_t *voff,
+                        hipStream_t st);
+
+}  // namespace mkv

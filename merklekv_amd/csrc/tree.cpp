@@ -1,0 +1,1015 @@
+// tree.cpp — native runtime behind include/mkv_merkle.h: device memory, stream, build / upsert / remove /
+// diff orchestration over the HIP kernels, sharded-tree seams, profiling. No CPU compute fallback: every
+// digest, sort, reduction and diff runs on the GPU; the host only plans launches and moves results.
+#include "mkv_merkle.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+using namespace mkv;
+
+static thread_local std::string g_err;
+
+namespace {
+
+struct EvPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    std::string group;
+};
+
+}  // namespace
+
+struct mkv_keylist {
+    std::vector<uint8_t> bytes;
+    std::vector<uint64_t> offsets;  // n+1
+};
+
+struct mkv_tree {
+    int dev = 0;
+    hipStream_t st = nullptr;
+
+    // ---- contents (device) ----
+    uint64_t n = 0;       // local leaves
+    uint64_t kbytes = 0;  // bytes of sorted keys
+    DevBuf kb, koff, pfx, nodes;
+    std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
+    bool has_root = false;
+    uint8_t root[32] = {0};
+    // shard state
+    uint64_t goff = 0, gN = 0;
+    bool sharded = false;
+    bool prepared = false;  // shard_prepare done, reduce pending
+
+    // ---- scratch (device) ----
+    DevBuf s_kb, s_koff, s_vb, s_voff, s_dig, s_tomb;
+    DevBuf s_k1, s_k2, s_v1, s_v2;
+    DevBuf s_tie, s_flags, s_scan, s_pos, s_lens;
+    DevBuf s_radix, s_misc;
+    DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
+    DevBuf s_nodes2;  // prefix-root scratch levels
+    DevBuf d_refs, d_diffscr, d_out, d_outoff;
+    DevBuf d_seam, d_S, d_fr;
+    uint64_t *h_small = nullptr;  // pinned host scalars
+
+    // ---- profiling ----
+    bool prof = false;
+    std::vector<EvPair> evpool;
+    size_t evused = 0;
+    std::map<std::string, std::pair<double, uint64_t>> pg;
+
+    // the device pointers of the current staged build input
+    const uint8_t *in_kb = nullptr;
+    const uint64_t *in_koff = nullptr;
+    uint64_t in_n = 0;
+    const uint8_t *in_tomb = nullptr;
+};
+
+namespace {
+
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(int d) {
+        (void)hipGetDevice(&prev);
+        MKV_HIP(hipSetDevice(d));
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+__global__ void k_clear_tomb(const uint8_t *__restrict__ tomb, const uint32_t *__restrict__ perm, uint64_t n,
+                             uint32_t *__restrict__ flags) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && tomb[perm[i]]) flags[i] = 0;
+}
+void launch_clear_tomb(const uint8_t *tomb, const uint32_t *perm, uint64_t n, uint32_t *flags, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_clear_tomb, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, tomb, perm, n, flags);
+    MKV_LAUNCH_CHECK();
+}
+
+size_t prof_begin(mkv_tree *t, const char *group) {
+    if (!t->prof) return SIZE_MAX;
+    if (t->evused == t->evpool.size()) {
+        EvPair p;
+        MKV_HIP(hipEventCreate(&p.a));
+        MKV_HIP(hipEventCreate(&p.b));
+        t->evpool.push_back(p);
+    }
+    size_t i = t->evused++;
+    t->evpool[i].group = group;
+    MKV_HIP(hipEventRecord(t->evpool[i].a, t->st));
+    return i;
+}
+void prof_end(mkv_tree *t, size_t i) {
+    if (i == SIZE_MAX) return;
+    MKV_HIP(hipEventRecord(t->evpool[i].b, t->st));
+}
+// after a stream sync
+void prof_collect(mkv_tree *t) {
+    if (!t->prof) return;
+    for (size_t i = 0; i < t->evused; ++i) {
+        float ms = 0;
+        MKV_HIP(hipEventElapsedTime(&ms, t->evpool[i].a, t->evpool[i].b));
+        auto &g = t->pg[t->evpool[i].group];
+        g.first += ms;
+        g.second += 1;
+    }
+    t->evused = 0;
+}
+
+void sync(mkv_tree *t) {
+    MKV_HIP(hipStreamSynchronize(t->st));
+    prof_collect(t);
+}
+
+template <class T> T *ens(DevBuf &b, uint64_t count) { return reinterpret_cast<T *>(b.ensure(count * sizeof(T))); }
+
+uint64_t d2h_u64(mkv_tree *t, const void *dptr) {
+    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint64_t), hipMemcpyDeviceToHost, t->st));
+    sync(t);
+    return t->h_small[0];
+}
+uint32_t d2h_u32(mkv_tree *t, const void *dptr) {
+    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint32_t), hipMemcpyDeviceToHost, t->st));
+    sync(t);
+    return reinterpret_cast<uint32_t *>(t->h_small)[0];
+}
+
+int bits_for(uint64_t m) {
+    int b = 0;
+    while (b < 64 && (m >> b)) ++b;
+    return b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Level plan (R5 ownership): level k owns global nodes [a_k, a_k + c_k) of a level with S_k nodes.
+// ---------------------------------------------------------------------------------------------
+void plan_levels(mkv_tree *t, uint64_t o, uint64_t n, uint64_t N) {
+    t->lev_cnt.clear();
+    t->lev_off.clear();
+    t->lev_base.clear();
+    t->lev_S.clear();
+    if (N == 0) return;
+    uint64_t a = o, e = o + n, S = N, off = 0;
+    while (true) {
+        uint64_t c = e > a ? e - a : 0;
+        t->lev_base.push_back(a);
+        t->lev_cnt.push_back(c);
+        t->lev_off.push_back(off);
+        t->lev_S.push_back(S);
+        off += c;
+        if (S == 1) break;
+        uint64_t a2 = (a + 1) / 2;
+        uint64_t e2 = (e == S) ? (e + 1) / 2 : e / 2;
+        a = a2;
+        e = e2;
+        S = (S + 1) / 2;
+    }
+}
+
+uint64_t total_nodes(const mkv_tree *t) {
+    uint64_t s = 0;
+    for (auto c : t->lev_cnt) s += c;
+    return s;
+}
+
+void run_reduce(mkv_tree *t, uint8_t *nodes) {
+    const size_t L = t->lev_S.size();
+    size_t l = 0;
+    while (l + 1 < L && t->lev_cnt[l] > 0) {
+        if (t->lev_cnt[l + 1] == 0) break;
+        const uint64_t a1 = t->lev_base[l + 1], c1 = t->lev_cnt[l + 1];
+        const uint64_t t0 = a1 / 512, t1 = (a1 + c1 - 1) / 512;
+        const uint64_t ntiles = t1 - t0 + 1;
+        const size_t remaining = L - 1 - l;
+        const size_t nl = std::min<size_t>(remaining, ntiles == 1 ? MAX_FUSE : 4);
+        FusePlan p{};
+        p.in = nodes + 32 * t->lev_off[l];
+        p.a[0] = t->lev_base[l];
+        p.c[0] = t->lev_cnt[l];
+        p.S[0] = t->lev_S[l];
+        for (size_t k = 1; k <= nl; ++k) {
+            p.out[k - 1] = nodes + 32 * t->lev_off[l + k];
+            p.a[k] = t->lev_base[l + k];
+            p.c[k] = t->lev_cnt[l + k];
+            p.S[k] = t->lev_S[l + k];
+        }
+        p.nl = (int)nl;
+        p.tile0 = t0;
+        p.ntiles = ntiles;
+        launch_reduce_fused(p, t->st);
+        l += nl;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Tie refinement (R3 on full keys): see k_sort.hip header. perm: sorted order (u32 input indices),
+// tie[i] = position i equals position i-1 on everything compared so far.
+// ---------------------------------------------------------------------------------------------
+void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint8_t *tie) {
+    hipStream_t st = t->st;
+    uint32_t *flags = ens<uint32_t>(t->s_flags, n + 1);
+    uint32_t *scan = ens<uint32_t>(t->s_scan, n + 1);
+    uint32_t *pos = ens<uint32_t>(t->s_pos, n + 1);
+    uint32_t *misc = ens<uint32_t>(t->s_misc, 64);
+    void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n), scan_scratch_bytes(n)));
+
+    auto active = [&]() -> uint64_t {
+        launch_active_flags(tie, n, flags, st);
+        exclusive_scan_u32(flags, scan, n, misc, radix, st);
+        launch_compact_positions(flags, scan, n, pos, st);
+        return d2h_u32(t, misc);
+    };
+    uint64_t m = active();
+    if (m == 0) return;
+    MKV_HIP(hipMemsetAsync(misc + 1, 0, 4, st));
+    launch_max_keylen(pos, m, perm, koff, misc + 1, st);
+    const uint32_t maxlen = d2h_u32(t, misc + 1);
+    const uint32_t D = (maxlen + 7) / 8;  // chunks; chunk 0 already sorted
+
+    for (uint32_t depth = 1;; ++depth) {
+        const int use_len = depth >= D;
+        if (depth > 1) {
+            m = active();
+            if (m == 0) break;
+        }
+        uint64_t *chunk = ens<uint64_t>(t->r_chunk, 2 * m);
+        uint64_t *chunk2 = ens<uint64_t>(t->r_chunk2, m);
+        uint32_t *kidx = ens<uint32_t>(t->r_kidx, m);
+        uint32_t *kidx2 = ens<uint32_t>(t->r_kidx2, m);
+        uint32_t *permact = ens<uint32_t>(t->r_permact, m);
+        uint32_t *head = ens<uint32_t>(t->r_head, m);
+        uint32_t *gexcl = ens<uint32_t>(t->r_gexcl, m);
+        uint64_t *key2 = ens<uint64_t>(t->r_key2, m);
+        uint64_t *key22 = ens<uint64_t>(t->r_key22, m);
+        launch_refine_keys(pos, m, perm, tie, kb, koff, depth, use_len, chunk, kidx, permact, head, st);
+        exclusive_scan_u32(head, gexcl, m, nullptr, radix, st);
+        // 1) stable sort by this round's chunk
+        const int cbits = use_len ? 64 : 64;
+        bool sw = radix_sort_pairs(chunk, kidx, chunk2, kidx2, m, 0, cbits, radix, st);
+        uint32_t *kk = sw ? kidx2 : kidx;
+        uint32_t *kk_alt = sw ? kidx : kidx2;
+        // 2) stable sort by group id (restores group blocks in position order)
+        launch_gid_keys(kk, gexcl, head, m, key2, st);
+        bool sw2 = radix_sort_pairs(key2, kk, key22, kk_alt, m, 0, std::max(8, bits_for(m)), radix, st);
+        uint32_t *kks = sw2 ? kk_alt : kk;
+        MKV_HIP(hipMemsetAsync(misc + 2, 0, 4, st));
+        launch_refine_apply(pos, m, kks, permact, chunk + m, perm, tie, misc + 2, st);
+        const uint32_t left = d2h_u32(t, misc + 2);
+        if (left == 0 || use_len) break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Core build over staged input records: keys (kb/koff, n_in), digests (s_dig, n_in), optional tombstones.
+// Produces sorted unique keys (last write wins), leaf level, and the level plan for [o, o+n) of N
+// (N == UINT64_MAX: unsharded, N = n).
+// ---------------------------------------------------------------------------------------------
+void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb) {
+    hipStream_t st = t->st;
+    const uint8_t *dig = t->s_dig.as<uint8_t>();
+    uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
+    uint64_t *k2 = ens<uint64_t>(t->s_k2, n_in + 1);
+    uint32_t *v1 = ens<uint32_t>(t->s_v1, n_in + 1);
+    uint32_t *v2 = ens<uint32_t>(t->s_v2, n_in + 1);
+    uint8_t *tie = ens<uint8_t>(t->s_tie, n_in + 2);
+    uint32_t *misc = ens<uint32_t>(t->s_misc, 64);
+    void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n_in), scan_scratch_bytes(n_in + 1)));
+
+    size_t ps = prof_begin(t, "sort");
+    launch_prefix64(kb, koff, n_in, k1, v1, st);
+    const bool sw = radix_sort_pairs(k1, v1, k2, v2, n_in, 0, 64, radix, st);
+    uint64_t *pk = sw ? k2 : k1;
+    uint32_t *perm = sw ? v2 : v1;
+    uint32_t *perm_alt = sw ? v1 : v2;
+    MKV_HIP(hipMemsetAsync(misc, 0, 4, st));
+    launch_mark_ties(pk, n_in, tie, misc, st);
+    prof_end(t, ps);
+    const uint32_t nties = n_in ? d2h_u32(t, misc) : 0;
+    if (nties) {
+        size_t pr = prof_begin(t, "sort");
+        refine_ties(t, kb, koff, n_in, perm, tie);
+        prof_end(t, pr);
+    }
+    uint64_t n = n_in;
+    if (nties || tomb) {
+        size_t pd = prof_begin(t, "sort");
+        uint32_t *flags = ens<uint32_t>(t->s_flags, n_in + 1);
+        uint32_t *scan = ens<uint32_t>(t->s_scan, n_in + 1);
+        launch_keep_flags(tie, perm, n_in, UINT64_MAX, flags, st);
+        if (tomb) launch_clear_tomb(tomb, perm, n_in, flags, st);  // removed keys never survive
+        exclusive_scan_u32(flags, scan, n_in, misc + 3, radix, st);
+        launch_compact_u32(perm, flags, scan, n_in, perm_alt, st);
+        prof_end(t, pd);
+        n = d2h_u32(t, misc + 3);
+        perm = perm_alt;
+    }
+    t->n = n;
+    // ---- gather into sorted order ----
+    size_t pg = prof_begin(t, "gather");
+    uint64_t *lens = ens<uint64_t>(t->s_lens, n + 1);
+    uint64_t *koff_out = ens<uint64_t>(t->koff, n + 1);
+    launch_gather_keylens(perm, koff, n, lens, st);
+    exclusive_scan_u64(lens, koff_out, n, koff_out + n, radix, st);
+    prof_end(t, pg);
+    t->kbytes = n ? d2h_u64(t, koff_out + n) : 0;
+    if (!n) MKV_HIP(hipMemsetAsync(koff_out, 0, sizeof(uint64_t), st));
+    pg = prof_begin(t, "gather");
+    uint8_t *kb_out = ens<uint8_t>(t->kb, t->kbytes + 16);
+    launch_gather_keys(perm, kb, koff, koff_out, n, kb_out, st);
+    uint64_t *pfx = ens<uint64_t>(t->pfx, n + 1);
+    launch_prefix64(kb_out, koff_out, n, pfx, v1 == perm ? v2 : v1, st);
+    prof_end(t, pg);
+    pg = prof_begin(t, "gather");
+    // leaf level = nodes[0 .. n); nodes is sized for every level of an unsharded tree (2n-1 nodes)
+    uint8_t *nodes = ens<uint8_t>(t->nodes, 2 * 32 * (n ? n : 1) + 64);
+    launch_gather_digests(perm, dig, n, nodes, st);
+    prof_end(t, pg);
+}
+
+void finish_unsharded(mkv_tree *t) {
+    t->sharded = false;
+    t->goff = 0;
+    t->gN = t->n;
+    plan_levels(t, 0, t->n, t->n);
+    size_t pr = prof_begin(t, "reduce");
+    run_reduce(t, t->nodes.as<uint8_t>());
+    prof_end(t, pr);
+    t->has_root = t->n > 0;
+    if (t->has_root) {
+        const size_t L = t->lev_S.size();
+        MKV_HIP(hipMemcpyAsync(t->root, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32, hipMemcpyDeviceToHost,
+                               t->st));
+    }
+    sync(t);
+}
+
+// Upload a host blob into (bytes, offsets) device buffers with offsets rebased to 0.
+void upload_blob(mkv_tree *t, const mkv_blob &b, DevBuf &bytes, DevBuf &offs, uint64_t dst_first = 0,
+                 uint64_t dst_index = 0, uint64_t byte_base = 0) {
+    const uint64_t n = b.n;
+    const uint64_t o0 = n ? b.offsets[0] : 0;
+    const uint64_t nbytes = n ? b.offsets[n] - o0 : 0;
+    (void)dst_first;
+    if (nbytes) MKV_HIP(hipMemcpyAsync(bytes.as<uint8_t>() + byte_base, b.bytes + o0, nbytes, hipMemcpyHostToDevice, t->st));
+    std::vector<uint64_t> tmp(n + 1);
+    for (uint64_t i = 0; i <= n; ++i) tmp[i] = (n ? b.offsets[i] - o0 : 0) + byte_base;
+    MKV_HIP(hipMemcpyAsync(offs.as<uint64_t>() + dst_index, tmp.data(), (n + 1) * sizeof(uint64_t),
+                           hipMemcpyHostToDevice, t->st));
+    MKV_HIP(hipStreamSynchronize(t->st));  // tmp goes out of scope
+}
+
+void check_blob(const mkv_blob &b, const char *what) {
+    if (b.n && (!b.offsets)) throw Error(ST_EINVAL, std::string(what) + ": null offsets");
+    if (b.n >= 0xFFFFFFF0ull) throw Error(ST_EINVAL, std::string(what) + ": too many records (max 2^32-16)");
+    if (b.n && b.offsets[b.n] > b.offsets[0] && !b.bytes) throw Error(ST_EINVAL, std::string(what) + ": null bytes");
+    for (uint64_t i = 0; i < b.n; ++i)
+        if (b.offsets[i + 1] < b.offsets[i]) throw Error(ST_EINVAL, std::string(what) + ": offsets not monotone");
+}
+
+// Stage [existing leaves ++ batch] for upsert / remove / apply. Returns staged record count.
+// Existing records carry their leaf digests; batch records are hashed on the device.
+uint64_t stage_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
+    if (t->sharded) throw Error(ST_ESTATE, "upsert/remove on a sharded tree is not supported");
+    const uint64_t m = t->n, nb = keys.n, tot = m + nb;
+    const uint64_t kb_new = nb ? keys.offsets[nb] - keys.offsets[0] : 0;
+    uint8_t *skb = ens<uint8_t>(t->s_kb, t->kbytes + kb_new + 16);
+    uint64_t *skoff = ens<uint64_t>(t->s_koff, tot + 1);
+    uint8_t *sdig = ens<uint8_t>(t->s_dig, (tot ? tot : 1) * 32);
+    if (t->kbytes) MKV_HIP(hipMemcpyAsync(skb, t->kb.p, t->kbytes, hipMemcpyDeviceToDevice, t->st));
+    if (m) {
+        MKV_HIP(hipMemcpyAsync(skoff, t->koff.p, m * sizeof(uint64_t), hipMemcpyDeviceToDevice, t->st));
+        MKV_HIP(hipMemcpyAsync(sdig, t->nodes.p, m * 32, hipMemcpyDeviceToDevice, t->st));
+    }
+    upload_blob(t, keys, t->s_kb, t->s_koff, 0, m, t->kbytes);
+    if (values && nb) {
+        const uint64_t vbytes = values->offsets[nb] - values->offsets[0];
+        ens<uint8_t>(t->s_vb, vbytes + 16);
+        ens<uint64_t>(t->s_voff, nb + 1);
+        upload_blob(t, *values, t->s_vb, t->s_voff);
+        size_t pl = prof_begin(t, "leaf_hash");
+        launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>() + m, t->s_vb.as<uint8_t>(),
+                         t->s_voff.as<uint64_t>(), nb, sdig + 32 * m, t->st);
+        prof_end(t, pl);
+    }
+    t->in_tomb = nullptr;
+    if (is_remove) {
+        uint8_t *tomb = ens<uint8_t>(t->s_tomb, tot + 1);
+        MKV_HIP(hipMemsetAsync(tomb, 0, tot, t->st));
+        if (nb) MKV_HIP(hipMemcpyAsync(tomb + m, is_remove, nb, hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipStreamSynchronize(t->st));
+        t->in_tomb = tomb;
+    }
+    return tot;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+#define MKV_TRY(...)                                                                                 \
+    try {                                                                                            \
+        __VA_ARGS__;                                                                                 \
+        return MKV_OK;                                                                               \
+    } catch (const Error &e) {                                                                       \
+        g_err = e.what();                                                                            \
+        return e.code;                                                                               \
+    } catch (const std::bad_alloc &) {                                                               \
+        g_err = "host allocation failed";                                                            \
+        return MKV_ENOMEM;                                                                           \
+    } catch (const std::exception &e) {                                                              \
+        g_err = e.what();                                                                            \
+        return MKV_EINVAL;                                                                           \
+    }
+
+#define NEED(cond, msg) \
+    if (!(cond)) throw Error(ST_EINVAL, msg)
+
+extern "C" {
+
+const char *mkv_last_error(void) { return g_err.c_str(); }
+const char *mkv_version(void) { return "merklekv_amd 0.1 (gfx950)"; }
+
+mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
+    MKV_TRY({
+        NEED(out, "out is null");
+        *out = nullptr;
+        int ndev = 0;
+        hipError_t e = hipGetDeviceCount(&ndev);
+        if (e != hipSuccess || ndev == 0) throw Error(ST_EHIP, "no HIP device available (MI355X required)");
+        NEED(hip_device >= 0 && hip_device < ndev, "bad device index");
+        DevGuard g(hip_device);
+        mkv_tree *t = new mkv_tree();
+        t->dev = hip_device;
+        hipError_t e2 = hipStreamCreateWithFlags(&t->st, hipStreamNonBlocking);
+        if (e2 != hipSuccess) {
+            delete t;
+            throw Error(ST_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e2));
+        }
+        e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 256, hipHostMallocDefault);
+        if (e2 != hipSuccess) {
+            (void)hipStreamDestroy(t->st);
+            delete t;
+            throw Error(ST_EHIP, std::string("hipHostMalloc: ") + hipGetErrorString(e2));
+        }
+        *out = t;
+    });
+}
+
+void mkv_tree_destroy(mkv_tree *t) {
+    if (!t) return;
+    (void)hipSetDevice(t->dev);
+    (void)hipStreamSynchronize(t->st);
+    for (auto &p : t->evpool) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    if (t->h_small) (void)hipHostFree(t->h_small);
+    (void)hipStreamDestroy(t->st);
+    delete t;
+}
+
+mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
+    MKV_TRY({
+        NEED(src && dst, "null argument");
+        NEED(src->dev == dst->dev, "clone across devices");
+        NEED(!src->prepared, "shard_reduce pending");
+        if (src == dst) return MKV_OK;
+        DevGuard g(src->dev);
+        MKV_HIP(hipStreamSynchronize(src->st));
+        const uint64_t nn = total_nodes(src);
+        uint8_t *kb = ens<uint8_t>(dst->kb, src->kbytes + 16);
+        uint64_t *ko = ens<uint64_t>(dst->koff, src->n + 1);
+        uint64_t *pf = ens<uint64_t>(dst->pfx, src->n + 1);
+        uint8_t *nd = ens<uint8_t>(dst->nodes, std::max<uint64_t>(nn, 2 * src->n) * 32 + 64);
+        if (src->kbytes) MKV_HIP(hipMemcpyAsync(kb, src->kb.p, src->kbytes, hipMemcpyDeviceToDevice, dst->st));
+        MKV_HIP(hipMemcpyAsync(ko, src->koff.p ? src->koff.p : ko, (src->koff.p ? (src->n + 1) : 0) * 8,
+                               hipMemcpyDeviceToDevice, dst->st));
+        if (src->n) {
+            MKV_HIP(hipMemcpyAsync(pf, src->pfx.p, src->n * 8, hipMemcpyDeviceToDevice, dst->st));
+            MKV_HIP(hipMemcpyAsync(nd, src->nodes.p, nn * 32, hipMemcpyDeviceToDevice, dst->st));
+        }
+        MKV_HIP(hipStreamSynchronize(dst->st));
+        dst->n = src->n;
+        dst->kbytes = src->kbytes;
+        dst->lev_cnt = src->lev_cnt;
+        dst->lev_off = src->lev_off;
+        dst->lev_base = src->lev_base;
+        dst->lev_S = src->lev_S;
+        dst->has_root = src->has_root;
+        std::memcpy(dst->root, src->root, 32);
+        dst->goff = src->goff;
+        dst->gN = src->gN;
+        dst->sharded = src->sharded;
+        dst->prepared = false;
+    });
+}
+
+static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
+                              const uint64_t *voff, uint64_t n) {
+    size_t ptot = prof_begin(t, "total_build");
+    uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+    size_t pl = prof_begin(t, "leaf_hash");
+    launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
+    prof_end(t, pl);
+    sort_dedup_gather(t, kb, koff, n, nullptr);
+    finish_unsharded(t);
+    prof_end(t, ptot);
+    sync(t);
+}
+
+mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        check_blob(keys, "keys");
+        check_blob(values, "values");
+        DevGuard g(t->dev);
+        const uint64_t n = keys.n;
+        const uint64_t kbn = n ? keys.offsets[n] - keys.offsets[0] : 0;
+        const uint64_t vbn = n ? values.offsets[n] - values.offsets[0] : 0;
+        ens<uint8_t>(t->s_kb, kbn + 16);
+        ens<uint64_t>(t->s_koff, n + 1);
+        ens<uint8_t>(t->s_vb, vbn + 16);
+        ens<uint64_t>(t->s_voff, n + 1);
+        upload_blob(t, keys, t->s_kb, t->s_koff);
+        upload_blob(t, values, t->s_vb, t->s_voff);
+        build_from_staged(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), t->s_vb.as<uint8_t>(),
+                          t->s_voff.as<uint64_t>(), n);
+    });
+}
+
+mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        NEED(keys.n < 0xFFFFFFF0ull, "too many records");
+        NEED(keys.n == 0 || (keys.offsets && values.offsets), "null offsets");
+        DevGuard g(t->dev);
+        build_from_staged(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n);
+    });
+}
+
+static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
+    size_t ptot = prof_begin(t, "total_build");
+    const uint64_t tot = stage_batch(t, keys, values, is_remove);
+    sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb);
+    finish_unsharded(t);
+    prof_end(t, ptot);
+    sync(t);
+}
+
+mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        check_blob(keys, "keys");
+        check_blob(values, "values");
+        DevGuard g(t->dev);
+        if (keys.n == 0) return MKV_OK;
+        apply_batch(t, keys, &values, nullptr);
+    });
+}
+
+mkv_status mkv_tree_remove(mkv_tree *t, mkv_blob keys) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        check_blob(keys, "keys");
+        DevGuard g(t->dev);
+        if (keys.n == 0 || t->n == 0) return MKV_OK;
+        std::vector<uint8_t> rm(keys.n, 1);
+        apply_batch(t, keys, nullptr, rm.data());
+    });
+}
+
+mkv_status mkv_tree_apply(mkv_tree *t, mkv_blob keys, mkv_blob values, const uint8_t *is_remove) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        NEED(is_remove || keys.n == 0, "is_remove is null");
+        check_blob(keys, "keys");
+        check_blob(values, "values");
+        DevGuard g(t->dev);
+        if (keys.n == 0) return MKV_OK;
+        bool any = false;
+        for (uint64_t i = 0; i < keys.n; ++i) any |= is_remove[i] != 0;
+        apply_batch(t, keys, &values, any ? is_remove : nullptr);
+    });
+}
+
+mkv_status mkv_tree_root(const mkv_tree *t, uint8_t out32[32], int *has_root) {
+    MKV_TRY({
+        NEED(t && out32 && has_root, "null argument");
+        NEED(!t->prepared, "shard_reduce pending");
+        *has_root = t->has_root ? 1 : 0;
+        if (t->has_root) std::memcpy(out32, t->root, 32);
+        else std::memset(out32, 0, 32);
+    });
+}
+
+mkv_status mkv_tree_len(const mkv_tree *t, uint64_t *n) {
+    MKV_TRY({
+        NEED(t && n, "null argument");
+        *n = t->n;
+    });
+}
+
+mkv_status mkv_tree_node_count(const mkv_tree *t, uint64_t *count) {
+    MKV_TRY({
+        NEED(t && count, "null argument");
+        *count = t->n ? 2 * t->n - 1 : 0;
+    });
+}
+
+mkv_status mkv_tree_level_count(const mkv_tree *t, uint32_t *nlevels) {
+    MKV_TRY({
+        NEED(t && nlevels, "null argument");
+        *nlevels = t->n ? (uint32_t)t->lev_S.size() : 0;
+    });
+}
+
+mkv_status mkv_tree_level(const mkv_tree *t, uint32_t level, uint64_t *count, uint8_t *out) {
+    MKV_TRY({
+        NEED(t && count, "null argument");
+        NEED(!t->prepared, "shard_reduce pending");
+        if (!t->n || level >= t->lev_S.size()) {
+            *count = 0;
+            return MKV_OK;
+        }
+        *count = t->lev_cnt[level];
+        if (out && t->lev_cnt[level]) {
+            DevGuard g(t->dev);
+            MKV_HIP(hipMemcpyAsync(out, t->nodes.as<uint8_t>() + 32 * t->lev_off[level], 32 * t->lev_cnt[level],
+                                   hipMemcpyDeviceToHost, t->st));
+            MKV_HIP(hipStreamSynchronize(t->st));
+        }
+    });
+}
+
+mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *digests_out) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        DevGuard g(t->dev);
+        if (keys) {
+            auto *l = new mkv_keylist();
+            l->offsets.resize(t->n + 1, 0);
+            l->bytes.resize(t->kbytes);
+            if (t->n) {
+                MKV_HIP(hipMemcpyAsync(l->offsets.data(), t->koff.p, (t->n + 1) * 8, hipMemcpyDeviceToHost, t->st));
+                if (t->kbytes)
+                    MKV_HIP(hipMemcpyAsync(l->bytes.data(), t->kb.p, t->kbytes, hipMemcpyDeviceToHost, t->st));
+            }
+            MKV_HIP(hipStreamSynchronize(t->st));
+            *keys = l;
+        }
+        if (digests_out && t->n) {
+            MKV_HIP(hipMemcpyAsync(digests_out, t->nodes.p, 32 * t->n, hipMemcpyDeviceToHost, t->st));
+            MKV_HIP(hipStreamSynchronize(t->st));
+        }
+    });
+}
+
+static DiffSide side_of(const mkv_tree *t) {
+    DiffSide s;
+    s.kb = t->kb.as<uint8_t>();
+    s.koff = t->koff.as<uint64_t>();
+    s.pfx = t->pfx.as<uint64_t>();
+    s.dig = t->nodes.as<uint8_t>();
+    s.n = t->n;
+    return s;
+}
+
+mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out) {
+    MKV_TRY({
+        NEED(a && b && out, "null argument");
+        NEED(a->dev == b->dev, "trees on different devices");
+        NEED(!a->prepared && !b->prepared, "shard_reduce pending");
+        *out = nullptr;
+        mkv_tree *t = const_cast<mkv_tree *>(a);
+        DevGuard g(t->dev);
+        // b's last work must be complete before a's stream reads it
+        MKV_HIP(hipStreamSynchronize(b->st));
+        DiffSide A = side_of(a), B = side_of(b);
+        const uint64_t M = A.n + B.n;
+        size_t pd = prof_begin(t, "diff");
+        void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
+        uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
+        uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
+        launch_diff(A, B, scr, refs, cnt, t->st);
+        prof_end(t, pd);
+        const uint64_t m = d2h_u64(t, cnt);
+        auto *l = new mkv_keylist();
+        l->offsets.assign(m + 1, 0);
+        if (m) {
+            size_t pk = prof_begin(t, "diff");
+            uint64_t *lens = ens<uint64_t>(t->s_lens, m + 1);
+            uint64_t *off = ens<uint64_t>(t->d_outoff, m + 1);
+            launch_diff_keylens(refs, m, A, B, lens, t->st);
+            exclusive_scan_u64(lens, off, m, off + m, t->d_diffscr.p, t->st);
+            prof_end(t, pk);
+            const uint64_t bytes = d2h_u64(t, off + m);
+            uint8_t *ob = ens<uint8_t>(t->d_out, bytes + 16);
+            launch_diff_keys(refs, m, A, B, off, ob, t->st);
+            l->bytes.resize(bytes);
+            MKV_HIP(hipMemcpyAsync(l->offsets.data(), off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st));
+            if (bytes) MKV_HIP(hipMemcpyAsync(l->bytes.data(), ob, bytes, hipMemcpyDeviceToHost, t->st));
+        }
+        sync(t);
+        *out = l;
+    });
+}
+
+mkv_status mkv_tree_prefix_root(const mkv_tree *tc, const uint8_t *prefix, uint64_t plen, uint8_t out32[32],
+                                int *has_root) {
+    MKV_TRY({
+        NEED(tc && out32 && has_root, "null argument");
+        NEED(plen == 0 || prefix, "null prefix");
+        NEED(!tc->prepared && !tc->sharded, "prefix root needs an unsharded tree");
+        mkv_tree *t = const_cast<mkv_tree *>(tc);
+        DevGuard g(t->dev);
+        *has_root = 0;
+        std::memset(out32, 0, 32);
+        if (t->n == 0) return MKV_OK;
+        uint64_t lo = 0, hi = t->n;
+        if (plen) {
+            uint8_t *dp = ens<uint8_t>(t->d_out, plen + 16);
+            MKV_HIP(hipMemcpyAsync(dp, prefix, plen, hipMemcpyHostToDevice, t->st));
+            uint64_t *lohi = ens<uint64_t>(t->s_misc, 64);
+            launch_prefix_bounds(side_of(t), dp, (uint32_t)plen, lohi, t->st);
+            MKV_HIP(hipMemcpyAsync(t->h_small, lohi, 16, hipMemcpyDeviceToHost, t->st));
+            sync(t);
+            lo = t->h_small[0];
+            hi = t->h_small[1];
+        }
+        if (hi <= lo) return MKV_OK;
+        const uint64_t c = hi - lo;
+        // fresh reduction over leaves [lo, hi): a temporary plan on a scratch node buffer
+        mkv_tree tmp;  // only its plan vectors are used
+        plan_levels(&tmp, 0, c, c);
+        uint64_t tn = total_nodes(&tmp);
+        uint8_t *nodes = ens<uint8_t>(t->s_nodes2, tn * 32 + 64);
+        MKV_HIP(hipMemcpyAsync(nodes, t->nodes.as<uint8_t>() + 32 * lo, 32 * c, hipMemcpyDeviceToDevice, t->st));
+        tmp.st = t->st;
+        run_reduce(&tmp, nodes);
+        const size_t L = tmp.lev_S.size();
+        MKV_HIP(hipMemcpyAsync(out32, nodes + 32 * tmp.lev_off[L - 1], 32, hipMemcpyDeviceToHost, t->st));
+        MKV_HIP(hipStreamSynchronize(t->st));
+        tmp.st = nullptr;
+        *has_root = 1;
+    });
+}
+
+mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets) {
+    MKV_TRY({
+        NEED(l && n, "null argument");
+        *n = l->offsets.empty() ? 0 : l->offsets.size() - 1;
+        if (bytes) *bytes = l->bytes.data();
+        if (offsets) *offsets = l->offsets.data();
+    });
+}
+
+void mkv_keylist_free(mkv_keylist *l) { delete l; }
+
+// ---------------- sharded ----------------
+mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on_device, uint64_t *n_local) {
+    MKV_TRY({
+        NEED(t && n_local, "null argument");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        DevGuard g(t->dev);
+        const uint64_t n = keys.n;
+        const uint8_t *kb, *vb;
+        const uint64_t *koff, *voff;
+        if (on_device) {
+            kb = keys.bytes;
+            koff = keys.offsets;
+            vb = values.bytes;
+            voff = values.offsets;
+        } else {
+            check_blob(keys, "keys");
+            check_blob(values, "values");
+            const uint64_t kbn = n ? keys.offsets[n] - keys.offsets[0] : 0;
+            const uint64_t vbn = n ? values.offsets[n] - values.offsets[0] : 0;
+            ens<uint8_t>(t->s_kb, kbn + 16);
+            ens<uint64_t>(t->s_koff, n + 1);
+            ens<uint8_t>(t->s_vb, vbn + 16);
+            ens<uint64_t>(t->s_voff, n + 1);
+            upload_blob(t, keys, t->s_kb, t->s_koff);
+            upload_blob(t, values, t->s_vb, t->s_voff);
+            kb = t->s_kb.as<uint8_t>();
+            koff = t->s_koff.as<uint64_t>();
+            vb = t->s_vb.as<uint8_t>();
+            voff = t->s_voff.as<uint64_t>();
+        }
+        size_t ptot = prof_begin(t, "total_build");
+        uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+        size_t pl = prof_begin(t, "leaf_hash");
+        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
+        prof_end(t, pl);
+        sort_dedup_gather(t, kb, koff, n, nullptr);
+        prof_end(t, ptot);
+        sync(t);
+        t->prepared = true;
+        t->sharded = true;
+        t->has_root = false;
+        *n_local = t->n;
+    });
+}
+
+mkv_status mkv_shard_reduce(mkv_tree *t, uint64_t global_offset, uint64_t global_n) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(t->prepared, "mkv_shard_prepare first");
+        NEED(global_offset + t->n <= global_n, "shard outside the global range");
+        DevGuard g(t->dev);
+        t->goff = global_offset;
+        t->gN = global_n;
+        plan_levels(t, global_offset, t->n, global_n);
+        const uint64_t need = total_nodes(t);
+        if (need * 32 + 64 > t->nodes.cap) {
+            // grow while keeping the leaf level
+            DevBuf tmp;
+            tmp.ensure(32 * (t->n ? t->n : 1));
+            if (t->n) MKV_HIP(hipMemcpyAsync(tmp.p, t->nodes.p, 32 * t->n, hipMemcpyDeviceToDevice, t->st));
+            MKV_HIP(hipStreamSynchronize(t->st));
+            t->nodes.ensure(need * 32 + 64);
+            if (t->n) MKV_HIP(hipMemcpyAsync(t->nodes.p, tmp.p, 32 * t->n, hipMemcpyDeviceToDevice, t->st));
+            MKV_HIP(hipStreamSynchronize(t->st));
+        }
+        size_t ptot = prof_begin(t, "total_build");
+        size_t pr = prof_begin(t, "reduce");
+        run_reduce(t, t->nodes.as<uint8_t>());
+        prof_end(t, pr);
+        prof_end(t, ptot);
+        sync(t);
+        t->prepared = false;
+        t->has_root = false;
+    });
+}
+
+namespace {
+struct FringeEntry {
+    uint32_t level;
+    uint32_t valid;
+    uint64_t idx;
+    uint8_t h[32];
+};
+static_assert(sizeof(FringeEntry) == MKV_FRINGE_ENTRY_BYTES, "fringe layout");
+}  // namespace
+
+mkv_status mkv_shard_fringe(const mkv_tree *tc, uint8_t *out) {
+    MKV_TRY({
+        NEED(tc && out, "null argument");
+        NEED(!tc->prepared, "mkv_shard_reduce first");
+        mkv_tree *t = const_cast<mkv_tree *>(tc);
+        DevGuard g(t->dev);
+        std::memset(out, 0, MKV_FRINGE_BYTES);
+        std::vector<FringeEntry> fe;
+        std::vector<uint32_t> nodeidx;
+        const size_t L = t->lev_S.size();
+        for (size_t l = 0; l < L; ++l) {
+            const uint64_t a = t->lev_base[l], c = t->lev_cnt[l];
+            if (!c) continue;
+            uint64_t cand[2] = {a, a + c - 1};
+            for (int q = 0; q < 2; ++q) {
+                if (q == 1 && cand[1] == cand[0]) break;
+                const uint64_t x = cand[q];
+                bool parent_owned = false;
+                if (l + 1 < L) {
+                    const uint64_t p = x / 2, a2 = t->lev_base[l + 1], c2 = t->lev_cnt[l + 1];
+                    parent_owned = p >= a2 && p < a2 + c2;
+                }
+                if (parent_owned) continue;
+                FringeEntry e{};
+                e.level = (uint32_t)l;
+                e.valid = 1;
+                e.idx = x;
+                fe.push_back(e);
+                nodeidx.push_back((uint32_t)(t->lev_off[l] + (x - a)));
+            }
+        }
+        NEED(fe.size() <= MKV_FRINGE_MAX_ENTRIES, "fringe overflow");
+        if (!fe.empty()) {
+            uint32_t *didx = ens<uint32_t>(t->d_fr, fe.size() + 64);
+            uint8_t *dh = ens<uint8_t>(t->d_seam, fe.size() * 32 + 64);
+            MKV_HIP(hipMemcpyAsync(didx, nodeidx.data(), nodeidx.size() * 4, hipMemcpyHostToDevice, t->st));
+            launch_gather_digests(didx, t->nodes.as<uint8_t>(), fe.size(), dh, t->st);
+            std::vector<uint8_t> hh(fe.size() * 32);
+            MKV_HIP(hipMemcpyAsync(hh.data(), dh, hh.size(), hipMemcpyDeviceToHost, t->st));
+            MKV_HIP(hipStreamSynchronize(t->st));
+            for (size_t i = 0; i < fe.size(); ++i) std::memcpy(fe[i].h, hh.data() + 32 * i, 32);
+        }
+        std::memcpy(out, fe.data(), fe.size() * sizeof(FringeEntry));
+    });
+}
+
+mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes, uint32_t world, uint64_t global_n,
+                             uint8_t out32[32], int *has_root) {
+    MKV_TRY({
+        NEED(t && fringes && out32 && has_root, "null argument");
+        DevGuard g(t->dev);
+        *has_root = 0;
+        std::memset(out32, 0, 32);
+        if (global_n == 0) return MKV_OK;
+        std::vector<FringeEntry> all;
+        for (uint32_t r = 0; r < world; ++r) {
+            const FringeEntry *f = reinterpret_cast<const FringeEntry *>(fringes + (size_t)r * MKV_FRINGE_BYTES);
+            for (int i = 0; i < MKV_FRINGE_MAX_ENTRIES && f[i].valid; ++i) all.push_back(f[i]);
+        }
+        std::sort(all.begin(), all.end(), [](const FringeEntry &x, const FringeEntry &y) {
+            return x.level != y.level ? x.level < y.level : x.idx < y.idx;
+        });
+        std::vector<uint64_t> S;
+        for (uint64_t s = global_n;; s = (s + 1) / 2) {
+            S.push_back(s);
+            if (s == 1) break;
+        }
+        uint8_t *dent = ens<uint8_t>(t->d_seam, all.size() * sizeof(FringeEntry) + 64);
+        uint64_t *dS = ens<uint64_t>(t->d_S, S.size() + 1);
+        uint8_t *droot = ens<uint8_t>(t->d_fr, 64);
+        if (!all.empty())
+            MKV_HIP(hipMemcpyAsync(dent, all.data(), all.size() * sizeof(FringeEntry), hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipMemcpyAsync(dS, S.data(), S.size() * 8, hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipMemsetAsync(droot, 0, 32, t->st));
+        launch_seam_combine(dent, (uint32_t)all.size(), dS, (uint32_t)S.size(), nullptr, droot, t->st);
+        MKV_HIP(hipMemcpyAsync(out32, droot, 32, hipMemcpyDeviceToHost, t->st));
+        MKV_HIP(hipStreamSynchronize(t->st));
+        *has_root = 1;
+        std::memcpy(t->root, out32, 32);
+        t->has_root = true;
+    });
+}
+
+// ---------------- utilities ----------------
+mkv_status mkv_prof_enable(mkv_tree *t, int on) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        t->prof = on != 0;
+    });
+}
+mkv_status mkv_prof_reset(mkv_tree *t) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        t->pg.clear();
+    });
+}
+mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms, uint64_t *count) {
+    MKV_TRY({
+        NEED(t && group && total_ms && count, "null argument");
+        auto it = t->pg.find(group);
+        *total_ms = it == t->pg.end() ? 0.0 : it->second.first;
+        *count = it == t->pg.end() ? 0 : it->second.second;
+    });
+}
+
+mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,
+                                  uint32_t vlen, uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb,
+                                  uint64_t *koff, uint8_t *vb, uint64_t *voff) {
+    MKV_TRY({
+        NEED(kb && koff && vb && voff, "null buffer");
+        NEED(nshards >= 1 && nshards <= 64 && (64 % nshards) == 0 && shard < nshards, "bad shard spec");
+        DevGuard g(hip_device);
+        launch_gen_records(seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb, voff, nullptr);
+        MKV_HIP(hipDeviceSynchronize());
+    });
+}
+
+mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint8_t *out) {
+    MKV_TRY({
+        NEED(out || keys.n == 0, "null out");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        check_blob(keys, "keys");
+        check_blob(values, "values");
+        mkv_tree *t = nullptr;
+        mkv_status s = mkv_tree_create(hip_device, &t);
+        if (s != MKV_OK) throw Error(s, g_err);
+        try {
+            DevGuard g(t->dev);
+            const uint64_t n = keys.n;
+            ens<uint8_t>(t->s_kb, (n ? keys.offsets[n] - keys.offsets[0] : 0) + 16);
+            ens<uint64_t>(t->s_koff, n + 1);
+            ens<uint8_t>(t->s_vb, (n ? values.offsets[n] - values.offsets[0] : 0) + 16);
+            ens<uint64_t>(t->s_voff, n + 1);
+            upload_blob(t, keys, t->s_kb, t->s_koff);
+            upload_blob(t, values, t->s_vb, t->s_voff);
+            uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+            launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), t->s_vb.as<uint8_t>(),
+                             t->s_voff.as<uint64_t>(), n, dig, t->st);
+            if (n) MKV_HIP(hipMemcpyAsync(out, dig, 32 * n, hipMemcpyDeviceToHost, t->st));
+            MKV_HIP(hipStreamSynchronize(t->st));
+        } catch (...) {
+            mkv_tree_destroy(t);
+            throw;
+        }
+        mkv_tree_destroy(t);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,382 @@
+"""MerkleTree — the reference's `crate::store::merkle::MerkleTree` API on the MI355X.
+
+Mirrors /root/reference/src/store/merkle.rs method for method (same names, argument meaning and
+empty/None behaviour) over the C ABI of include/mkv_merkle.h. All hashing, ordering, reduction and
+diffing runs in the HIP kernels of merklekv_amd/csrc; this module only packs arguments.
+
+Per-call semantics are identical to the reference even though `insert`/`remove` are batched: the
+reference rebuilds the whole tree after every insert (merkle.rs:52-56) and that rebuild depends only on
+the final leaf map, so queued operations are applied as one ordered batch (last write wins, removes
+honoured in order) right before anything observes the tree.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from ._lib import FRINGE_BYTES, Blob, MerkleError, check, lib
+
+__all__ = ["MerkleTree", "NodeView", "pack_blob", "MerkleError"]
+
+
+def _b(x) -> bytes:
+    if isinstance(x, str):
+        return x.encode("utf-8", "surrogateescape")
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return bytes(x)
+    raise TypeError(f"key/value must be str or bytes, got {type(x).__name__}")
+
+
+def _s(b: bytes) -> str:
+    return b.decode("utf-8", "surrogateescape")
+
+
+class _Packed:
+    """Keeps the numpy buffers of a host mkv_blob alive for the duration of a call."""
+
+    def __init__(self, blob_bytes: np.ndarray, offsets: np.ndarray):
+        self.bytes = np.ascontiguousarray(blob_bytes, dtype=np.uint8)
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.n = len(self.offsets) - 1
+
+    def blob(self) -> Blob:
+        return Blob(self.bytes.ctypes.data if self.bytes.size else None,
+                    self.offsets.ctypes.data, self.n)
+
+
+def pack_blob(items: Sequence[bytes] | tuple) -> _Packed:
+    """Pack byte strings (or pass through a (bytes_array, offsets_array) pair)."""
+    if isinstance(items, tuple) and len(items) == 2 and isinstance(items[1], np.ndarray):
+        return _Packed(items[0], items[1])
+    items = [_b(x) for x in items]
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        off[1:] = np.cumsum(np.fromiter((len(x) for x in items), dtype=np.uint64, count=len(items)))
+    raw = b"".join(items)
+    return _Packed(np.frombuffer(raw, dtype=np.uint8) if raw else np.zeros(0, np.uint8), off)
+
+
+def _keylist(handle) -> list[bytes]:
+    n = C.c_uint64()
+    bp = C.c_void_p()
+    op = C.c_void_p()
+    check(lib().mkv_keylist_get(handle, C.byref(n), C.byref(bp), C.byref(op)))
+    cnt = n.value
+    if cnt == 0:
+        return []
+    offs = np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_uint64)), shape=(cnt + 1,)).copy()
+    raw = C.string_at(bp, int(offs[-1])) if offs[-1] else b""
+    o = offs.tolist()
+    return [raw[o[i]:o[i + 1]] for i in range(cnt)]
+
+
+class NodeView:
+    """Read-only view of a node of the implicit tree, shaped like the reference's MerkleNode
+    (merkle.rs:18-25): .hash, .left, .right (None at leaves), .key (leaves only). A promoted node
+    (R5, merkle.rs:111-114) is the same node as its only child, exactly as in the reference."""
+
+    def __init__(self, tree: "MerkleTree", level: int, idx: int):
+        sizes = tree._level_sizes()
+        # resolve promotion chains down to the node that actually owns this hash
+        while level > 0 and 2 * idx + 1 >= sizes[level - 1]:
+            level, idx = level - 1, 2 * idx
+        self._t, self.level, self.idx = tree, level, idx
+
+    @property
+    def hash(self) -> bytes:
+        return self._t.level_digests(self.level)[self.idx]
+
+    @property
+    def left(self):
+        return None if self.level == 0 else NodeView(self._t, self.level - 1, 2 * self.idx)
+
+    @property
+    def right(self):
+        return None if self.level == 0 else NodeView(self._t, self.level - 1, 2 * self.idx + 1)
+
+    @property
+    def key(self):
+        return _s(self._t._leaf_keys()[self.idx]) if self.level == 0 else None
+
+
+class MerkleTree:
+    """MerkleTree::new() (merkle.rs:36-41). `device` = HIP device index."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().mkv_tree_create(device, C.byref(h)))
+        self._h = h
+        self.device = device
+        self._pending: list[tuple[bool, bytes, bytes]] = []
+        self._cache: dict = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().mkv_tree_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------------------------ mutation
+    def insert(self, key, value) -> None:
+        """insert(&mut self, key, value) — merkle.rs:52-56."""
+        self._pending.append((False, _b(key), _b(value)))
+        self._cache.clear()
+
+    def remove(self, key) -> None:
+        """remove(&mut self, key) — merkle.rs:59-62."""
+        self._pending.append((True, _b(key), b""))
+        self._cache.clear()
+
+    def build(self, keys, values) -> None:
+        """new() + n x insert(k_i, v_i) as one device build (sync.rs:104-143, server.rs:661-669).
+        keys/values: sequences of str/bytes, or (bytes_array, offsets_array) pairs."""
+        self._pending.clear()
+        self._cache.clear()
+        pk, pv = pack_blob(keys), pack_blob(values)
+        if pk.n != pv.n:
+            raise ValueError("keys and values differ in length")
+        check(lib().mkv_tree_build(self._h, pk.blob(), pv.blob()))
+
+    def upsert(self, keys, values) -> None:
+        """Batch of insert() calls on the current contents (one device rebuild)."""
+        self._flush()
+        self._cache.clear()
+        pk, pv = pack_blob(keys), pack_blob(values)
+        check(lib().mkv_tree_upsert(self._h, pk.blob(), pv.blob()))
+
+    def remove_many(self, keys) -> None:
+        self._flush()
+        self._cache.clear()
+        check(lib().mkv_tree_remove(self._h, pack_blob(keys).blob()))
+
+    def _flush(self) -> None:
+        if not self._pending:
+            return
+        ops, self._pending = self._pending, []
+        self._cache.clear()
+        keys = [k for _, k, _ in ops]
+        vals = [v for _, _, v in ops]
+        pk, pv = pack_blob(keys), pack_blob(vals)
+        any_rm = any(r for r, _, _ in ops)
+        all_rm = all(r for r, _, _ in ops)
+        if all_rm:
+            check(lib().mkv_tree_remove(self._h, pk.blob()))
+        elif not any_rm:
+            if len(self) == 0:
+                check(lib().mkv_tree_build(self._h, pk.blob(), pv.blob()))
+            else:
+                check(lib().mkv_tree_upsert(self._h, pk.blob(), pv.blob()))
+        else:
+            rm = np.array([1 if r else 0 for r, _, _ in ops], dtype=np.uint8)
+            check(lib().mkv_tree_apply(self._h, pk.blob(), pv.blob(), rm.ctypes.data))
+
+    # ------------------------------------------------------------------ queries
+    def __len__(self) -> int:
+        self._flush()
+        n = C.c_uint64()
+        check(lib().mkv_tree_len(self._h, C.byref(n)))
+        return n.value
+
+    def get_root_hash(self) -> bytes | None:
+        """get_root_hash() — merkle.rs:65-67 (None for the empty tree, R6)."""
+        self._flush()
+        out = (C.c_uint8 * 32)()
+        has = C.c_int()
+        check(lib().mkv_tree_root(self._h, out, C.byref(has)))
+        return bytes(out) if has.value else None
+
+    @property
+    def root(self) -> NodeView | None:
+        """The public `root` field (merkle.rs:29) as a node view."""
+        self._flush()
+        sizes = self._level_sizes()
+        return NodeView(self, len(sizes) - 1, 0) if sizes else None
+
+    def _level_sizes(self) -> list[int]:
+        if "sizes" not in self._cache:
+            L = C.c_uint32()
+            check(lib().mkv_tree_level_count(self._h, C.byref(L)))
+            sizes = []
+            for l in range(L.value):
+                c = C.c_uint64()
+                check(lib().mkv_tree_level(self._h, l, C.byref(c), None))
+                sizes.append(c.value)
+            self._cache["sizes"] = sizes
+        return self._cache["sizes"]
+
+    def level_count(self) -> int:
+        self._flush()
+        return len(self._level_sizes())
+
+    def level_digests(self, level: int) -> list[bytes]:
+        """Level `level` of the implicit tree (0 = leaves in key order)."""
+        self._flush()
+        key = ("level", level)
+        if key not in self._cache:
+            c = C.c_uint64()
+            check(lib().mkv_tree_level(self._h, level, C.byref(c), None))
+            buf = np.zeros(max(c.value, 1) * 32, np.uint8)
+            check(lib().mkv_tree_level(self._h, level, C.byref(c), buf.ctypes.data))
+            raw = buf.tobytes()
+            self._cache[key] = [raw[32 * i:32 * i + 32] for i in range(c.value)]
+        return self._cache[key]
+
+    def _leaf_keys(self) -> list[bytes]:
+        if "keys" not in self._cache:
+            kl = C.c_void_p()
+            check(lib().mkv_tree_leaves(self._h, C.byref(kl), None))
+            try:
+                self._cache["keys"] = _keylist(kl)
+            finally:
+                lib().mkv_keylist_free(kl)
+        return self._cache["keys"]
+
+    def inorder_keys(self) -> list[str]:
+        """inorder_keys() — merkle.rs:126-130."""
+        self._flush()
+        return [_s(k) for k in self._leaf_keys()]
+
+    def leaves(self) -> list[tuple[str, bytes]]:
+        """leaves() — merkle.rs:133-138: (key, leaf digest) in key order."""
+        self._flush()
+        keys = self._leaf_keys()
+        dig = self.level_digests(0) if keys else []
+        return [(_s(k), d) for k, d in zip(keys, dig)]
+
+    def preorder_hashes(self) -> list[bytes]:
+        """preorder_hashes() — merkle.rs:142-153 (a promoted node is visited once, as in the reference)."""
+        self._flush()
+        sizes = self._level_sizes()
+        if not sizes:
+            return []
+        lv = [self.level_digests(l) for l in range(len(sizes))]
+        out: list[bytes] = []
+        stack = [(len(sizes) - 1, 0, True)]
+        while stack:
+            l, j, emit = stack.pop()
+            if emit:
+                out.append(lv[l][j])
+            if l == 0:
+                continue
+            if 2 * j + 1 < sizes[l - 1]:
+                stack.append((l - 1, 2 * j + 1, True))
+                stack.append((l - 1, 2 * j, True))
+            else:
+                stack.append((l - 1, 2 * j, False))  # promoted: same node, do not emit twice
+        return out
+
+    def node_count(self) -> int:
+        """node_count() — merkle.rs:156-163."""
+        self._flush()
+        c = C.c_uint64()
+        check(lib().mkv_tree_node_count(self._h, C.byref(c)))
+        return c.value
+
+    def diff_keys(self, other: "MerkleTree") -> list[str]:
+        """diff_keys(&other) — merkle.rs:171-196: sorted keys missing on one side or differing."""
+        return [_s(k) for k in self.diff_keys_bytes(other)]
+
+    def diff_keys_bytes(self, other: "MerkleTree") -> list[bytes]:
+        self._flush()
+        other._flush()
+        kl = C.c_void_p()
+        check(lib().mkv_tree_diff(self._h, other._h, C.byref(kl)))
+        try:
+            return _keylist(kl)
+        finally:
+            lib().mkv_keylist_free(kl)
+
+    def diff_first_key(self, other: "MerkleTree") -> str | None:
+        """diff_first_key(&other) — merkle.rs:199-204."""
+        d = self.diff_keys(other)
+        return d[0] if d else None
+
+    def prefix_root(self, prefix) -> bytes | None:
+        """Root of a fresh tree over the keys starting with prefix (HASH <prefix>, server.rs:647-685)."""
+        self._flush()
+        p = _b(prefix)
+        buf = (C.c_uint8 * max(len(p), 1)).from_buffer_copy(p or b"\0")
+        out = (C.c_uint8 * 32)()
+        has = C.c_int()
+        check(lib().mkv_tree_prefix_root(self._h, buf, len(p), out, C.byref(has)))
+        return bytes(out) if has.value else None
+
+    def clone(self) -> "MerkleTree":
+        """#[derive(Clone)] — merkle.rs:27."""
+        self._flush()
+        t = MerkleTree(self.device)
+        check(lib().mkv_tree_clone(self._h, t._h))
+        return t
+
+    __copy__ = clone
+
+    # ------------------------------------------------------------------ profiling
+    def prof_enable(self, on: bool = True) -> None:
+        check(lib().mkv_prof_enable(self._h, 1 if on else 0))
+
+    def prof_reset(self) -> None:
+        check(lib().mkv_prof_reset(self._h))
+
+    def prof_read(self, group: str) -> tuple[float, int]:
+        ms = C.c_double()
+        cnt = C.c_uint64()
+        check(lib().mkv_prof_read(self._h, group.encode(), C.byref(ms), C.byref(cnt)))
+        return ms.value, cnt.value
+
+    # ------------------------------------------------------------------ sharded build
+    def shard_prepare(self, keys, values, on_device: bool = False) -> int:
+        n = C.c_uint64()
+        if on_device:
+            kb, ko, vb, vo, cnt = keys
+            check(lib().mkv_shard_prepare(self._h, Blob(kb, ko, cnt), Blob(vb, vo, cnt), 1, C.byref(n)))
+        else:
+            pk, pv = pack_blob(keys), pack_blob(values)
+            check(lib().mkv_shard_prepare(self._h, pk.blob(), pv.blob(), 0, C.byref(n)))
+        self._cache.clear()
+        return n.value
+
+    def shard_reduce(self, global_offset: int, global_n: int) -> None:
+        check(lib().mkv_shard_reduce(self._h, global_offset, global_n))
+        self._cache.clear()
+
+    def shard_fringe(self) -> bytes:
+        buf = (C.c_uint8 * FRINGE_BYTES)()
+        check(lib().mkv_shard_fringe(self._h, buf))
+        return bytes(buf)
+
+    def shard_combine(self, fringes: bytes, world: int, global_n: int) -> bytes | None:
+        src = (C.c_uint8 * len(fringes)).from_buffer_copy(fringes)
+        out = (C.c_uint8 * 32)()
+        has = C.c_int()
+        check(lib().mkv_shard_combine(self._h, src, world, global_n, out, C.byref(has)))
+        return bytes(out) if has.value else None
+
+    def build_device(self, kb_ptr: int, koff_ptr: int, vb_ptr: int, voff_ptr: int, n: int) -> None:
+        """Build from records already resident in HBM (device pointers)."""
+        self._pending.clear()
+        self._cache.clear()
+        check(lib().mkv_tree_build_device(self._h, Blob(kb_ptr, koff_ptr, n), Blob(vb_ptr, voff_ptr, n)))
+
+
+def leaf_digests(keys, values, device: int = 0) -> list[bytes]:
+    """Kernel A alone: R2 digests of (key, value) records in input order."""
+    pk, pv = pack_blob(keys), pack_blob(values)
+    out = np.zeros(max(pk.n, 1) * 32, np.uint8)
+    check(lib().mkv_leaf_digests(device, pk.blob(), pv.blob(), out.ctypes.data))
+    raw = out.tobytes()
+    return [raw[32 * i:32 * i + 32] for i in range(pk.n)]
+
+
+def gen_records_device(device: int, seed: int, idx0: int, n: int, klen: int, vlen: int, kb: int, koff: int,
+                       vb: int, voff: int, shard: int = 0, nshards: int = 1, vfield: int = 1) -> None:
+    check(lib().mkv_gen_records_device(device, seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb,
+                                       voff))
+
+
+def version() -> str:
+    return lib().mkv_version().decode()

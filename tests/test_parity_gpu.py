@@ -1,0 +1,306 @@
+"""Bit-exact parity of the HIP path against the oracle (C restatement + committed golden fixtures).
+
+Integer/byte work, so the bar is exact equality everywhere: leaf digests, every level array, sorted
+keys, roots, diff key lists (order included), prefix roots.
+"""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from merklekv_amd import MerkleTree, leaf_digests  # noqa: E402
+from oracle.merkle_oracle import DEFAULT_SEED, PyMerkleTree, gen_records, pack, split_blob  # noqa: E402
+
+
+def levels_of(t: MerkleTree):
+    return [t.level_digests(l) for l in range(t.level_count())]
+
+
+def assert_tree_equal(gpu: MerkleTree, orc, check_levels=True):
+    assert len(gpu) == len(orc)
+    assert gpu.get_root_hash() == orc.root()
+    if check_levels:
+        assert gpu.level_count() == orc.nlevels()
+        for l in range(orc.nlevels()):
+            assert b"".join(gpu.level_digests(l)) == orc.level(l).tobytes(), l
+    ol = orc.leaves()
+    gl = gpu.leaves()
+    assert [k.encode("utf-8", "surrogateescape") for k, _ in gl] == [k for k, _ in ol]
+    assert [d for _, d in gl] == [d for _, d in ol]
+
+
+# ---------------------------------------------------------------- Kernel A alone
+def test_leaf_digest_every_length_against_hashlib():
+    """Every (|k|, |v|) combination around the 55/56/64-byte padding edges, aligned and unaligned."""
+    rng = random.Random(5)
+    keys, vals = [], []
+    for kl in list(range(0, 20)) + [31, 32, 33, 55, 56, 57, 63, 64, 65, 120, 200]:
+        for vl in [0, 1, 3, 4, 5, 44, 45, 46, 47, 48, 52, 56, 60, 64, 100, 119, 120, 121, 300]:
+            keys.append(bytes(rng.randrange(256) for _ in range(kl)))
+            vals.append(bytes(rng.randrange(256) for _ in range(vl)))
+    got = leaf_digests(keys, vals)
+    for k, v, g in zip(keys, vals, got):
+        enc = len(k).to_bytes(4, "big") + k + len(v).to_bytes(4, "big") + v
+        assert g == hashlib.sha256(enc).digest(), (len(k), len(v))
+
+
+def test_leaf_digest_uniform_fast_path():
+    """Uniform 4-aligned lengths (the fast path) incl. a partial last wave."""
+    for kl, vl, n in [(32, 100, 1000), (4, 0, 130), (0, 4, 65), (8, 48, 64), (60, 64, 200)]:
+        kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, n, klen=max(kl, 1), vlen=max(vl, 1))
+        keys = [k[:kl] for k in split_blob(kb, ko)]
+        vals = [v[:vl] for v in split_blob(vb, vo)]
+        got = leaf_digests(keys, vals)
+        for k, v, g in zip(keys, vals, got):
+            assert g == hashlib.sha256(len(k).to_bytes(4, "big") + k + len(v).to_bytes(4, "big") + v).digest()
+
+
+def test_leaf_digest_oversized_wave_global_path():
+    """A wave whose span does not fit its LDS region hashes straight from HBM."""
+    keys = [b"k%d" % i for i in range(70)]
+    vals = [bytes([i % 251]) * (300 + 37 * i) for i in range(70)]
+    got = leaf_digests(keys, vals)
+    for k, v, g in zip(keys, vals, got):
+        assert g == hashlib.sha256(len(k).to_bytes(4, "big") + k + len(v).to_bytes(4, "big") + v).digest()
+
+
+# ---------------------------------------------------------------- fixtures
+def test_known_answers(fixtures):
+    for name, case in fixtures["known_answers"].items():
+        t = MerkleTree()
+        t.build([bytes.fromhex(k) for k, _ in case["pairs"]], [bytes.fromhex(v) for _, v in case["pairs"]])
+        assert t.get_root_hash().hex() == case["root"], name
+        assert [[h.hex() for h in lv] for lv in levels_of(t)] == case["levels"], name
+
+
+def test_sizes_k_v(fixtures):
+    t = MerkleTree()
+    for n, root in fixtures["sizes_k_v"].items():
+        n = int(n)
+        t.build([f"k{i}" for i in range(n)], [f"v{i}" for i in range(n)])
+        assert t.get_root_hash().hex() == root, n
+
+
+def test_synthetic_fixtures(fixtures):
+    for case in fixtures["synthetic"]:
+        kb, ko, vb, vo = gen_records(case["seed"], 0, case["n"], klen=case["klen"], vlen=case["vlen"],
+                                     ragged=case["ragged"])
+        t = MerkleTree()
+        t.build((kb, ko), (vb, vo))
+        assert len(t) == case["n_unique"]
+        assert t.get_root_hash().hex() == case["root"]
+        for l, want in enumerate(case["level_sha256"]):
+            assert hashlib.sha256(b"".join(t.level_digests(l))).hexdigest() == want, l
+        lv = t.leaves()
+        assert [[k.encode().hex(), h.hex()] for k, h in lv[:16]] == case["first_leaves"]
+        assert [[k.encode().hex(), h.hex()] for k, h in lv[-16:]] == case["last_leaves"]
+
+
+def test_prefix_roots(fixtures):
+    kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 1000)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    for p, want in fixtures["prefix_roots"].items():
+        got = t.prefix_root(p)
+        assert (got.hex() if got else None) == want, p
+
+
+def test_diff_fixture(fixtures):
+    from tests.golden.make_golden import replica_b
+    d = fixtures["diff"]
+    kb, ko, vb, vo = gen_records(d["seed"], 0, d["n"])
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    bk, bv = replica_b(keys, vals, d["seed"], d["rate_ppm"])
+    a, b = MerkleTree(), MerkleTree()
+    a.build(keys, vals)
+    b.build(bk, bv)
+    assert a.get_root_hash().hex() == d["root_a"]
+    assert b.get_root_hash().hex() == d["root_b"]
+    assert a.diff_keys(b) == d["diff"]
+    assert b.diff_keys(a) == d["diff"]
+
+
+# ---------------------------------------------------------------- ordering edge cases vs C oracle
+def _check_pairs(oracle_lib, pairs):
+    t = MerkleTree()
+    t.build([k for k, _ in pairs], [v for _, v in pairs])
+    o = oracle_lib.OracleTree.from_pairs(pairs)
+    assert_tree_equal(t, o)
+    return t, o
+
+
+def test_long_common_prefixes_refinement(oracle_lib):
+    """Keys sharing >8-byte prefixes force the segmented refinement (chunks 1..k and the length pass)."""
+    rng = random.Random(11)
+    pairs = []
+    for i in range(3000):
+        p = rng.choice([b"user:000000", b"user:0000001", b"", b"\x00\x00\x00\x00\x00\x00\x00\x00",
+                        b"abcdefghabcdefghabcdefgh", b"abcdefgh"])
+        suffix = rng.choice([b"", b"\x00", b"\x00\x00", str(rng.randrange(500)).encode(), b"\xff" * rng.randrange(4)])
+        pairs.append((p + suffix, b"v%d" % rng.randrange(10 ** 6)))
+    _check_pairs(oracle_lib, pairs)
+
+
+def test_prefix_of_other_key_order(oracle_lib):
+    """Rust str Ord: a proper prefix sorts first; zero bytes vs end of string (R3)."""
+    ks = [b"ab", b"ab\x00", b"ab\x00\x00", b"ab\x01", b"a", b"", b"abcdefgh", b"abcdefgh\x00", b"abcdefg",
+          b"abcdefgh\x00\x00\x00\x00\x00\x00\x00\x00", b"abcdefgh\x00\x00\x00\x00\x00\x00\x00\x00\x00"]
+    t, _ = _check_pairs(oracle_lib, [(k, b"v") for k in ks])
+    assert [k.encode("utf-8", "surrogateescape") for k in t.inorder_keys()] == sorted(ks)
+
+
+def test_duplicates_last_write_wins(oracle_lib):
+    rng = random.Random(3)
+    pairs = [(b"k%d" % rng.randrange(300), b"v%d" % i) for i in range(5000)]
+    t, o = _check_pairs(oracle_lib, pairs)
+    assert len(t) == len({k for k, _ in pairs})
+
+
+def test_unicode_nul_ragged(oracle_lib):
+    rng = random.Random(7)
+    alphabet = ["a", "b", "\0", "é", "中", "🙂", "z", "\x7f"]
+    pairs = []
+    for _ in range(4000):
+        k = "".join(rng.choice(alphabet) for _ in range(rng.randrange(0, 14))).encode()
+        v = "".join(rng.choice(alphabet) for _ in range(rng.randrange(0, 60))).encode()
+        pairs.append((k, v))
+    _check_pairs(oracle_lib, pairs)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 63, 64, 65, 511, 512, 513, 1023, 1024, 1025, 4097, 65537])
+def test_synthetic_sizes_vs_oracle(oracle_lib, n):
+    kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED + n, 0, n)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    assert_tree_equal(t, oracle_lib.OracleTree.build(kb, ko, vb, vo))
+
+
+def test_ragged_synthetic_vs_oracle(oracle_lib):
+    kb, ko, vb, vo = oracle_lib.gen_records(99, 0, 50000, 24, 300, ragged=True)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    assert_tree_equal(t, oracle_lib.OracleTree.build(kb, ko, vb, vo))
+
+
+def test_large_1m_vs_oracle(oracle_lib):
+    n = 1_000_000
+    kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED, 0, n)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    oracle_lib.set_backend(1)
+    try:
+        o = oracle_lib.OracleTree.build(kb, ko, vb, vo)
+    finally:
+        oracle_lib.set_backend(0)
+    assert t.get_root_hash() == o.root()
+    assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
+    assert b"".join(t.level_digests(1)) == o.level(1).tobytes()
+
+
+# ---------------------------------------------------------------- diff vs oracle
+def test_random_diffs_vs_oracle(oracle_lib):
+    rng = random.Random(42)
+    for trial in range(6):
+        base = [(("key%07d" % rng.randrange(10 ** 6)).encode() + (b"\x00" if trial % 2 else b""),
+                 b"v%d" % rng.randrange(10 ** 9)) for _ in range(rng.choice([10, 1000, 20000]))]
+        other = []
+        for k, v in base:
+            r = rng.random()
+            if r < 0.05:
+                continue
+            other.append((k, v + b"!" if r < 0.15 else v))
+        other += [(b"new%d" % rng.randrange(10 ** 5), b"x") for _ in range(rng.randrange(50))]
+        rng.shuffle(other)
+        a, b = MerkleTree(), MerkleTree()
+        a.build([k for k, _ in base], [v for _, v in base])
+        b.build([k for k, _ in other], [v for _, v in other])
+        oa = oracle_lib.OracleTree.from_pairs(base)
+        ob = oracle_lib.OracleTree.from_pairs(other)
+        assert a.diff_keys_bytes(b) == oa.diff(ob)
+        assert b.diff_keys_bytes(a) == ob.diff(oa)
+
+
+def test_diff_shared_long_prefixes_vs_oracle(oracle_lib):
+    keys = [b"tenant/0001/object/%08d" % i for i in range(5000)]
+    a_pairs = [(k, b"A") for k in keys]
+    b_pairs = [(k, b"A" if i % 97 else b"B") for i, k in enumerate(keys) if i % 211] + [(b"tenant/0001/object/", b"z")]
+    a, b = MerkleTree(), MerkleTree()
+    a.build([k for k, _ in a_pairs], [v for _, v in a_pairs])
+    b.build([k for k, _ in b_pairs], [v for _, v in b_pairs])
+    oa = oracle_lib.OracleTree.from_pairs(a_pairs)
+    ob = oracle_lib.OracleTree.from_pairs(b_pairs)
+    assert a.diff_keys_bytes(b) == oa.diff(ob)
+
+
+def test_diff_empty_trees():
+    a, b = MerkleTree(), MerkleTree()
+    assert a.diff_keys(b) == []
+    b.insert("x", "1")
+    assert a.diff_keys(b) == ["x"] and b.diff_keys(a) == ["x"]
+
+
+# ---------------------------------------------------------------- batches (upsert/remove/apply)
+def test_insert_remove_sequences_vs_python_oracle():
+    rng = random.Random(17)
+    t, py = MerkleTree(), PyMerkleTree()
+    for step in range(40):
+        for _ in range(rng.randrange(1, 60)):
+            k = b"k%d" % rng.randrange(200)
+            if rng.random() < 0.3:
+                t.remove(k)
+                py.remove(k)
+            else:
+                v = b"v%d" % rng.randrange(1000)
+                t.insert(k, v)
+                py.insert(k, v)
+        assert t.get_root_hash() == py.get_root_hash(), step
+        assert len(t) == len(py.leaf_map)
+        assert [k.encode() for k in t.inorder_keys()] == py.inorder_keys()
+
+
+def test_upsert_remove_batches_vs_oracle(oracle_lib):
+    kb, ko, vb, vo = oracle_lib.gen_records(5, 0, 20000, 16, 40, ragged=True)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    o = oracle_lib.OracleTree.build(kb, ko, vb, vo)
+    kb2, ko2, vb2, vo2 = oracle_lib.gen_records(5, 15000, 10000, 16, 40, ragged=True, vfield=3)
+    t.upsert((kb2, ko2), (vb2, vo2))
+    o = o.upsert(kb2, ko2, vb2, vo2)
+    assert_tree_equal(t, o)
+    keys = split_blob(kb, ko)[::3]
+    rb, ro = pack(keys)
+    t.remove_many((rb, ro))
+    o = o.remove(rb, ro)
+    assert_tree_equal(t, o)
+
+
+def test_clone_is_deep():
+    a = MerkleTree()
+    a.build([f"k{i}" for i in range(100)], [f"v{i}" for i in range(100)])
+    b = a.clone()
+    b.insert("k5", "changed")
+    assert a.get_root_hash() != b.get_root_hash()
+    assert a.diff_keys(b) == ["k5"]
+
+
+def test_level_structure_and_views():
+    n = 1000
+    t = MerkleTree()
+    t.build([f"k{i}" for i in range(n)], [f"v{i}" for i in range(n)])
+    sizes = [len(t.level_digests(l)) for l in range(t.level_count())]
+    s, want = n, []
+    while True:
+        want.append(s)
+        if s == 1:
+            break
+        s = (s + 1) // 2
+    assert sizes == want
+    assert t.node_count() == 2 * n - 1
+    assert len(t.preorder_hashes()) == 2 * n - 1
+    py = PyMerkleTree()
+    for i in range(n):
+        py.insert(f"k{i}".encode(), f"v{i}".encode())
+    assert [t.level_digests(l) for l in range(len(sizes))] == py.levels()
