@@ -25,7 +25,13 @@ enum : int { ST_OK = 0, ST_EINVAL = 1, ST_EHIP = 2, ST_ENOMEM = 3, ST_ESTATE = 4
                                std::string(#expr " failed: ") + hipGetErrorString(e_));               \
     } while (0)
 
-#define MKV_LAUNCH_CHECK() MKV_HIP(hipGetLastError())
+#define MKV_LAUNCH_CHECK()                                                                             \
+    do {                                                                                               \
+        hipError_t e_ = hipGetLastError();                                                             \
+        if (e_ != hipSuccess)                                                                          \
+            throw ::mkv::Error(::mkv::ST_EHIP, std::string("kernel launch in ") + __func__ + ": " +     \
+                                                   hipGetErrorString(e_));                             \
+    } while (0)
 
 // Growable device buffer. Grows only; steady-state builds of the same size never re-allocate.
 struct DevBuf {

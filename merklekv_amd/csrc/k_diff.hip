@@ -24,11 +24,20 @@ constexpr int DT = DIFF_THREADS;
 constexpr int DI = DIFF_ITEMS;
 constexpr int DTILE = DT * DI;
 
+// Sorted key i of a side: storage record perm[i].
+__device__ __forceinline__ const uint8_t *key_at(const DiffSide &S, uint64_t i, uint64_t *len) {
+    const uint32_t o = S.perm[i];
+    const uint64_t a = S.koff[o];
+    *len = S.koff[o + 1] - a;
+    return S.kb + a;
+}
+
 __device__ __forceinline__ int cmp_ab(const DiffSide &A, uint64_t i, uint64_t pa, const DiffSide &B, uint64_t j,
                                       uint64_t pb) {
     if (pa != pb) return pa < pb ? -1 : 1;
-    uint64_t a0 = A.koff[i], a1 = A.koff[i + 1], b0 = B.koff[j], b1 = B.koff[j + 1];
-    return key_cmp(A.kb + a0, a1 - a0, pa, B.kb + b0, b1 - b0, pb);
+    uint64_t la, lb;
+    const uint8_t *ka = key_at(A, i, &la), *kb = key_at(B, j, &lb);
+    return key_cmp(ka, la, pa, kb, lb, pb);
 }
 
 __device__ __forceinline__ bool digest_eq(const uint8_t *a, const uint8_t *b) {
@@ -200,7 +209,9 @@ __global__ void k_diff_keylens(const uint64_t *__restrict__ refs, uint64_t m, Di
     uint64_t r = refs[k];
     const DiffSide &S = (r >> 63) ? B : A;
     uint64_t i = r & ~(1ull << 63);
-    lens[k] = S.koff[i + 1] - S.koff[i];
+    uint64_t len;
+    (void)key_at(S, i, &len);
+    lens[k] = len;
 }
 
 __global__ void k_diff_keys(const uint64_t *__restrict__ refs, uint64_t m, DiffSide A, DiffSide B,
@@ -210,8 +221,8 @@ __global__ void k_diff_keys(const uint64_t *__restrict__ refs, uint64_t m, DiffS
     uint64_t r = refs[k];
     const DiffSide &S = (r >> 63) ? B : A;
     uint64_t i = r & ~(1ull << 63);
-    uint64_t a = S.koff[i], len = S.koff[i + 1] - a;
-    const uint8_t *s = S.kb + a;
+    uint64_t len;
+    const uint8_t *s = key_at(S, i, &len);
     uint8_t *d = out + off[k];
     for (uint64_t x = 0; x < len; ++x) d[x] = s[x];
 }
@@ -224,17 +235,19 @@ __global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, 
     uint64_t lo = 0, hi = A.n;
     while (lo < hi) {
         uint64_t mid = (lo + hi) >> 1;
-        uint64_t a0 = A.koff[mid], a1 = A.koff[mid + 1];
-        if (key_cmp(A.kb + a0, a1 - a0, A.pfx[mid], prefix, plen, pp) < 0) lo = mid + 1;
+        uint64_t la;
+        const uint8_t *ka = key_at(A, mid, &la);
+        if (key_cmp(ka, la, A.pfx[mid], prefix, plen, pp) < 0) lo = mid + 1;
         else hi = mid;
     }
     // keys with the prefix are exactly those >= prefix that start with it: binary search on "starts with"
     uint64_t l2 = lo, h2 = A.n;
     while (l2 < h2) {
         uint64_t mid = (l2 + h2) >> 1;
-        uint64_t a0 = A.koff[mid], a1 = A.koff[mid + 1];
-        bool starts = (a1 - a0) >= plen;
-        for (uint32_t x = 0; starts && x < plen; ++x) starts = A.kb[a0 + x] == prefix[x];
+        uint64_t la;
+        const uint8_t *ka = key_at(A, mid, &la);
+        bool starts = la >= plen;
+        for (uint32_t x = 0; starts && x < plen; ++x) starts = ka[x] == prefix[x];
         if (starts) l2 = mid + 1;
         else h2 = mid;
     }

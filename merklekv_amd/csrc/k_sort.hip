@@ -273,6 +273,12 @@ __global__ void k_compact_u32(const uint32_t *__restrict__ src, const uint32_t *
     if (i < n && flags[i]) dst[scan[i]] = src[i];
 }
 
+__global__ void k_compact_u64(const uint64_t *__restrict__ src, const uint32_t *__restrict__ flags,
+                              const uint32_t *__restrict__ scan, uint64_t n, uint64_t *__restrict__ dst) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && flags[i]) dst[scan[i]] = src[i];
+}
+
 // ---- gathers ----
 __global__ void k_gather_digests(const uint32_t *__restrict__ perm, const uint8_t *__restrict__ dig, uint64_t n,
                                  uint8_t *__restrict__ out) {
@@ -451,6 +457,12 @@ void launch_compact_u32(const uint32_t *src, const uint32_t *flags, const uint32
                         hipStream_t st) {
     if (!n) return;
     hipLaunchKernelGGL(k_compact_u32, grid1d(n), dim3(256), 0, st, src, flags, scan, n, dst);
+    MKV_LAUNCH_CHECK();
+}
+void launch_compact_u64(const uint64_t *src, const uint32_t *flags, const uint32_t *scan, uint64_t n, uint64_t *dst,
+                        hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_compact_u64, grid1d(n), dim3(256), 0, st, src, flags, scan, n, dst);
     MKV_LAUNCH_CHECK();
 }
 void launch_gather_digests(const uint32_t *perm, const uint8_t *dig_in, uint64_t n, uint8_t *out, hipStream_t st) {

@@ -46,6 +46,8 @@ void launch_refine_apply(const uint32_t *pos, uint64_t m, const uint32_t *sorted
 // keep[i] = !tie[i+1] && perm[i] < n_live
 void launch_keep_flags(const uint8_t *tie, const uint32_t *perm, uint64_t n, uint64_t n_live, uint32_t *flags,
                        hipStream_t st);
+void launch_compact_u64(const uint64_t *src, const uint32_t *flags, const uint32_t *scan, uint64_t n, uint64_t *dst,
+                        hipStream_t st);
 void launch_compact_u32(const uint32_t *src, const uint32_t *flags, const uint32_t *scan, uint64_t n, uint32_t *dst,
                         hipStream_t st);
 
@@ -81,8 +83,9 @@ void launch_seam_combine(const uint8_t *entries, uint32_t nent, const uint64_t *
 
 // ---- Kernel D: diff (k_diff.hip) ----
 struct DiffSide {
-    const uint8_t *kb;
+    const uint8_t *kb;      // keys in storage order
     const uint64_t *koff;
+    const uint32_t *perm;   // sorted position -> storage index
     const uint64_t *pfx;
     const uint8_t *dig;
     uint64_t n;

@@ -54,16 +54,31 @@ __host__ __device__ constexpr Sched64 make_pad64_kw() {
 // Constant-amount rotate: clang emits llvm.fshr, which lowers to one v_alignbit_b32.
 __device__ __forceinline__ uint32_t rotr(uint32_t x, uint32_t n) { return (x >> n) | (x << (32 - n)); }
 
-__device__ __forceinline__ uint32_t bsig0(uint32_t a) { return rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22); }
-__device__ __forceinline__ uint32_t bsig1(uint32_t e) { return rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25); }
-__device__ __forceinline__ uint32_t ssig0(uint32_t w) { return rotr(w, 7) ^ rotr(w, 18) ^ (w >> 3); }
-__device__ __forceinline__ uint32_t ssig1(uint32_t w) { return rotr(w, 17) ^ rotr(w, 19) ^ (w >> 10); }
-// Ch = e ? f : g (v_bfi_b32); Maj = (a^b) ? c : b
-__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return (e & f) | (~e & g); }
-__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t x = a ^ b;
-    return (x & c) | (~x & b);
+// gfx950 v_bitop3_b32: D = LUT[4*S0 + 2*S1 + S2] per bit. hipcc does not fold x^y^z, Ch or Maj into
+// it (it emits two v_xor_b32 per three-way xor), so the three-input functions are written directly:
+// XOR3 = 0x96, Ch(e,f,g) = e ? f : g = 0xCA, Maj = 0xE8. One VALU op each.
+__device__ __forceinline__ uint32_t bitop3_96(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
+__device__ __forceinline__ uint32_t bitop3_ca(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t bitop3_e8(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t bsig0(uint32_t a) { return bitop3_96(rotr(a, 2), rotr(a, 13), rotr(a, 22)); }
+__device__ __forceinline__ uint32_t bsig1(uint32_t e) { return bitop3_96(rotr(e, 6), rotr(e, 11), rotr(e, 25)); }
+__device__ __forceinline__ uint32_t ssig0(uint32_t w) { return bitop3_96(rotr(w, 7), rotr(w, 18), w >> 3); }
+__device__ __forceinline__ uint32_t ssig1(uint32_t w) { return bitop3_96(rotr(w, 17), rotr(w, 19), w >> 10); }
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return bitop3_ca(e, f, g); }
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return bitop3_e8(a, b, c); }
 
 __device__ __forceinline__ void sha_init(uint32_t s[8]) {
 #pragma unroll

@@ -21,6 +21,7 @@ namespace {
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
     std::string group;
+    bool closed = false;
 };
 
 }  // namespace
@@ -36,8 +37,11 @@ struct mkv_tree {
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
-    uint64_t kbytes = 0;  // bytes of sorted keys
-    DevBuf kb, koff, pfx, nodes;
+    // Keys are owned in storage (input) order: kb/koff hold nstore records (kbytes bytes); perm[i] is the
+    // storage index of sorted leaf i; pfx[i] its 8-byte big-endian key prefix. Keeping input order
+    // avoids a random-access gather of every key on each build.
+    uint64_t nstore = 0, kbytes = 0;
+    DevBuf kb, koff, perm, pfx, nodes;
     std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
     bool has_root = false;
     uint8_t root[32] = {0};
@@ -60,7 +64,7 @@ struct mkv_tree {
     // ---- profiling ----
     bool prof = false;
     std::vector<EvPair> evpool;
-    size_t evused = 0;
+    std::vector<size_t> evfree, evdone;
     std::map<std::string, std::pair<double, uint64_t>> pg;
 
     // the device pointers of the current staged build input
@@ -75,6 +79,7 @@ namespace {
 struct DevGuard {
     int prev = -1;
     explicit DevGuard(int d) {
+        (void)hipGetLastError();  // a stale error from an unrelated earlier call must not fail this one
         (void)hipGetDevice(&prev);
         MKV_HIP(hipSetDevice(d));
     }
@@ -96,37 +101,47 @@ void launch_clear_tomb(const uint8_t *tomb, const uint32_t *perm, uint64_t n, ui
 
 size_t prof_begin(mkv_tree *t, const char *group) {
     if (!t->prof) return SIZE_MAX;
-    if (t->evused == t->evpool.size()) {
+    if (t->evfree.empty()) {
         EvPair p;
         MKV_HIP(hipEventCreate(&p.a));
         MKV_HIP(hipEventCreate(&p.b));
         t->evpool.push_back(p);
+        t->evfree.push_back(t->evpool.size() - 1);
     }
-    size_t i = t->evused++;
+    size_t i = t->evfree.back();
+    t->evfree.pop_back();
     t->evpool[i].group = group;
+    t->evpool[i].closed = false;
     MKV_HIP(hipEventRecord(t->evpool[i].a, t->st));
     return i;
 }
 void prof_end(mkv_tree *t, size_t i) {
     if (i == SIZE_MAX) return;
     MKV_HIP(hipEventRecord(t->evpool[i].b, t->st));
+    t->evpool[i].closed = true;
+    t->evdone.push_back(i);
 }
-// after a stream sync
+// after a stream sync: accumulate every closed pair (open ones stay pending)
 void prof_collect(mkv_tree *t) {
-    if (!t->prof) return;
-    for (size_t i = 0; i < t->evused; ++i) {
+    for (size_t i : t->evdone) {
         float ms = 0;
         MKV_HIP(hipEventElapsedTime(&ms, t->evpool[i].a, t->evpool[i].b));
         auto &g = t->pg[t->evpool[i].group];
         g.first += ms;
         g.second += 1;
+        t->evfree.push_back(i);
     }
-    t->evused = 0;
+    t->evdone.clear();
 }
 
 void sync(mkv_tree *t) {
     MKV_HIP(hipStreamSynchronize(t->st));
     prof_collect(t);
+}
+
+void swap_buf(DevBuf &a, DevBuf &b) {
+    std::swap(a.p, b.p);
+    std::swap(a.cap, b.cap);
 }
 
 template <class T> T *ens(DevBuf &b, uint64_t count) { return reinterpret_cast<T *>(b.ensure(count * sizeof(T))); }
@@ -272,7 +287,8 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
 // Produces sorted unique keys (last write wins), leaf level, and the level plan for [o, o+n) of N
 // (N == UINT64_MAX: unsharded, N = n).
 // ---------------------------------------------------------------------------------------------
-void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb) {
+void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
+                       bool staged_inputs, uint64_t staged_kbytes) {
     hipStream_t st = t->st;
     const uint8_t *dig = t->s_dig.as<uint8_t>();
     uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
@@ -286,16 +302,17 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     size_t ps = prof_begin(t, "sort");
     launch_prefix64(kb, koff, n_in, k1, v1, st);
     const bool sw = radix_sort_pairs(k1, v1, k2, v2, n_in, 0, 64, radix, st);
-    uint64_t *pk = sw ? k2 : k1;
-    uint32_t *perm = sw ? v2 : v1;
-    uint32_t *perm_alt = sw ? v1 : v2;
+    DevBuf *pkbuf = sw ? &t->s_k2 : &t->s_k1, *pkalt = sw ? &t->s_k1 : &t->s_k2;
+    DevBuf *pmbuf = sw ? &t->s_v2 : &t->s_v1, *pmalt = sw ? &t->s_v1 : &t->s_v2;
+    uint64_t *pk = pkbuf->as<uint64_t>();
+    uint32_t *perm = pmbuf->as<uint32_t>();
     MKV_HIP(hipMemsetAsync(misc, 0, 4, st));
     launch_mark_ties(pk, n_in, tie, misc, st);
     prof_end(t, ps);
     const uint32_t nties = n_in ? d2h_u32(t, misc) : 0;
     if (nties) {
         size_t pr = prof_begin(t, "sort");
-        refine_ties(t, kb, koff, n_in, perm, tie);
+        refine_ties(t, kb, koff, n_in, perm, tie);  // reorders perm inside equal-prefix runs only
         prof_end(t, pr);
     }
     uint64_t n = n_in;
@@ -303,35 +320,60 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         size_t pd = prof_begin(t, "sort");
         uint32_t *flags = ens<uint32_t>(t->s_flags, n_in + 1);
         uint32_t *scan = ens<uint32_t>(t->s_scan, n_in + 1);
-        launch_keep_flags(tie, perm, n_in, UINT64_MAX, flags, st);
-        if (tomb) launch_clear_tomb(tomb, perm, n_in, flags, st);  // removed keys never survive
+        launch_keep_flags(tie, perm, n_in, UINT64_MAX, flags, st);  // dedup: keep the last write
+        if (tomb) launch_clear_tomb(tomb, perm, n_in, flags, st);   // removed keys never survive
         exclusive_scan_u32(flags, scan, n_in, misc + 3, radix, st);
-        launch_compact_u32(perm, flags, scan, n_in, perm_alt, st);
+        launch_compact_u32(perm, flags, scan, n_in, pmalt->as<uint32_t>(), st);
+        launch_compact_u64(pk, flags, scan, n_in, pkalt->as<uint64_t>(), st);
         prof_end(t, pd);
         n = d2h_u32(t, misc + 3);
-        perm = perm_alt;
+        std::swap(pkbuf, pkalt);
+        std::swap(pmbuf, pmalt);
+        perm = pmbuf->as<uint32_t>();
     }
     t->n = n;
-    // ---- gather into sorted order ----
+    // adopt the sorted prefixes and the permutation
+    swap_buf(t->pfx, *pkbuf);
+    swap_buf(t->perm, *pmbuf);
+    perm = t->perm.as<uint32_t>();
+    // own the keys (storage order): adopt staged uploads, copy borrowed device inputs
+    t->nstore = n_in;
+    if (staged_inputs) {
+        swap_buf(t->kb, t->s_kb);
+        swap_buf(t->koff, t->s_koff);
+        t->kbytes = staged_kbytes;
+    } else {
+        const uint64_t kbytes = n_in ? d2h_u64(t, koff + n_in) : 0;
+        uint8_t *dkb = ens<uint8_t>(t->kb, kbytes + 16);
+        uint64_t *dko = ens<uint64_t>(t->koff, n_in + 1);
+        size_t pc = prof_begin(t, "gather");
+        if (kbytes) MKV_HIP(hipMemcpyAsync(dkb, kb, kbytes, hipMemcpyDeviceToDevice, st));
+        MKV_HIP(hipMemcpyAsync(dko, koff, (n_in + 1) * 8, hipMemcpyDeviceToDevice, st));
+        prof_end(t, pc);
+        t->kbytes = kbytes;
+    }
     size_t pg = prof_begin(t, "gather");
-    uint64_t *lens = ens<uint64_t>(t->s_lens, n + 1);
-    uint64_t *koff_out = ens<uint64_t>(t->koff, n + 1);
-    launch_gather_keylens(perm, koff, n, lens, st);
-    exclusive_scan_u64(lens, koff_out, n, koff_out + n, radix, st);
-    prof_end(t, pg);
-    t->kbytes = n ? d2h_u64(t, koff_out + n) : 0;
-    if (!n) MKV_HIP(hipMemsetAsync(koff_out, 0, sizeof(uint64_t), st));
-    pg = prof_begin(t, "gather");
-    uint8_t *kb_out = ens<uint8_t>(t->kb, t->kbytes + 16);
-    launch_gather_keys(perm, kb, koff, koff_out, n, kb_out, st);
-    uint64_t *pfx = ens<uint64_t>(t->pfx, n + 1);
-    launch_prefix64(kb_out, koff_out, n, pfx, v1 == perm ? v2 : v1, st);
-    prof_end(t, pg);
-    pg = prof_begin(t, "gather");
-    // leaf level = nodes[0 .. n); nodes is sized for every level of an unsharded tree (2n-1 nodes)
-    uint8_t *nodes = ens<uint8_t>(t->nodes, 2 * 32 * (n ? n : 1) + 64);
+    // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
+    // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
+    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
     launch_gather_digests(perm, dig, n, nodes, st);
     prof_end(t, pg);
+}
+
+// Sorted keys of the tree packed into (dst_kb, dst_koff[0..n]) starting at byte base; returns bytes.
+uint64_t pack_sorted_keys(mkv_tree *t, DevBuf &dst_kb, DevBuf &dst_koff, uint64_t extra_bytes,
+                          uint64_t extra_items) {
+    const uint64_t n = t->n;
+    uint64_t *lens = ens<uint64_t>(t->s_lens, n + 1);
+    uint64_t *ko = ens<uint64_t>(dst_koff, n + extra_items + 1);
+    void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n), scan_scratch_bytes(n + 1)));
+    launch_gather_keylens(t->perm.as<uint32_t>(), t->koff.as<uint64_t>(), n, lens, t->st);
+    exclusive_scan_u64(lens, ko, n, ko + n, radix, t->st);
+    const uint64_t bytes = n ? d2h_u64(t, ko + n) : 0;
+    if (!n) MKV_HIP(hipMemsetAsync(ko, 0, 8, t->st));
+    uint8_t *kb = ens<uint8_t>(dst_kb, bytes + extra_bytes + 16);
+    launch_gather_keys(t->perm.as<uint32_t>(), t->kb.as<uint8_t>(), t->koff.as<uint64_t>(), ko, n, kb, t->st);
+    return bytes;
 }
 
 void finish_unsharded(mkv_tree *t) {
@@ -376,19 +418,17 @@ void check_blob(const mkv_blob &b, const char *what) {
 
 // Stage [existing leaves ++ batch] for upsert / remove / apply. Returns staged record count.
 // Existing records carry their leaf digests; batch records are hashed on the device.
-uint64_t stage_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
+uint64_t stage_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove,
+                     uint64_t *staged_kbytes) {
     if (t->sharded) throw Error(ST_ESTATE, "upsert/remove on a sharded tree is not supported");
     const uint64_t m = t->n, nb = keys.n, tot = m + nb;
     const uint64_t kb_new = nb ? keys.offsets[nb] - keys.offsets[0] : 0;
-    uint8_t *skb = ens<uint8_t>(t->s_kb, t->kbytes + kb_new + 16);
-    uint64_t *skoff = ens<uint64_t>(t->s_koff, tot + 1);
+    // existing leaves first (sorted, unique, with their digests), then the batch in order
+    const uint64_t old_bytes = pack_sorted_keys(t, t->s_kb, t->s_koff, kb_new, nb);
     uint8_t *sdig = ens<uint8_t>(t->s_dig, (tot ? tot : 1) * 32);
-    if (t->kbytes) MKV_HIP(hipMemcpyAsync(skb, t->kb.p, t->kbytes, hipMemcpyDeviceToDevice, t->st));
-    if (m) {
-        MKV_HIP(hipMemcpyAsync(skoff, t->koff.p, m * sizeof(uint64_t), hipMemcpyDeviceToDevice, t->st));
-        MKV_HIP(hipMemcpyAsync(sdig, t->nodes.p, m * 32, hipMemcpyDeviceToDevice, t->st));
-    }
-    upload_blob(t, keys, t->s_kb, t->s_koff, 0, m, t->kbytes);
+    if (m) MKV_HIP(hipMemcpyAsync(sdig, t->nodes.p, m * 32, hipMemcpyDeviceToDevice, t->st));
+    upload_blob(t, keys, t->s_kb, t->s_koff, 0, m, old_bytes);
+    *staged_kbytes = old_bytes + kb_new;
     if (values && nb) {
         const uint64_t vbytes = values->offsets[nb] - values->offsets[0];
         ens<uint8_t>(t->s_vb, vbytes + 16);
@@ -475,6 +515,7 @@ void mkv_tree_destroy(mkv_tree *t) {
     if (t->h_small) (void)hipHostFree(t->h_small);
     (void)hipStreamDestroy(t->st);
     delete t;
+    (void)hipGetLastError();
 }
 
 mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
@@ -487,18 +528,21 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         MKV_HIP(hipStreamSynchronize(src->st));
         const uint64_t nn = total_nodes(src);
         uint8_t *kb = ens<uint8_t>(dst->kb, src->kbytes + 16);
-        uint64_t *ko = ens<uint64_t>(dst->koff, src->n + 1);
+        uint64_t *ko = ens<uint64_t>(dst->koff, src->nstore + 1);
+        uint32_t *pm = ens<uint32_t>(dst->perm, src->n + 1);
         uint64_t *pf = ens<uint64_t>(dst->pfx, src->n + 1);
-        uint8_t *nd = ens<uint8_t>(dst->nodes, std::max<uint64_t>(nn, 2 * src->n) * 32 + 64);
+        uint8_t *nd = ens<uint8_t>(dst->nodes, 32 * (2 * src->n + 66));
         if (src->kbytes) MKV_HIP(hipMemcpyAsync(kb, src->kb.p, src->kbytes, hipMemcpyDeviceToDevice, dst->st));
-        MKV_HIP(hipMemcpyAsync(ko, src->koff.p ? src->koff.p : ko, (src->koff.p ? (src->n + 1) : 0) * 8,
-                               hipMemcpyDeviceToDevice, dst->st));
+        if (src->koff.p)
+            MKV_HIP(hipMemcpyAsync(ko, src->koff.p, (src->nstore + 1) * 8, hipMemcpyDeviceToDevice, dst->st));
         if (src->n) {
+            MKV_HIP(hipMemcpyAsync(pm, src->perm.p, src->n * 4, hipMemcpyDeviceToDevice, dst->st));
             MKV_HIP(hipMemcpyAsync(pf, src->pfx.p, src->n * 8, hipMemcpyDeviceToDevice, dst->st));
             MKV_HIP(hipMemcpyAsync(nd, src->nodes.p, nn * 32, hipMemcpyDeviceToDevice, dst->st));
         }
         MKV_HIP(hipStreamSynchronize(dst->st));
         dst->n = src->n;
+        dst->nstore = src->nstore;
         dst->kbytes = src->kbytes;
         dst->lev_cnt = src->lev_cnt;
         dst->lev_off = src->lev_off;
@@ -514,13 +558,13 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
 }
 
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
-                              const uint64_t *voff, uint64_t n) {
+                              const uint64_t *voff, uint64_t n, bool staged, uint64_t staged_kbytes) {
     size_t ptot = prof_begin(t, "total_build");
     uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
     size_t pl = prof_begin(t, "leaf_hash");
     launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
     prof_end(t, pl);
-    sort_dedup_gather(t, kb, koff, n, nullptr);
+    sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes);
     finish_unsharded(t);
     prof_end(t, ptot);
     sync(t);
@@ -543,7 +587,7 @@ mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         upload_blob(t, keys, t->s_kb, t->s_koff);
         upload_blob(t, values, t->s_vb, t->s_voff);
         build_from_staged(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), t->s_vb.as<uint8_t>(),
-                          t->s_voff.as<uint64_t>(), n);
+                          t->s_voff.as<uint64_t>(), n, true, kbn);
     });
 }
 
@@ -554,14 +598,15 @@ mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         NEED(keys.n < 0xFFFFFFF0ull, "too many records");
         NEED(keys.n == 0 || (keys.offsets && values.offsets), "null offsets");
         DevGuard g(t->dev);
-        build_from_staged(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n);
+        build_from_staged(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n, false, 0);
     });
 }
 
 static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
     size_t ptot = prof_begin(t, "total_build");
-    const uint64_t tot = stage_batch(t, keys, values, is_remove);
-    sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb);
+    uint64_t kbytes = 0;
+    const uint64_t tot = stage_batch(t, keys, values, is_remove, &kbytes);
+    sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb, true, kbytes);
     finish_unsharded(t);
     prof_end(t, ptot);
     sync(t);
@@ -660,12 +705,14 @@ mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *diges
         DevGuard g(t->dev);
         if (keys) {
             auto *l = new mkv_keylist();
+            mkv_tree *tm = const_cast<mkv_tree *>(t);
+            const uint64_t bytes = pack_sorted_keys(tm, tm->d_out, tm->d_outoff, 0, 0);
             l->offsets.resize(t->n + 1, 0);
-            l->bytes.resize(t->kbytes);
+            l->bytes.resize(bytes);
             if (t->n) {
-                MKV_HIP(hipMemcpyAsync(l->offsets.data(), t->koff.p, (t->n + 1) * 8, hipMemcpyDeviceToHost, t->st));
-                if (t->kbytes)
-                    MKV_HIP(hipMemcpyAsync(l->bytes.data(), t->kb.p, t->kbytes, hipMemcpyDeviceToHost, t->st));
+                MKV_HIP(hipMemcpyAsync(l->offsets.data(), tm->d_outoff.p, (t->n + 1) * 8, hipMemcpyDeviceToHost,
+                                       t->st));
+                if (bytes) MKV_HIP(hipMemcpyAsync(l->bytes.data(), tm->d_out.p, bytes, hipMemcpyDeviceToHost, t->st));
             }
             MKV_HIP(hipStreamSynchronize(t->st));
             *keys = l;
@@ -681,6 +728,7 @@ static DiffSide side_of(const mkv_tree *t) {
     DiffSide s;
     s.kb = t->kb.as<uint8_t>();
     s.koff = t->koff.as<uint64_t>();
+    s.perm = t->perm.as<uint32_t>();
     s.pfx = t->pfx.as<uint64_t>();
     s.dig = t->nodes.as<uint8_t>();
     s.n = t->n;
@@ -787,6 +835,7 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         const uint64_t n = keys.n;
         const uint8_t *kb, *vb;
         const uint64_t *koff, *voff;
+        uint64_t staged_kbytes = 0;
         if (on_device) {
             kb = keys.bytes;
             koff = keys.offsets;
@@ -807,13 +856,14 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
             koff = t->s_koff.as<uint64_t>();
             vb = t->s_vb.as<uint8_t>();
             voff = t->s_voff.as<uint64_t>();
+            staged_kbytes = kbn;
         }
         size_t ptot = prof_begin(t, "total_build");
         uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
         size_t pl = prof_begin(t, "leaf_hash");
         launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
         prof_end(t, pl);
-        sort_dedup_gather(t, kb, koff, n, nullptr);
+        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes);
         prof_end(t, ptot);
         sync(t);
         t->prepared = true;
