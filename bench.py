@@ -58,8 +58,8 @@ def main():
     torch.cuda.set_device(local)
 
     from merklekv_amd import MerkleTree
-    from merklekv_amd._lib import FRINGE_BYTES
     from merklekv_amd.merkle import gen_records_device
+    from merklekv_amd.shard import sharded_root
 
     n = args.n
     kb = torch.empty(n * KLEN + 64, dtype=torch.uint8, device=dev)
@@ -81,18 +81,9 @@ def main():
         if world == 1:
             tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
             return tree.get_root_hash()
-        nl = tree.shard_prepare((kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), None,
-                                on_device=True)
-        cnt = torch.tensor([nl], dtype=torch.int64, device=dev)
-        allc = torch.empty(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(allc, cnt)
-        counts = allc.tolist()
-        off, total = sum(counts[:rank]), sum(counts)
-        tree.shard_reduce(off, total)
-        fr = torch.frombuffer(bytearray(tree.shard_fringe()), dtype=torch.uint8).to(dev)
-        allf = torch.empty(world * FRINGE_BYTES, dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(allf, fr)
-        return tree.shard_combine(bytes(allf.cpu().numpy()), world, total)
+        root, _ = sharded_root(tree, (kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), None,
+                               dist, device=dev, on_device=True)
+        return root
 
     for _ in range(args.warmup):
         root = step()

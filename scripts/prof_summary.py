@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/gpu_prof.sh run (gpurun_out/prof) into profiles/:
+  <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  <tag>_pmc.json           per-kernel averages of every PMC counter collected + derived metrics
+  pmc_leaf_hash.json       HBM bytes per k_leaf_hash launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction)
+Usage: python scripts/prof_summary.py <tag> [n_records]
+"""
+import collections
+import csv
+import json
+import os
+import re
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "gpurun_out", "prof")
+OUT = os.path.join(ROOT, "profiles")
+
+
+def kname(s):
+    m = re.search(r"(k_[a-z0-9_]+)", s)
+    return m.group(1) if m else s.split("(")[0][:40]
+
+
+def main():
+    tag = sys.argv[1]
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
+    os.makedirs(OUT, exist_ok=True)
+    stats = os.path.join(PROF, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(OUT, f"{tag}_kernel_stats.csv"))
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for d in sorted(os.listdir(PROF)):
+        f = os.path.join(PROF, d, "run_counter_collection.csv")
+        if d.startswith("pmc") and os.path.exists(f):
+            for r in csv.DictReader(open(f)):
+                dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                agg[kname(r["Kernel_Name"])][r["Counter_Name"]].append((float(r["Counter_Value"]), dur))
+    summary = {}
+    for k, d in agg.items():
+        e = {c: sum(v for v, _ in vals) / len(vals) for c, vals in d.items()}
+        e["avg_duration_us"] = sum(t for vals in d.values() for _, t in vals) / sum(len(v) for v in d.values()) / 1e3
+        if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
+            e["hbm_bytes_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+        if "GRBM_GUI_ACTIVE" in e:
+            e["eff_clock_ghz"] = e["GRBM_GUI_ACTIVE"] / 8 / (e["avg_duration_us"] * 1e-6) / 1e9
+            if "SQ_INSTS_VALU" in e:
+                cycles = e["avg_duration_us"] * 1e-6 * e["eff_clock_ghz"] * 1e9
+                e["valu_busy_frac"] = e["SQ_INSTS_VALU"] * 2 / 1024 / cycles  # wave64 VALU = 2 cycles on SIMD32
+        if "SQ_WAIT_INST_ANY" in e and "SQ_WAVE_CYCLES" in e:
+            e["issue_stall_frac"] = e["SQ_WAIT_INST_ANY"] / e["SQ_WAVE_CYCLES"]
+        summary[k] = e
+    json.dump(summary, open(os.path.join(OUT, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
+    lh = summary.get("k_leaf_hash")
+    if lh and "hbm_bytes_corrected" in lh:
+        json.dump({"n": n, "hbm_bytes_per_launch": lh["hbm_bytes_corrected"], "source": f"{tag}_pmc.json",
+                   "algorithmic_bytes_per_launch": 172 * n,
+                   "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes"},
+                  open(os.path.join(OUT, "pmc_leaf_hash.json"), "w"), indent=1)
+    for k in sorted(summary, key=lambda k: -summary[k].get("avg_duration_us", 0))[:8]:
+        e = summary[k]
+        print(f"{k:24s} {e['avg_duration_us']:9.1f} us  valu_busy={e.get('valu_busy_frac', 0):.2f} "
+              f"stall={e.get('issue_stall_frac', 0):.2f} clk={e.get('eff_clock_ghz', 0):.2f} "
+              f"hbm={e.get('hbm_bytes_corrected', 0) / 1e6:.0f} MB")
+
+
+if __name__ == "__main__":
+    main()

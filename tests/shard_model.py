@@ -1,0 +1,99 @@
+"""Pure-Python model of a shard tree (TEST INFRASTRUCTURE): same protocol and fringe byte format as
+mkv_shard_prepare / _reduce / _fringe / _combine, computed with the hashlib oracle. Lets the
+torch.distributed orchestration in merklekv_amd/shard.py and the seam math be tested on CPU with gloo.
+"""
+from __future__ import annotations
+
+import struct
+
+from oracle.merkle_oracle import PyMerkleTree, node_hash
+
+ENTRY = struct.Struct("<IIQ32s")  # level, valid, idx, digest  (MKV_FRINGE_ENTRY_BYTES = 48)
+MAX_ENTRIES = 130
+
+
+def plan_levels(o: int, n: int, N: int):
+    """(base, count, size) per level: the owned global node range of a shard (tree.cpp plan_levels)."""
+    out = []
+    if N == 0:
+        return out
+    a, e, S = o, o + n, N
+    while True:
+        out.append((a, max(0, e - a), S))
+        if S == 1:
+            break
+        a, e, S = (a + 1) // 2, ((e + 1) // 2 if e == S else e // 2), (S + 1) // 2
+    return out
+
+
+class ModelShardTree:
+    def shard_prepare(self, keys, values, on_device=False):
+        t = PyMerkleTree()
+        for k, v in zip(keys, values):
+            t.insert(k, v)
+        self.leaves = [h for _, h in t.leaves()]
+        return len(self.leaves)
+
+    def shard_reduce(self, offset, total):
+        self.plan = plan_levels(offset, len(self.leaves), total)
+        self.levels = [list(self.leaves)]
+        for l in range(1, len(self.plan)):
+            a, c, _ = self.plan[l]
+            pa, _, pS = self.plan[l - 1]
+            prev = self.levels[-1]
+            cur = []
+            for j in range(a, a + c):
+                c0 = 2 * j - pa
+                cur.append(node_hash(prev[c0], prev[c0 + 1]) if 2 * j + 1 < pS else prev[c0])
+            self.levels.append(cur)
+
+    def shard_fringe(self) -> bytes:
+        ents = []
+        L = len(self.plan)
+        for l, (a, c, _) in enumerate(self.plan):
+            if not c:
+                continue
+            for x in sorted({a, a + c - 1}):
+                owned_parent = False
+                if l + 1 < L:
+                    a2, c2, _ = self.plan[l + 1]
+                    owned_parent = a2 <= x // 2 < a2 + c2
+                if not owned_parent:
+                    ents.append(ENTRY.pack(l, 1, x, self.levels[l][x - a]))
+        assert len(ents) <= MAX_ENTRIES
+        return b"".join(ents) + b"\0" * (ENTRY.size * (MAX_ENTRIES - len(ents)))
+
+    def shard_combine(self, fringes: bytes, world: int, total: int):
+        if total == 0:
+            return None
+        ents = []
+        for r in range(world):
+            blk = fringes[r * ENTRY.size * MAX_ENTRIES:(r + 1) * ENTRY.size * MAX_ENTRIES]
+            for i in range(MAX_ENTRIES):
+                lv, valid, idx, h = ENTRY.unpack_from(blk, i * ENTRY.size)
+                if not valid:
+                    break
+                ents.append((lv, idx, h))
+        ents.sort()
+        S = []
+        s = total
+        while True:
+            S.append(s)
+            if s == 1:
+                break
+            s = (s + 1) // 2
+        cur: list[tuple[int, bytes]] = []
+        for l in range(len(S)):
+            computed = []
+            if l > 0:
+                for i, (x, h) in enumerate(cur):
+                    if x % 2:
+                        continue
+                    if x + 1 < S[l - 1]:
+                        assert i + 1 < len(cur) and cur[i + 1][0] == x + 1, "seam sibling missing"
+                        computed.append((x // 2, node_hash(h, cur[i + 1][1])))
+                    else:
+                        computed.append((x // 2, h))
+            cur = sorted(computed + [(idx, h) for lv, idx, h in ents if lv == l])
+        assert len(cur) == 1
+        return cur[0][1]

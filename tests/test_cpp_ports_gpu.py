@@ -1,0 +1,22 @@
+"""Runs the C++ ports of merkle.rs's 56 tests (tests/cpp/test_merkle_ref.cpp, built by
+__graft_entry__.build()) against the HIP library through include/mkv_merkle.hpp."""
+import os
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "tests", "cpp", "test_merkle_ref")
+
+
+def test_cpp_reference_ports():
+    if not os.path.exists(BIN):
+        import __graft_entry__
+        __graft_entry__.build_cpp_tests()
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=600)
+    print(r.stdout[-4000:])
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    assert "56 tests, 0 failed" in r.stdout

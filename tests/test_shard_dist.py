@@ -1,0 +1,111 @@
+"""Multi-process (gloo, CPU) tests of the sharded build protocol: merklekv_amd/shard.py orchestration
+(all-gather of counts and seam fringes) over a model shard tree; the global root must equal the
+unsharded root for uneven, odd-aligned, tiny and empty shards."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from oracle.merkle_oracle import PyMerkleTree
+from tests.shard_model import ModelShardTree, plan_levels
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _split(keys, cuts):
+    ks = sorted(keys)
+    out, prev = [], 0
+    for c in list(cuts) + [len(ks)]:
+        out.append(ks[prev:c])
+        prev = c
+    return out
+
+
+def _worker(rank, world, port, shards, values, q):
+    import torch.distributed as dist
+
+    from merklekv_amd.shard import sharded_root
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        keys = shards[rank]
+        root, counts = sharded_root(ModelShardTree(), keys, [values[k] for k in keys], dist, device="cpu")
+        q.put((rank, root, counts))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, shards, values):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shards, values, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(res)
+
+
+@pytest.mark.parametrize("world,n,cuts", [
+    (2, 1000, [500]),
+    (2, 1001, [333]),
+    (3, 777, [1, 400]),
+    (2, 64, [0]),          # empty first shard
+    (3, 5, [2, 2]),        # empty middle shard
+])
+def test_sharded_root_matches_unsharded_gloo(world, n, cuts):
+    keys = [b"key%05d" % i for i in range(n)]
+    values = {k: b"val" + k for k in keys}
+    ref = PyMerkleTree()
+    for k in keys:
+        ref.insert(k, values[k])
+    shards = _split(keys, cuts)
+    res = _run(world, shards, values)
+    for rank, root, counts in res:
+        assert counts == [len(s) for s in shards]
+        assert root == ref.get_root_hash(), rank
+
+
+def test_seam_model_exhaustive_small():
+    """Every split point of every size up to 40 into 2 and 3 shards (no processes)."""
+    import itertools
+    for n in range(1, 41):
+        keys = [b"k%03d" % i for i in range(n)]
+        ref = PyMerkleTree()
+        for k in keys:
+            ref.insert(k, k)
+        want = ref.get_root_hash()
+        for g in (2, 3):
+            for cuts in itertools.combinations(range(n + 1), g - 1):
+                shards = _split(keys, cuts)
+                trees = [ModelShardTree() for _ in shards]
+                counts = [t.shard_prepare(s, s) for t, s in zip(trees, shards)]
+                fr = b""
+                for r, t in enumerate(trees):
+                    t.shard_reduce(sum(counts[:r]), n)
+                    fr += t.shard_fringe()
+                for t in trees:
+                    assert t.shard_combine(fr, g, n) == want, (n, cuts)
+
+
+def test_plan_levels_single_shard_is_whole_tree():
+    for n in (1, 2, 3, 7, 1000, 1025):
+        p = plan_levels(0, n, n)
+        s, sizes = n, []
+        while True:
+            sizes.append(s)
+            if s == 1:
+                break
+            s = (s + 1) // 2
+        assert [c for _, c, _ in p] == sizes and [b for b, _, _ in p] == [0] * len(sizes)
