@@ -110,7 +110,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
     leaf_ms, leaf_cnt = tree.prof_read("leaf_hash")
-    groups = {g: tree.prof_read(g) for g in ("leaf_hash", "sort", "gather", "reduce", "total_build")}
+    groups = {g: tree.prof_read(g) for g in ("leaf_hash", "sort", "keycopy", "gather", "reduce", "total_build")}
     leaf_avg_ms = leaf_ms / max(leaf_cnt, 1)
     achieved = LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9
     hashed_gbs = (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9

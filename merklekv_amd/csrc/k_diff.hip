@@ -12,6 +12,8 @@
 //   scan    exclusive scan of tile counts;
 //   pass 2  ballot/LDS compaction writes (side, index) refs of divergent keys in merged = sorted order.
 // Ties on the 8-byte prefix fall back to a full-key compare in HBM (key_cmp), so any key set is exact.
+#include <algorithm>
+
 #include "common.hpp"
 #include "dev_util.hpp"
 #include "kernels.hpp"
@@ -255,6 +257,43 @@ __global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, 
     lohi[1] = l2;
 }
 
+// ---- top-down diff (equal leaf counts): expand the divergent frontier one level down ----
+// frontier_in holds node indices of level l whose digests differ between the trees; children (l-1)
+// whose digests differ are appended to frontier_out (wave-aggregated: one atomic per wave).
+__global__ __launch_bounds__(256) void k_topdown_level(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
+                                                      uint64_t child_count, const uint32_t *__restrict__ fin,
+                                                      const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
+                                                      uint32_t *__restrict__ nout) {
+    const uint32_t cnt = *nin;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < 2ull * cnt; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;  // two candidate children per frontier node
+        bool d = false;
+        uint32_t c = 0;
+        if (t < 2ull * cnt) {
+            c = 2u * fin[t >> 1] + (uint32_t)(t & 1);
+            if (c < child_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
+        }
+        const uint64_t m = __ballot(d);
+        uint32_t slot = 0;
+        if (lane == 0 && m) slot = atomicAdd(nout, (uint32_t)__popcll(m));
+        slot = __shfl(slot, 0);
+        if (d) fout[slot + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = c;
+    }
+}
+
+// Divergent leaf positions (sorted): refs of keys equal on both sides; counts positions whose keys
+// differ (then the key sets differ there and the caller falls back to the merge-join).
+__global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, DiffSide A, DiffSide B,
+                                 uint64_t *__restrict__ refs, uint32_t *__restrict__ nbad) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t i = pos[k];
+    const bool same = cmp_ab(A, i, A.pfx[i], B, i, B.pfx[i]) == 0;
+    refs[k] = i;
+    if (!same) atomicAdd(nbad, 1u);
+}
+
 __global__ void k_widen_u32(const uint32_t *__restrict__ c, uint64_t *__restrict__ o, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) o[i] = c[i];
@@ -300,6 +339,21 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);
     exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
     hipLaunchKernelGGL(k_diff_pass2, dim3((uint32_t)nt), dim3(DT), 0, st, A, B, split, packed, tileoff, refs);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, const uint32_t *fin,
+                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_frontier, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * (max_frontier ? max_frontier : 1), 256), 2048);
+    hipLaunchKernelGGL(k_topdown_level, dim3((uint32_t)blocks), dim3(256), 0, st, ca, cb, child_count, fin, nin, fout,
+                       nout);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
+                           uint32_t *nbad, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_topdown_leaves, grid1d(m), dim3(256), 0, st, pos, m, A, B, refs, nbad);
     MKV_LAUNCH_CHECK();
 }
 

@@ -24,7 +24,9 @@ namespace mkv {
 namespace {
 
 constexpr int LEAF_WAVES = 4;                 // waves per workgroup
-constexpr uint32_t LEAF_LDS_WAVE = 10240;     // bytes of LDS per wave (4 waves -> 40 KiB per WG)
+// LDS per wave: 64 x 132-B records + alignment slack (8,512 B) fit; 4 waves -> 36 KiB per WG, so four
+// leaf workgroups (144 KiB) leave room on the CU for a sort workgroup running on the aux stream.
+constexpr uint32_t LEAF_LDS_WAVE = 9216;
 
 // Big-endian word of the 4 bytes at byte offset `off` of an LDS byte region starting at `base` (bytes).
 __device__ __forceinline__ uint32_t lds_be_word(const uint32_t *lds, uint32_t byte) {
@@ -92,7 +94,7 @@ __device__ __forceinline__ uint32_t msg_word(const Src &src, uint32_t p, uint32_
     return w;
 }
 
-template <class Src>
+template <bool SHORT, class Src>
 __device__ __forceinline__ void hash_generic(const Src &src, uint32_t klen, uint32_t vlen, uint32_t out[8]) {
     uint32_t L = 8 + klen + vlen;
     uint32_t nb = (L + 9 + 63) >> 6;
@@ -106,12 +108,13 @@ __device__ __forceinline__ void hash_generic(const Src &src, uint32_t klen, uint
             w[14] |= (uint32_t)(bits >> 32);
             w[15] |= (uint32_t)bits;
         }
-        sha_compress(out, w);
+        sha_compress<SHORT>(out, w);
     }
 }
 
 // Fast path: K0 = |k|, V0 = |v| wave-uniform multiples of 4, data 4-aligned in LDS. Word g of the
 // message is: 0 -> K0 | 1..K0/4 -> key | K0/4+1 -> V0 | .. -> value | L/4 -> 0x80000000 | 0.
+template <bool SHORT>
 __device__ __forceinline__ void hash_fast(const uint32_t *lds, uint32_t kword, uint32_t vword, uint32_t K0,
                                           uint32_t V0, uint32_t out[8]) {
     const uint32_t kw = K0 >> 2, vw = V0 >> 2;
@@ -138,10 +141,11 @@ __device__ __forceinline__ void hash_fast(const uint32_t *lds, uint32_t kword, u
             w[14] = (uint32_t)(bits >> 32);
             w[15] = (uint32_t)bits;
         }
-        sha_compress(out, w);
+        sha_compress<SHORT>(out, w);
     }
 }
 
+template <bool SHORT>
 __global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                   const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
                                                   uint64_t n, uint8_t *__restrict__ out) {
@@ -191,15 +195,15 @@ __global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ k
         const uint32_t K0 = __shfl(klen, 0), V0 = __shfl(vlen, 0);
         const bool mine = klen == K0 && vlen == V0 && ((K0 | V0 | kbyte | vbyte) & 3) == 0;
         if (__all(mine)) {
-            hash_fast(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
+            hash_fast<SHORT>(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
                       __builtin_amdgcn_readfirstlane(V0), st);
         } else {
             LdsSrc src{lds, kbyte, vbyte};
-            hash_generic(src, klen, vlen, st);
+            hash_generic<SHORT>(src, klen, vlen, st);
         }
     } else {
         GlbSrc src{kb + kbeg, vb + vbeg, kb + kend, vb + vend};
-        hash_generic(src, klen, vlen, st);
+        hash_generic<SHORT>(src, klen, vlen, st);
     }
     store_digest(out + 32 * r, st);
 }
@@ -211,7 +215,12 @@ void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
     if (n == 0) return;
     uint64_t waves = ceil_div(n, 64);
     uint64_t blocks = ceil_div(waves, LEAF_WAVES);
-    hipLaunchKernelGGL(k_leaf_hash, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff, n, out);
+    if (sha_variant() == 0)
+        hipLaunchKernelGGL(k_leaf_hash<false>, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff,
+                           n, out);
+    else
+        hipLaunchKernelGGL(k_leaf_hash<true>, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff,
+                           n, out);
     MKV_LAUNCH_CHECK();
 }
 

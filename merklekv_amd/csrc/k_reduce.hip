@@ -27,6 +27,7 @@ namespace {
 constexpr int RD_THREADS = 512;
 constexpr int RD_TILE = 512;
 
+template <bool SHORT>
 __global__ __launch_bounds__(RD_THREADS) void k_reduce_fused(FusePlan p) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
     const uint64_t t = p.tile0 + blockIdx.x;
@@ -52,7 +53,7 @@ __global__ __launch_bounds__(RD_THREADS) void k_reduce_fused(FusePlan p) {
                 }
             }
             if (pair) {
-                sha_node(l, r, o);
+                sha_node<SHORT>(l, r, o);
             } else {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) o[q] = l[q];  // R5: promote unchanged
@@ -164,7 +165,10 @@ __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict
 
 void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
-    hipLaunchKernelGGL(k_reduce_fused, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
+    if (sha_variant() == 0)
+        hipLaunchKernelGGL(k_reduce_fused<false>, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
+    else
+        hipLaunchKernelGGL(k_reduce_fused<true>, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 

@@ -38,33 +38,55 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
     idx[i] = (uint32_t)i;
 }
 
-__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const uint64_t *__restrict__ keys, uint64_t n, int shift,
-                                                       uint32_t *__restrict__ counts, uint32_t nblocks) {
-    __shared__ uint32_t h[4][256];
-    for (int i = threadIdx.x; i < 1024; i += RS_THREADS) (&h[0][0])[i] = 0;
+// ---- onesweep LSD radix pass ----
+// Look-back word per (tile, digit): [31:30] status (0 not ready, 1 aggregate, 2 inclusive), [29:0] count.
+constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_VAL = (1u << 30) - 1u;
+constexpr uint32_t LB_SPIN_LIMIT = 1u << 26;  // bounded spin: sets an error flag instead of hanging
+
+// Global digit counts of every pass in one read of the keys (counts[p*256 + d]).
+__global__ __launch_bounds__(RS_THREADS) void k_os_hist(const uint64_t *__restrict__ keys, uint64_t n, int bit0,
+                                                       int npass, uint32_t *__restrict__ counts) {
+    __shared__ uint32_t h[8][256];
+    for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
     __syncthreads();
-    const int w = threadIdx.x >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + threadIdx.x;
-#pragma unroll
-    for (int s = 0; s < RS_IPT; ++s) {
-        uint64_t i = base + (uint64_t)s * RS_THREADS;
-        if (i < n) atomicAdd(&h[w][(uint32_t)(keys[i] >> shift) & 255u], 1u);
+    const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS;
+    for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
+        const uint64_t k = keys[i];
+        for (int p = 0; p < npass; ++p) atomicAdd(&h[p][(uint32_t)(k >> (bit0 + 8 * p)) & 255u], 1u);
     }
     __syncthreads();
-    const uint32_t d = threadIdx.x;
-    counts[(uint64_t)d * nblocks + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+    for (int i = threadIdx.x; i < npass * 256; i += RS_THREADS) {
+        const uint32_t c = (&h[0][0])[i];
+        if (c) atomicAdd(&counts[i], c);
+    }
 }
 
-__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const uint64_t *__restrict__ kin,
-                                                          const uint32_t *__restrict__ vin,
-                                                          uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
-                                                          uint64_t n, int shift, const uint32_t *__restrict__ offs,
-                                                          uint32_t nblocks) {
+// One stable pass over 4096-pair tiles. Tiles take logical ids from an atomic counter in dispatch
+// order, so a tile only ever waits on tiles that are already running or done (no deadlock whatever
+// the hardware dispatch order). Ranks: 8 ballots per slot give each lane its peers with the same
+// digit; per-wave LDS counters make them tile ranks. The tile publishes its digit counts, looks back
+// over predecessors' words (agent-scope atomics: coherent across XCD L2s and CU L1s), sorts itself
+// in LDS by digit and writes each digit run contiguously (coalesced) to its global slot.
+__global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restrict__ kin,
+                                                       const uint32_t *__restrict__ vin,
+                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
+                                                       uint64_t n, int shift, const uint32_t *__restrict__ gcount,
+                                                       uint32_t *__restrict__ lookback, uint32_t *__restrict__ ctl) {
+    __shared__ uint64_t sk[RS_TILE];
+    __shared__ uint32_t sv[RS_TILE];
     __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint64_t gofs[256];
+    __shared__ uint32_t scan_lds[16];
+    __shared__ uint64_t scan_lds64[16];
+    __shared__ uint32_t sbid;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) sbid = atomicAdd(&ctl[0], 1u);
     for (int i = threadIdx.x; i < 1024; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * RS_TILE + (uint64_t)w * RS_WAVE_ITEMS + lane;
+    const uint32_t bid = sbid;
+    const uint64_t tile0 = (uint64_t)bid * RS_TILE;
+    const uint64_t base = tile0 + (uint64_t)w * RS_WAVE_ITEMS + lane;
     const uint64_t lt = (1ull << lane) - 1ull;
     uint64_t key[RS_IPT];
     uint32_t val[RS_IPT];
@@ -96,26 +118,63 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const uint64_t *__res
         rk[s] = before + r;
     }
     __syncthreads();
-    {
-        const uint32_t d = threadIdx.x;
-        uint32_t run = offs[(uint64_t)d * nblocks + blockIdx.x];
+    // ---- per digit (thread d): tile count, wave prefixes, publish, look back ----
+    const uint32_t d = threadIdx.x;
+    uint32_t c = 0;
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) {
-            uint32_t c = wcnt[ww][d];
-            wcnt[ww][d] = run;
-            run += c;
-        }
+    for (int ww = 0; ww < 4; ++ww) {
+        const uint32_t x = wcnt[ww][d];
+        wcnt[ww][d] = c;  // exclusive prefix over waves
+        c += x;
     }
+    if (bid == 0) __hip_atomic_exchange(&lookback[d], LB_INC | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], LB_AGG | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ds = block_excl_scan<uint32_t>(c, scan_lds, nullptr);
+    const uint64_t gb = block_excl_scan<uint64_t>((uint64_t)gcount[d], scan_lds64, nullptr);
+    dstart[d] = ds;
+    uint64_t excl = 0;
+    if (bid > 0) {
+        int64_t j = (int64_t)bid - 1;
+        uint32_t spins = 0;
+        while (j >= 0) {
+            const uint32_t v = __hip_atomic_fetch_add(&lookback[(uint64_t)j * 256 + d], 0u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t stt = v >> 30;
+            if (stt == 0) {
+                if (++spins > LB_SPIN_LIMIT) {
+                    atomicOr(&ctl[1], 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += v & LB_VAL;
+            if (stt == 2) break;
+            --j;
+        }
+        __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], LB_INC | (uint32_t)(excl + c), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+    gofs[d] = gb + excl - ds;  // output position = gofs[digit] + local sorted position
     __syncthreads();
+    // ---- local sort in LDS (stable: wave-major, slot, lane order) ----
 #pragma unroll
     for (int s = 0; s < RS_IPT; ++s) {
         const uint64_t i = base + (uint64_t)s * 64;
         if (i < n) {
-            const uint32_t d = (uint32_t)(key[s] >> shift) & 255u;
-            const uint32_t pos = wcnt[w][d] + rk[s];
-            kout[pos] = key[s];
-            vout[pos] = val[s];
+            const uint32_t dd = (uint32_t)(key[s] >> shift) & 255u;
+            const uint32_t lp = dstart[dd] + wcnt[w][dd] + rk[s];
+            sk[lp] = key[s];
+            sv[lp] = val[s];
         }
+    }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)(n - tile0 < RS_TILE ? n - tile0 : RS_TILE);
+    for (uint32_t p = threadIdx.x; p < cnt; p += RS_THREADS) {
+        const uint64_t k = sk[p];
+        const uint64_t pos = gofs[(uint32_t)(k >> shift) & 255u] + p;
+        kout[pos] = k;
+        vout[pos] = sv[p];
     }
 }
 
@@ -363,23 +422,31 @@ void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64
 size_t scan_scratch_bytes(uint64_t n) { return (ceil_div(n ? n : 1, SC_TILE) + 16) * sizeof(uint64_t); }
 
 size_t radix_scratch_bytes(uint64_t n) {
-    uint64_t nb = ceil_div(n ? n : 1, RS_TILE);
-    return 256 * nb * sizeof(uint32_t) + 256 + scan_scratch_bytes(256 * nb);
+    const uint64_t nb = ceil_div(n ? n : 1, RS_TILE);
+    // digit counts (8 x 256) + control words (8 passes x 4) + look-back words (8 passes x tiles x 256)
+    return (8 * 256 + 64 + 8ull * nb * 256) * sizeof(uint32_t) + 1024 + scan_scratch_bytes(n);
 }
 
 bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, int bit0, int bit1,
                       void *scratch, hipStream_t st) {
     if (n <= 1 || bit1 <= bit0) return false;
-    uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
+    if (n >= (1ull << 30)) throw Error(ST_EINVAL, "radix sort: more than 2^30 - 1 keys per device");
+    const uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
+    const int npass = (bit1 - bit0 + 7) / 8;
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
-    void *sc = reinterpret_cast<uint8_t *>(scratch) + ((256ull * nb * sizeof(uint32_t) + 255) & ~255ull);
+    uint32_t *ctl = counts + 8 * 256;
+    uint32_t *lookback = ctl + 64;
+    const size_t zero_words = 8 * 256 + 64 + (size_t)npass * nb * 256;
+    MKV_HIP(hipMemsetAsync(counts, 0, zero_words * sizeof(uint32_t), st));
+    const uint32_t hist_blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 16), 2048);
+    hipLaunchKernelGGL(k_os_hist, dim3(hist_blocks), dim3(RS_THREADS), 0, st, k, n, bit0, npass, counts);
+    MKV_LAUNCH_CHECK();
     uint64_t *ki = k, *ko = k2;
     uint32_t *vi = v, *vo = v2;
     bool swapped = false;
-    for (int shift = bit0; shift < bit1; shift += 8) {
-        hipLaunchKernelGGL(k_rs_hist, dim3(nb), dim3(RS_THREADS), 0, st, ki, n, shift, counts, nb);
-        scan_impl<uint32_t>(counts, counts, 256ull * nb, nullptr, sc, st);
-        hipLaunchKernelGGL(k_rs_scatter, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, shift, counts, nb);
+    for (int p = 0; p < npass; ++p) {
+        hipLaunchKernelGGL(k_os_pass, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
+                           counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
         MKV_LAUNCH_CHECK();
         std::swap(ki, ko);
         std::swap(vi, vo);

@@ -97,6 +97,11 @@ size_t diff_scratch_bytes(uint64_t nmerged);
 // in sorted order; *count (device) receives the number. Returns nothing; host reads count.
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
                  hipStream_t st);
+// Top-down diff for trees with equal leaf counts (identical level shapes).
+void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, const uint32_t *fin,
+                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_frontier, hipStream_t st);
+void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
+                           uint32_t *nbad, hipStream_t st);
 void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
                          hipStream_t st);
 void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,

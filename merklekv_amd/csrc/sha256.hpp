@@ -85,9 +85,53 @@ __device__ __forceinline__ void sha_init(uint32_t s[8]) {
     for (int i = 0; i < 8; ++i) s[i] = h256(i);
 }
 
+__device__ __forceinline__ uint32_t add3_asm(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t add3_asm_s(uint32_t a, uint32_t k, uint32_t c) {
+    uint32_t r;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t add_asm(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// One SHA-256 round. Variant SHORT (true): hkw = h + K + W and dhkw = d + hkw depend only on values
+// known a round earlier, so new e = Σ1(e) + Ch(e,f,g) + dhkw and new a = T1 + Σ0(a) + Maj(a,b,c) are
+// alignbit -> bitop3 -> add3 (3 dependent VALU levels) from the previous state; the association is
+// pinned with inline asm because LLVM re-associates the sums back into a 5-level chain
+// (add3(w,h,Σ1) -> add3(.,Ch,K) -> +d). Variant false: plain C, LLVM's own association.
+// Registers rotate by renaming: the new a goes into h's slot and the new e into d's slot.
+template <bool SHORT>
+__device__ __forceinline__ void sha_round(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                          uint32_t &f, uint32_t &g, uint32_t &h, uint32_t k, uint32_t w) {
+    if constexpr (SHORT) {
+        const uint32_t hkw = add3_asm_s(h, k, w);
+        const uint32_t dhkw = add_asm(d, hkw);
+        const uint32_t s1 = bsig1(e), c1 = ch(e, f, g);
+        const uint32_t t1 = add3_asm(s1, c1, hkw);
+        d = add3_asm(s1, c1, dhkw);
+        h = add3_asm(t1, bsig0(a), maj(a, b, c));
+    } else {
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + k + w;
+        d = d + t1;
+        h = t1 + bsig0(a) + maj(a, b, c);
+    }
+}
+
+#ifndef MKV_SHA_SHORT_DEFAULT
+#define MKV_SHA_SHORT_DEFAULT true
+#endif
+
 // One compression over the 16 big-endian message words in w (w is clobbered: rolling schedule).
+template <bool SHORT = MKV_SHA_SHORT_DEFAULT>
 __device__ __forceinline__ void sha_compress(uint32_t s[8], uint32_t w[16]) {
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+    uint32_t v[8] = {s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
 #pragma unroll
     for (int t = 0; t < 64; ++t) {
         uint32_t wt;
@@ -97,42 +141,32 @@ __device__ __forceinline__ void sha_compress(uint32_t s[8], uint32_t w[16]) {
             wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
             w[t & 15] = wt;
         }
-        uint32_t t1 = h + bsig1(e) + ch(e, f, g) + k256(t) + wt;
-        uint32_t t2 = bsig0(a) + maj(a, b, c);
-        h = g;
-        g = f;
-        f = e;
-        e = d + t1;
-        d = c;
-        c = b;
-        b = a;
-        a = t1 + t2;
+        const int A = (64 - t) & 7;  // slot of a at round t
+        sha_round<SHORT>(v[A], v[(A + 1) & 7], v[(A + 2) & 7], v[(A + 3) & 7], v[(A + 4) & 7], v[(A + 5) & 7],
+                         v[(A + 6) & 7], v[(A + 7) & 7], k256(t), wt);
     }
-    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += v[i];  // 64 % 8 == 0: the renaming is back at the origin
 }
 
 // The constant padding block of a 64-byte message (schedule folded into K+W immediates).
+template <bool SHORT = MKV_SHA_SHORT_DEFAULT>
 __device__ __forceinline__ void sha_compress_pad64(uint32_t s[8]) {
     constexpr Sched64 KW = make_pad64_kw();
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+    uint32_t v[8] = {s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
 #pragma unroll
     for (int t = 0; t < 64; ++t) {
-        uint32_t t1 = h + bsig1(e) + ch(e, f, g) + KW.v[t];
-        uint32_t t2 = bsig0(a) + maj(a, b, c);
-        h = g;
-        g = f;
-        f = e;
-        e = d + t1;
-        d = c;
-        c = b;
-        b = a;
-        a = t1 + t2;
+        const int A = (64 - t) & 7;
+        sha_round<SHORT>(v[A], v[(A + 1) & 7], v[(A + 2) & 7], v[(A + 3) & 7], v[(A + 4) & 7], v[(A + 5) & 7],
+                         v[(A + 6) & 7], v[(A + 7) & 7], KW.v[t], 0u);
     }
-    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += v[i];
 }
 
 // R4 (merkle.rs:99-103): parent = SHA-256(left32 || right32). l/r are the children's digest words
 // already in big-endian word form (i.e. bswapped from the canonical byte order).
+template <bool SHORT = MKV_SHA_SHORT_DEFAULT>
 __device__ __forceinline__ void sha_node(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
     uint32_t w[16];
 #pragma unroll
@@ -141,8 +175,8 @@ __device__ __forceinline__ void sha_node(const uint32_t l[8], const uint32_t r[8
         w[8 + i] = r[i];
     }
     sha_init(out);
-    sha_compress(out, w);
-    sha_compress_pad64(out);
+    sha_compress<SHORT>(out, w);
+    sha_compress_pad64<SHORT>(out);
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }

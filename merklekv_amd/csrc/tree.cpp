@@ -4,6 +4,7 @@
 #include "mkv_merkle.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -16,10 +17,19 @@ using namespace mkv;
 
 static thread_local std::string g_err;
 
+int mkv::sha_variant() {
+    static const int v = [] {
+        const char *e = getenv("MKV_SHA_VARIANT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
 namespace {
 
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
+    hipStream_t s = nullptr;
     std::string group;
     bool closed = false;
 };
@@ -33,7 +43,9 @@ struct mkv_keylist {
 
 struct mkv_tree {
     int dev = 0;
-    hipStream_t st = nullptr;
+    hipStream_t st = nullptr;   // main stream: leaf hashing, digest gather, reduction, diff
+    hipStream_t st2 = nullptr;  // aux stream: key ownership copy, prefix sort, ties, dedup (overlaps st)
+    hipEvent_t ev_in = nullptr, ev_join = nullptr;
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
@@ -58,6 +70,7 @@ struct mkv_tree {
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
+    DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf d_seam, d_S, d_fr;
     uint64_t *h_small = nullptr;  // pinned host scalars
 
@@ -93,14 +106,29 @@ __global__ void k_clear_tomb(const uint8_t *__restrict__ tomb, const uint32_t *_
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n && tomb[perm[i]]) flags[i] = 0;
 }
+__global__ void k_widen_positions(const uint32_t *__restrict__ f, uint64_t m, uint64_t *__restrict__ k,
+                                  uint32_t *__restrict__ v) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) {
+        k[i] = f[i];
+        v[i] = (uint32_t)i;
+    }
+}
+void launch_widen_positions(const uint32_t *f, uint64_t m, uint64_t *k, uint32_t *v, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_widen_positions, dim3((uint32_t)ceil_div(m, 256)), dim3(256), 0, st, f, m, k, v);
+    MKV_LAUNCH_CHECK();
+}
+
 void launch_clear_tomb(const uint8_t *tomb, const uint32_t *perm, uint64_t n, uint32_t *flags, hipStream_t st) {
     if (!n) return;
     hipLaunchKernelGGL(k_clear_tomb, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, tomb, perm, n, flags);
     MKV_LAUNCH_CHECK();
 }
 
-size_t prof_begin(mkv_tree *t, const char *group) {
+size_t prof_begin(mkv_tree *t, const char *group, hipStream_t s = nullptr) {
     if (!t->prof) return SIZE_MAX;
+    if (!s) s = t->st;
     if (t->evfree.empty()) {
         EvPair p;
         MKV_HIP(hipEventCreate(&p.a));
@@ -112,12 +140,13 @@ size_t prof_begin(mkv_tree *t, const char *group) {
     t->evfree.pop_back();
     t->evpool[i].group = group;
     t->evpool[i].closed = false;
-    MKV_HIP(hipEventRecord(t->evpool[i].a, t->st));
+    t->evpool[i].s = s;
+    MKV_HIP(hipEventRecord(t->evpool[i].a, s));
     return i;
 }
 void prof_end(mkv_tree *t, size_t i) {
     if (i == SIZE_MAX) return;
-    MKV_HIP(hipEventRecord(t->evpool[i].b, t->st));
+    MKV_HIP(hipEventRecord(t->evpool[i].b, t->evpool[i].s));
     t->evpool[i].closed = true;
     t->evdone.push_back(i);
 }
@@ -134,7 +163,9 @@ void prof_collect(mkv_tree *t) {
     t->evdone.clear();
 }
 
+// Full completion point of an API call: both streams drained, profiling pairs collected.
 void sync(mkv_tree *t) {
+    MKV_HIP(hipStreamSynchronize(t->st2));
     MKV_HIP(hipStreamSynchronize(t->st));
     prof_collect(t);
 }
@@ -146,14 +177,17 @@ void swap_buf(DevBuf &a, DevBuf &b) {
 
 template <class T> T *ens(DevBuf &b, uint64_t count) { return reinterpret_cast<T *>(b.ensure(count * sizeof(T))); }
 
-uint64_t d2h_u64(mkv_tree *t, const void *dptr) {
-    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint64_t), hipMemcpyDeviceToHost, t->st));
-    sync(t);
+// Scalar readback that waits only for the stream that produced it (the other stream keeps running).
+uint64_t d2h_u64(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
+    if (!s) s = t->st;
+    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    MKV_HIP(hipStreamSynchronize(s));
     return t->h_small[0];
 }
-uint32_t d2h_u32(mkv_tree *t, const void *dptr) {
-    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint32_t), hipMemcpyDeviceToHost, t->st));
-    sync(t);
+uint32_t d2h_u32(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
+    if (!s) s = t->st;
+    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MKV_HIP(hipStreamSynchronize(s));
     return reinterpret_cast<uint32_t *>(t->h_small)[0];
 }
 
@@ -229,7 +263,7 @@ void run_reduce(mkv_tree *t, uint8_t *nodes) {
 // tie[i] = position i equals position i-1 on everything compared so far.
 // ---------------------------------------------------------------------------------------------
 void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint8_t *tie) {
-    hipStream_t st = t->st;
+    hipStream_t st = t->st2;
     uint32_t *flags = ens<uint32_t>(t->s_flags, n + 1);
     uint32_t *scan = ens<uint32_t>(t->s_scan, n + 1);
     uint32_t *pos = ens<uint32_t>(t->s_pos, n + 1);
@@ -240,13 +274,13 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
         launch_active_flags(tie, n, flags, st);
         exclusive_scan_u32(flags, scan, n, misc, radix, st);
         launch_compact_positions(flags, scan, n, pos, st);
-        return d2h_u32(t, misc);
+        return d2h_u32(t, misc, st);
     };
     uint64_t m = active();
     if (m == 0) return;
     MKV_HIP(hipMemsetAsync(misc + 1, 0, 4, st));
     launch_max_keylen(pos, m, perm, koff, misc + 1, st);
-    const uint32_t maxlen = d2h_u32(t, misc + 1);
+    const uint32_t maxlen = d2h_u32(t, misc + 1, st);
     const uint32_t D = (maxlen + 7) / 8;  // chunks; chunk 0 already sorted
 
     for (uint32_t depth = 1;; ++depth) {
@@ -277,7 +311,7 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
         uint32_t *kks = sw2 ? kk_alt : kk;
         MKV_HIP(hipMemsetAsync(misc + 2, 0, 4, st));
         launch_refine_apply(pos, m, kks, permact, chunk + m, perm, tie, misc + 2, st);
-        const uint32_t left = d2h_u32(t, misc + 2);
+        const uint32_t left = d2h_u32(t, misc + 2, st);
         if (left == 0 || use_len) break;
     }
 }
@@ -289,7 +323,9 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
 // ---------------------------------------------------------------------------------------------
 void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
                        bool staged_inputs, uint64_t staged_kbytes) {
-    hipStream_t st = t->st;
+    // Ordering work runs on the aux stream and overlaps the VALU-bound leaf hashing already enqueued on
+    // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
+    hipStream_t st = t->st2;
     const uint8_t *dig = t->s_dig.as<uint8_t>();
     uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
     uint64_t *k2 = ens<uint64_t>(t->s_k2, n_in + 1);
@@ -299,7 +335,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     uint32_t *misc = ens<uint32_t>(t->s_misc, 64);
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n_in), scan_scratch_bytes(n_in + 1)));
 
-    size_t ps = prof_begin(t, "sort");
+    size_t ps = prof_begin(t, "sort", st);
     launch_prefix64(kb, koff, n_in, k1, v1, st);
     const bool sw = radix_sort_pairs(k1, v1, k2, v2, n_in, 0, 64, radix, st);
     DevBuf *pkbuf = sw ? &t->s_k2 : &t->s_k1, *pkalt = sw ? &t->s_k1 : &t->s_k2;
@@ -309,15 +345,15 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     MKV_HIP(hipMemsetAsync(misc, 0, 4, st));
     launch_mark_ties(pk, n_in, tie, misc, st);
     prof_end(t, ps);
-    const uint32_t nties = n_in ? d2h_u32(t, misc) : 0;
+    const uint32_t nties = n_in ? d2h_u32(t, misc, st) : 0;
     if (nties) {
-        size_t pr = prof_begin(t, "sort");
+        size_t pr = prof_begin(t, "sort", st);
         refine_ties(t, kb, koff, n_in, perm, tie);  // reorders perm inside equal-prefix runs only
         prof_end(t, pr);
     }
     uint64_t n = n_in;
     if (nties || tomb) {
-        size_t pd = prof_begin(t, "sort");
+        size_t pd = prof_begin(t, "sort", st);
         uint32_t *flags = ens<uint32_t>(t->s_flags, n_in + 1);
         uint32_t *scan = ens<uint32_t>(t->s_scan, n_in + 1);
         launch_keep_flags(tie, perm, n_in, UINT64_MAX, flags, st);  // dedup: keep the last write
@@ -326,7 +362,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         launch_compact_u32(perm, flags, scan, n_in, pmalt->as<uint32_t>(), st);
         launch_compact_u64(pk, flags, scan, n_in, pkalt->as<uint64_t>(), st);
         prof_end(t, pd);
-        n = d2h_u32(t, misc + 3);
+        n = d2h_u32(t, misc + 3, st);
         std::swap(pkbuf, pkalt);
         std::swap(pmbuf, pmalt);
         perm = pmbuf->as<uint32_t>();
@@ -343,21 +379,30 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         swap_buf(t->koff, t->s_koff);
         t->kbytes = staged_kbytes;
     } else {
-        const uint64_t kbytes = n_in ? d2h_u64(t, koff + n_in) : 0;
+        const uint64_t kbytes = n_in ? d2h_u64(t, koff + n_in, st) : 0;
         uint8_t *dkb = ens<uint8_t>(t->kb, kbytes + 16);
         uint64_t *dko = ens<uint64_t>(t->koff, n_in + 1);
-        size_t pc = prof_begin(t, "gather");
+        size_t pc = prof_begin(t, "keycopy", st);
         if (kbytes) MKV_HIP(hipMemcpyAsync(dkb, kb, kbytes, hipMemcpyDeviceToDevice, st));
         MKV_HIP(hipMemcpyAsync(dko, koff, (n_in + 1) * 8, hipMemcpyDeviceToDevice, st));
         prof_end(t, pc);
         t->kbytes = kbytes;
     }
+    MKV_HIP(hipEventRecord(t->ev_join, st));
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
     size_t pg = prof_begin(t, "gather");
     // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
     // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
     uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
-    launch_gather_digests(perm, dig, n, nodes, st);
+    launch_gather_digests(perm, dig, n, nodes, t->st);
     prof_end(t, pg);
+}
+
+// Inputs staged on t->st become visible to the aux stream; call before enqueueing the leaf hash so the
+// ordering work on st2 overlaps it.
+void fork_streams(mkv_tree *t) {
+    MKV_HIP(hipEventRecord(t->ev_in, t->st));
+    MKV_HIP(hipStreamWaitEvent(t->st2, t->ev_in, 0));
 }
 
 // Sorted keys of the tree packed into (dst_kb, dst_koff[0..n]) starting at byte base; returns bytes.
@@ -434,10 +479,6 @@ uint64_t stage_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, 
         ens<uint8_t>(t->s_vb, vbytes + 16);
         ens<uint64_t>(t->s_voff, nb + 1);
         upload_blob(t, *values, t->s_vb, t->s_voff);
-        size_t pl = prof_begin(t, "leaf_hash");
-        launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>() + m, t->s_vb.as<uint8_t>(),
-                         t->s_voff.as<uint64_t>(), nb, sdig + 32 * m, t->st);
-        prof_end(t, pl);
     }
     t->in_tomb = nullptr;
     if (is_remove) {
@@ -495,10 +536,12 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             throw Error(ST_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e2));
         }
         e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 256, hipHostMallocDefault);
+        if (e2 == hipSuccess) e2 = hipStreamCreateWithFlags(&t->st2, hipStreamNonBlocking);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming);
         if (e2 != hipSuccess) {
-            (void)hipStreamDestroy(t->st);
-            delete t;
-            throw Error(ST_EHIP, std::string("hipHostMalloc: ") + hipGetErrorString(e2));
+            mkv_tree_destroy(t);
+            throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
         }
         *out = t;
     });
@@ -507,13 +550,17 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
 void mkv_tree_destroy(mkv_tree *t) {
     if (!t) return;
     (void)hipSetDevice(t->dev);
-    (void)hipStreamSynchronize(t->st);
+    if (t->st2) (void)hipStreamSynchronize(t->st2);
+    if (t->st) (void)hipStreamSynchronize(t->st);
+    if (t->ev_in) (void)hipEventDestroy(t->ev_in);
+    if (t->ev_join) (void)hipEventDestroy(t->ev_join);
+    if (t->st2) (void)hipStreamDestroy(t->st2);
     for (auto &p : t->evpool) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
     }
     if (t->h_small) (void)hipHostFree(t->h_small);
-    (void)hipStreamDestroy(t->st);
+    if (t->st) (void)hipStreamDestroy(t->st);
     delete t;
     (void)hipGetLastError();
 }
@@ -561,6 +608,7 @@ static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *ko
                               const uint64_t *voff, uint64_t n, bool staged, uint64_t staged_kbytes) {
     size_t ptot = prof_begin(t, "total_build");
     uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+    fork_streams(t);
     size_t pl = prof_begin(t, "leaf_hash");
     launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
     prof_end(t, pl);
@@ -606,6 +654,14 @@ static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     size_t ptot = prof_begin(t, "total_build");
     uint64_t kbytes = 0;
     const uint64_t tot = stage_batch(t, keys, values, is_remove, &kbytes);
+    const uint64_t m = tot - keys.n;
+    fork_streams(t);
+    if (values && keys.n) {
+        size_t pl = prof_begin(t, "leaf_hash");
+        launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>() + m, t->s_vb.as<uint8_t>(),
+                         t->s_voff.as<uint64_t>(), keys.n, t->s_dig.as<uint8_t>() + 32 * m, t->st);
+        prof_end(t, pl);
+    }
     sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb, true, kbytes);
     finish_unsharded(t);
     prof_end(t, ptot);
@@ -724,6 +780,45 @@ mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *diges
     });
 }
 
+// Top-down diff of two unsharded trees with equal leaf counts. Returns false (caller falls back to the
+// merge-join) when a divergent leaf position holds different keys, i.e. the key sets differ there.
+static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, const DiffSide &A, const DiffSide &B,
+                         uint64_t *refs, uint64_t *m_out) {
+    *m_out = 0;
+    if (std::memcmp(a->root, b->root, 32) == 0) return true;  // equal roots: identical leaves
+    const size_t L = a->lev_S.size();
+    const uint64_t n = a->n;
+    uint32_t *f0 = ens<uint32_t>(t->td_f0, n + 1);
+    uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 1);
+    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 1);
+    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 1) * 4, t->st));
+    MKV_HIP(hipMemsetAsync(f0, 0, 4, t->st));            // frontier at the top level: the root (index 0)
+    const uint32_t one = 1;
+    MKV_HIP(hipMemcpyAsync(cnt + (L - 1), &one, 4, hipMemcpyHostToDevice, t->st));
+    const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
+    uint32_t *fin = f0, *fout = f1;
+    for (size_t l = L - 1; l >= 1; --l) {
+        launch_topdown_level(na + 32 * a->lev_off[l - 1], nb + 32 * b->lev_off[l - 1], a->lev_cnt[l - 1], fin, cnt + l,
+                             fout, cnt + (l - 1), a->lev_cnt[l], t->st);
+        std::swap(fin, fout);
+    }
+    const uint64_t m = d2h_u32(t, cnt);
+    if (m) {
+        // divergent leaf positions -> sorted u64 (they are appended in no particular order)
+        uint64_t *k1 = ens<uint64_t>(t->td_k1, m + 1), *k2 = ens<uint64_t>(t->td_k2, m + 1);
+        uint32_t *v1 = ens<uint32_t>(t->td_v1, m + 1), *v2 = ens<uint32_t>(t->td_v2, m + 1);
+        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
+        launch_widen_positions(fin, m, k1, v1, t->st);
+        const bool sw = radix_sort_pairs(k1, v1, k2, v2, m, 0, std::max(8, bits_for(n)), radix, t->st);
+        const uint64_t *pos = sw ? k2 : k1;
+        uint32_t *nbad = cnt + L;
+        launch_topdown_leaves(pos, m, A, B, refs, nbad, t->st);
+        if (d2h_u32(t, nbad) != 0) return false;
+    }
+    *m_out = m;
+    return true;
+}
+
 static DiffSide side_of(const mkv_tree *t) {
     DiffSide s;
     s.kb = t->kb.as<uint8_t>();
@@ -747,13 +842,25 @@ mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out
         MKV_HIP(hipStreamSynchronize(b->st));
         DiffSide A = side_of(a), B = side_of(b);
         const uint64_t M = A.n + B.n;
-        size_t pd = prof_begin(t, "diff");
-        void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
         uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
-        uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
-        launch_diff(A, B, scr, refs, cnt, t->st);
-        prof_end(t, pd);
-        const uint64_t m = d2h_u64(t, cnt);
+        uint64_t m = 0;
+        bool done = false;
+        if (A.n == B.n && A.n > 0 && !a->sharded && !b->sharded) {
+            // Top-down: identical level shapes, so node (l, j) covers the same leaf positions in both trees.
+            // Equal digests prune whole subtrees; only the divergent frontier is expanded, level by level.
+            size_t pd = prof_begin(t, "diff");
+            done = topdown_diff(t, a, b, A, B, refs, &m);
+            prof_end(t, pd);
+        }
+        if (!done) {
+            size_t pd = prof_begin(t, "diff");
+            void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
+            uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
+            launch_diff(A, B, scr, refs, cnt, t->st);
+            prof_end(t, pd);
+            m = d2h_u64(t, cnt);
+        }
+        t->d_diffscr.ensure(diff_scratch_bytes(M));
         auto *l = new mkv_keylist();
         l->offsets.assign(m + 1, 0);
         if (m) {
@@ -860,6 +967,7 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         }
         size_t ptot = prof_begin(t, "total_build");
         uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+        fork_streams(t);
         size_t pl = prof_begin(t, "leaf_hash");
         launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
         prof_end(t, pl);

@@ -304,3 +304,48 @@ def test_level_structure_and_views():
     for i in range(n):
         py.insert(f"k{i}".encode(), f"v{i}".encode())
     assert [t.level_digests(l) for l in range(len(sizes))] == py.levels()
+
+
+# ---------------------------------------------------------------- top-down diff (equal leaf counts)
+@pytest.mark.parametrize("n,stride", [(1, 1), (2, 1), (3, 2), (1000, 7), (65_537, 1000), (200_000, 97)])
+def test_topdown_value_only_vs_oracle(oracle_lib, n, stride):
+    kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED + 5, 0, n)
+    vb2 = vb.copy().reshape(n, 100)
+    vb2[::stride, 3] ^= 1  # value-only divergence: same key set, same leaf count
+    vb2 = vb2.reshape(-1)
+    a, b = MerkleTree(), MerkleTree()
+    a.build((kb, ko), (vb, vo))
+    b.build((kb, ko), (vb2, vo))
+    oa = oracle_lib.OracleTree.build(kb, ko, vb, vo)
+    ob = oracle_lib.OracleTree.build(kb, ko, vb2, vo)
+    want = oa.diff(ob)
+    assert len(want) == len(range(0, n, stride))
+    assert a.diff_keys_bytes(b) == want
+    assert b.diff_keys_bytes(a) == want
+
+
+def test_topdown_equal_count_key_swap_falls_back(oracle_lib):
+    """Same leaf count but different key sets: divergent positions hold different keys -> merge-join."""
+    n = 10_000
+    kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED + 6, 0, n)
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    keys2 = list(keys)
+    keys2[17] = b"!" + keys2[17][1:]        # one key replaced (sorts first), count unchanged
+    keys2[4242] = keys2[4242][:-1] + b"~"
+    vals2 = list(vals)
+    vals2[99] = b"changed"
+    a, b = MerkleTree(), MerkleTree()
+    a.build(keys, vals)
+    b.build(keys2, vals2)
+    oa = oracle_lib.OracleTree.from_pairs(list(zip(keys, vals)))
+    ob = oracle_lib.OracleTree.from_pairs(list(zip(keys2, vals2)))
+    assert a.diff_keys_bytes(b) == oa.diff(ob)
+    assert b.diff_keys_bytes(a) == ob.diff(oa)
+
+
+def test_topdown_identical_trees_empty():
+    kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 5000)
+    a, b = MerkleTree(), MerkleTree()
+    a.build((kb, ko), (vb, vo))
+    b.build((kb, ko), (vb, vo))
+    assert a.diff_keys(b) == [] and a.diff_first_key(b) is None
