@@ -15,6 +15,9 @@
 //             LDS: every message word is one whole LDS word or a constant (the bench/config path).
 //   generic — any lengths / alignments: words are assembled from byte-range masks.
 //   global  — the wave's spans do not fit its LDS region: generic assembly straight from HBM.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "sha256.hpp"
@@ -208,13 +211,171 @@ __global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ k
     store_digest(out + 32 * r, st);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent variant: each wave loops over 64-record chunks (grid sized to the device), and while it
+// hashes chunk c from LDS the next chunk's spans (<= 9 x 16 B per lane) and per-lane offsets are
+// already in flight into registers. Staging latency disappears behind the VALU work, LDS regions are
+// wave-private (no workgroup barrier), and the bounded grid leaves CU slots for the ordering kernels
+// running concurrently on the aux stream.
+// ---------------------------------------------------------------------------------------------
+constexpr int PF = LEAF_LDS_WAVE / (16 * 64);  // uint4 prefetch registers per lane
+
+struct ChunkPlan {
+    const uint8_t *kstart, *vstart;
+    uint32_t kspan, vspan;
+    bool staged;
+};
+
+__device__ __forceinline__ ChunkPlan plan_chunk(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
+                                                const uint64_t *voff, uint64_t n, uint64_t r0) {
+    ChunkPlan P;
+    const uint64_t rc = n - r0 < 64 ? n - r0 : 64;
+    const uint64_t k0 = koff[r0], k1 = koff[r0 + rc], v0 = voff[r0], v1 = voff[r0 + rc];
+    P.kstart = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(kb + k0) & ~uintptr_t(15));
+    P.vstart = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(vb + v0) & ~uintptr_t(15));
+    const uint64_t ks = ((uint64_t)((kb + k1) - P.kstart) + 15) & ~uint64_t(15);
+    const uint64_t vs = ((uint64_t)((vb + v1) - P.vstart) + 15) & ~uint64_t(15);
+    P.staged = ks + vs + 32 <= LEAF_LDS_WAVE;
+    P.kspan = P.staged ? (uint32_t)ks : 0;
+    P.vspan = P.staged ? (uint32_t)vs : 0;
+    return P;
+}
+
+__device__ __forceinline__ void load_chunk(const ChunkPlan &P, uint32_t lane, uint4 R[PF]) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        const uint32_t byte = (lane + 64u * i) * 16u;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (byte < P.kspan) x = *reinterpret_cast<const uint4 *>(P.kstart + byte);
+        else if (byte - P.kspan < P.vspan) x = *reinterpret_cast<const uint4 *>(P.vstart + (byte - P.kspan));
+        R[i] = x;
+    }
+}
+
+__device__ __forceinline__ void store_chunk(const ChunkPlan &P, uint32_t lane, const uint4 R[PF], uint32_t *lds) {
+    uint4 *l4 = reinterpret_cast<uint4 *>(lds);
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+        const uint32_t idx = lane + 64u * i;
+        if (idx * 16u < P.kspan + P.vspan) l4[idx] = R[i];
+    }
+}
+
+template <bool SHORT>
+__global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict__ kb,
+                                                     const uint64_t *__restrict__ koff,
+                                                     const uint8_t *__restrict__ vb,
+                                                     const uint64_t *__restrict__ voff, uint64_t n,
+                                                     uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *lds = lds_all + wave * (LEAF_LDS_WAVE / 4);
+    const uint64_t nchunks = (n + 63) / 64;
+    const uint64_t stride = (uint64_t)gridDim.x * LEAF_WAVES;
+    uint64_t c = (uint64_t)blockIdx.x * LEAF_WAVES + wave;
+    if (c >= nchunks) return;  // wave-private work: no workgroup barrier anywhere
+
+    ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
+    uint4 R[PF];
+    load_chunk(P, lane, R);
+    uint64_t r = c * 64 + lane;
+    bool valid = r < n;
+    uint64_t kbeg = valid ? koff[r] : 0, kend = valid ? koff[r + 1] : 0;
+    uint64_t vbeg = valid ? voff[r] : 0, vend = valid ? voff[r + 1] : 0;
+    while (true) {
+        if (P.staged) store_chunk(P, lane, R, lds);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes land before its reads
+        // ---- prefetch chunk c + stride (registers only; consumed next iteration) ----
+        const uint64_t cn = c + stride;
+        ChunkPlan Pn = P;
+        uint64_t nkb = 0, nke = 0, nvb = 0, nve = 0;
+        const bool more = cn < nchunks;
+        if (more) {
+            Pn = plan_chunk(kb, koff, vb, voff, n, cn * 64);
+            load_chunk(Pn, lane, R);
+            const uint64_t rn = cn * 64 + lane;
+            if (rn < n) {
+                nkb = koff[rn];
+                nke = koff[rn + 1];
+                nvb = voff[rn];
+                nve = voff[rn + 1];
+            }
+        }
+        // ---- hash chunk c ----
+        if (valid) {
+            const uint32_t klen = (uint32_t)(kend - kbeg), vlen = (uint32_t)(vend - vbeg);
+            uint32_t st[8];
+            if (P.staged) {
+                const uint32_t kbyte = (uint32_t)((kb + kbeg) - P.kstart);
+                const uint32_t vbyte = P.kspan + (uint32_t)((vb + vbeg) - P.vstart);
+                const uint32_t K0 = __shfl(klen, 0), V0 = __shfl(vlen, 0);
+                const bool mine = klen == K0 && vlen == V0 && ((K0 | V0 | kbyte | vbyte) & 3) == 0;
+                if (__all(mine)) {
+                    hash_fast<SHORT>(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
+                                     __builtin_amdgcn_readfirstlane(V0), st);
+                } else {
+                    LdsSrc src{lds, kbyte, vbyte};
+                    hash_generic<SHORT>(src, klen, vlen, st);
+                }
+            } else {
+                GlbSrc src{kb + kbeg, vb + vbeg, kb + kend, vb + vend};
+                hash_generic<SHORT>(src, klen, vlen, st);
+            }
+            store_digest(out + 32 * r, st);
+        }
+        if (!more) break;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of chunk c done before it is overwritten
+        c = cn;
+        P = Pn;
+        r = c * 64 + lane;
+        valid = r < n;
+        kbeg = nkb;
+        kend = nke;
+        vbeg = nvb;
+        vend = nve;
+    }
+}
+
 }  // namespace
+
+static int leaf_kernel_variant() {
+    static const int v = [] {
+        const char *e = getenv("MKV_LEAF_KERNEL");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
 
 void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                       uint8_t *out, hipStream_t st) {
     if (n == 0) return;
     uint64_t waves = ceil_div(n, 64);
     uint64_t blocks = ceil_div(waves, LEAF_WAVES);
+    if (leaf_kernel_variant() == 1) {
+        static int cus = [] {
+            int dev = 0, c = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+            return c > 0 ? c : 256;
+        }();
+        // Bounded residency (default 2 workgroups = 8 waves per CU, 2 per SIMD): leaves VGPRs, LDS and
+        // wave slots for the aux-stream sort workgroups (k_os_pass needs 165 VGPRs/wave + 56.5 KiB LDS).
+        static int wgs = [] {
+            const char *e = getenv("MKV_LEAF_WGS");
+            int v = e ? atoi(e) : 2;
+            return v < 1 ? 1 : (v > 4 ? 4 : v);
+        }();
+        const uint64_t pblocks = std::min<uint64_t>(blocks, (uint64_t)cus * wgs);
+        if (sha_variant() == 0)
+            hipLaunchKernelGGL(k_leaf_persist<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                               vb, voff, n, out);
+        else
+            hipLaunchKernelGGL(k_leaf_persist<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                               vb, voff, n, out);
+        MKV_LAUNCH_CHECK();
+        return;
+    }
     if (sha_variant() == 0)
         hipLaunchKernelGGL(k_leaf_hash<false>, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff,
                            n, out);

@@ -40,7 +40,26 @@ __global__ __launch_bounds__(RD_THREADS) void k_reduce_fused(FusePlan p) {
             uint32_t l[8], r[8], o[8];
             const uint64_t c0 = 2 * j;
             const bool pair = c0 + 1 < p.S[k - 1];
-            if (k == 1) {
+            if (k == 1 && p.perm) {
+                // a[0] == 0 here: every leaf is a child of exactly one owned parent
+                uint4 *dst0 = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(p.in) + 32 * c0);
+                const uint4 *s0 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[c0]);
+                const uint4 x0 = s0[0], y0 = s0[1];
+                uint4 x1 = make_uint4(0, 0, 0, 0), y1 = x1;
+                if (pair) {
+                    const uint4 *s1 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[c0 + 1]);
+                    x1 = s1[0];
+                    y1 = s1[1];
+                    dst0[2] = x1;
+                    dst0[3] = y1;
+                }
+                dst0[0] = x0;
+                dst0[1] = y0;
+                l[0] = bswap32(x0.x); l[1] = bswap32(x0.y); l[2] = bswap32(x0.z); l[3] = bswap32(x0.w);
+                l[4] = bswap32(y0.x); l[5] = bswap32(y0.y); l[6] = bswap32(y0.z); l[7] = bswap32(y0.w);
+                r[0] = bswap32(x1.x); r[1] = bswap32(x1.y); r[2] = bswap32(x1.z); r[3] = bswap32(x1.w);
+                r[4] = bswap32(y1.x); r[5] = bswap32(y1.y); r[6] = bswap32(y1.z); r[7] = bswap32(y1.w);
+            } else if (k == 1) {
                 const uint8_t *src = p.in + 32 * (c0 - p.a[0]);
                 load_digest(src, l);
                 if (pair) load_digest(src + 32, r);
@@ -165,7 +184,11 @@ __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict
 
 void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
-    if (sha_variant() == 0)
+    // Few tiles = latency-bound (each fused level waits one full node hash): use the short dependency
+    // chain there; many tiles = throughput-bound: fewer instructions win (profiles/r01_valu_microbench.md).
+    const bool latency_bound = p.ntiles < 256;
+    const int v = sha_variant();
+    if (v == 0 || (v == 1 && !latency_bound))
         hipLaunchKernelGGL(k_reduce_fused<false>, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
     else
         hipLaunchKernelGGL(k_reduce_fused<true>, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);

@@ -31,6 +31,7 @@ constexpr int SC_TILE = SC_THREADS * SC_IPT;
 
 __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                  uint64_t n, uint64_t *__restrict__ pfx, uint32_t *__restrict__ idx) {
+    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t a = koff[i], b = koff[i + 1];
@@ -46,6 +47,7 @@ constexpr uint32_t LB_SPIN_LIMIT = 1u << 26;  // bounded spin: sets an error fla
 // Global digit counts of every pass in one read of the keys (counts[p*256 + d]).
 __global__ __launch_bounds__(RS_THREADS) void k_os_hist(const uint64_t *__restrict__ keys, uint64_t n, int bit0,
                                                        int npass, uint32_t *__restrict__ counts) {
+    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
     __shared__ uint32_t h[8][256];
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
     __syncthreads();
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                        uint64_t n, int shift, const uint32_t *__restrict__ gcount,
                                                        uint32_t *__restrict__ lookback, uint32_t *__restrict__ ctl) {
+    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
     __shared__ uint64_t sk[RS_TILE];
     __shared__ uint32_t sv[RS_TILE];
     __shared__ uint32_t wcnt[4][256];
@@ -244,6 +247,7 @@ template <class T> void scan_impl(const T *in, T *out, uint64_t n, T *total, voi
 // ---- ties / refinement ----
 __global__ void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, uint8_t *__restrict__ tie,
                             uint32_t *__restrict__ count) {
+    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool t = false;
     if (i < n) {

@@ -73,6 +73,10 @@ struct FusePlan {
     int nl;
     uint64_t tile0;  // first tile index (global, in units of 512 first-level parents)
     uint64_t ntiles;
+    // Fused leaf gather (unsharded first launch only): level-0 child c is read from dig[perm[c]] and
+    // also written to in[c], so the sorted leaf level is produced by the reduction itself.
+    const uint32_t *perm;
+    const uint8_t *dig;
 };
 void launch_reduce_fused(const FusePlan &p, hipStream_t st);
 

@@ -45,7 +45,7 @@ struct mkv_tree {
     int dev = 0;
     hipStream_t st = nullptr;   // main stream: leaf hashing, digest gather, reduction, diff
     hipStream_t st2 = nullptr;  // aux stream: key ownership copy, prefix sort, ties, dedup (overlaps st)
-    hipEvent_t ev_in = nullptr, ev_join = nullptr;
+    hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr;
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
@@ -60,6 +60,7 @@ struct mkv_tree {
     // shard state
     uint64_t goff = 0, gN = 0;
     bool sharded = false;
+    bool gather_pending = false;  // sorted leaf level not yet materialised (fused into the reduce)
     bool prepared = false;  // shard_prepare done, reduce pending
 
     // ---- scratch (device) ----
@@ -163,10 +164,21 @@ void prof_collect(mkv_tree *t) {
     t->evdone.clear();
 }
 
+// Low-latency wait: poll an event recorded on the stream instead of the runtime's blocking sync
+// (tens of microseconds of wake-up latency per scalar readback otherwise).
+void wait_stream(mkv_tree *t, hipStream_t s) {
+    MKV_HIP(hipEventRecord(t->ev_wait, s));
+    for (;;) {
+        hipError_t e = hipEventQuery(t->ev_wait);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) MKV_HIP(e);
+    }
+}
+
 // Full completion point of an API call: both streams drained, profiling pairs collected.
 void sync(mkv_tree *t) {
-    MKV_HIP(hipStreamSynchronize(t->st2));
-    MKV_HIP(hipStreamSynchronize(t->st));
+    wait_stream(t, t->st2);
+    wait_stream(t, t->st);
     prof_collect(t);
 }
 
@@ -181,13 +193,13 @@ template <class T> T *ens(DevBuf &b, uint64_t count) { return reinterpret_cast<T
 uint64_t d2h_u64(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
     if (!s) s = t->st;
     MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    MKV_HIP(hipStreamSynchronize(s));
+    wait_stream(t, s);
     return t->h_small[0];
 }
 uint32_t d2h_u32(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
     if (!s) s = t->st;
     MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MKV_HIP(hipStreamSynchronize(s));
+    wait_stream(t, s);
     return reinterpret_cast<uint32_t *>(t->h_small)[0];
 }
 
@@ -229,8 +241,16 @@ uint64_t total_nodes(const mkv_tree *t) {
     return s;
 }
 
-void run_reduce(mkv_tree *t, uint8_t *nodes) {
+// gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch; only for an
+// unsharded plan (every leaf has an owned parent). A single-leaf tree has no launch: plain gather.
+void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, const uint8_t *gdig = nullptr) {
     const size_t L = t->lev_S.size();
+    if (gperm) {
+        if (L < 2 || t->lev_base[0] != 0 || t->lev_cnt[0] != t->lev_S[0] || t->lev_cnt[1] == 0) {
+            launch_gather_digests(gperm, gdig, L ? t->lev_cnt[0] : 0, nodes, t->st);
+            gperm = nullptr;
+        }
+    }
     size_t l = 0;
     while (l + 1 < L && t->lev_cnt[l] > 0) {
         if (t->lev_cnt[l + 1] == 0) break;
@@ -253,6 +273,10 @@ void run_reduce(mkv_tree *t, uint8_t *nodes) {
         p.nl = (int)nl;
         p.tile0 = t0;
         p.ntiles = ntiles;
+        if (l == 0 && gperm) {
+            p.perm = gperm;
+            p.dig = gdig;
+        }
         launch_reduce_fused(p, t->st);
         l += nl;
     }
@@ -322,7 +346,7 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
 // (N == UINT64_MAX: unsharded, N = n).
 // ---------------------------------------------------------------------------------------------
 void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
-                       bool staged_inputs, uint64_t staged_kbytes) {
+                       bool staged_inputs, uint64_t staged_kbytes, bool defer_gather) {
     // Ordering work runs on the aux stream and overlaps the VALU-bound leaf hashing already enqueued on
     // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
     hipStream_t st = t->st2;
@@ -372,30 +396,35 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     swap_buf(t->pfx, *pkbuf);
     swap_buf(t->perm, *pmbuf);
     perm = t->perm.as<uint32_t>();
-    // own the keys (storage order): adopt staged uploads, copy borrowed device inputs
+    // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
+    // a readback there would hold the host until the gather finishes and delay the reduce launches)
+    const uint64_t kbytes = staged_inputs ? staged_kbytes : (n_in ? d2h_u64(t, koff + n_in, st) : 0);
+    MKV_HIP(hipEventRecord(t->ev_join, st));
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
+    // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
+    // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
+    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
+    t->gather_pending = defer_gather;
+    if (!defer_gather) {
+        size_t pg = prof_begin(t, "gather");
+        launch_gather_digests(perm, dig, n, nodes, t->st);
+        prof_end(t, pg);
+    }
+    // own the keys (storage order): adopt staged uploads, copy borrowed device inputs. The copy is
+    // not needed until the call returns, so it runs on st2 beside the (VALU-bound) reduction.
     t->nstore = n_in;
+    t->kbytes = kbytes;
     if (staged_inputs) {
         swap_buf(t->kb, t->s_kb);
         swap_buf(t->koff, t->s_koff);
-        t->kbytes = staged_kbytes;
     } else {
-        const uint64_t kbytes = n_in ? d2h_u64(t, koff + n_in, st) : 0;
         uint8_t *dkb = ens<uint8_t>(t->kb, kbytes + 16);
         uint64_t *dko = ens<uint64_t>(t->koff, n_in + 1);
         size_t pc = prof_begin(t, "keycopy", st);
         if (kbytes) MKV_HIP(hipMemcpyAsync(dkb, kb, kbytes, hipMemcpyDeviceToDevice, st));
         MKV_HIP(hipMemcpyAsync(dko, koff, (n_in + 1) * 8, hipMemcpyDeviceToDevice, st));
         prof_end(t, pc);
-        t->kbytes = kbytes;
     }
-    MKV_HIP(hipEventRecord(t->ev_join, st));
-    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
-    size_t pg = prof_begin(t, "gather");
-    // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
-    // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
-    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
-    launch_gather_digests(perm, dig, n, nodes, t->st);
-    prof_end(t, pg);
 }
 
 // Inputs staged on t->st become visible to the aux stream; call before enqueueing the leaf hash so the
@@ -427,7 +456,11 @@ void finish_unsharded(mkv_tree *t) {
     t->gN = t->n;
     plan_levels(t, 0, t->n, t->n);
     size_t pr = prof_begin(t, "reduce");
-    run_reduce(t, t->nodes.as<uint8_t>());
+    if (t->gather_pending)
+        run_reduce(t, t->nodes.as<uint8_t>(), t->perm.as<uint32_t>(), t->s_dig.as<uint8_t>());
+    else
+        run_reduce(t, t->nodes.as<uint8_t>());
+    t->gather_pending = false;
     prof_end(t, pr);
     t->has_root = t->n > 0;
     if (t->has_root) {
@@ -536,9 +569,14 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             throw Error(ST_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e2));
         }
         e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 256, hipHostMallocDefault);
-        if (e2 == hipSuccess) e2 = hipStreamCreateWithFlags(&t->st2, hipStreamNonBlocking);
+        if (e2 == hipSuccess) {
+            int lo = 0, hi = 0;  // aux (ordering) stream at the highest priority: its WGs dispatch first
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            e2 = hipStreamCreateWithPriority(&t->st2, hipStreamNonBlocking, hi);
+        }
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_wait, hipEventDisableTiming);
         if (e2 != hipSuccess) {
             mkv_tree_destroy(t);
             throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
@@ -554,6 +592,7 @@ void mkv_tree_destroy(mkv_tree *t) {
     if (t->st) (void)hipStreamSynchronize(t->st);
     if (t->ev_in) (void)hipEventDestroy(t->ev_in);
     if (t->ev_join) (void)hipEventDestroy(t->ev_join);
+    if (t->ev_wait) (void)hipEventDestroy(t->ev_wait);
     if (t->st2) (void)hipStreamDestroy(t->st2);
     for (auto &p : t->evpool) {
         (void)hipEventDestroy(p.a);
@@ -612,7 +651,7 @@ static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *ko
     size_t pl = prof_begin(t, "leaf_hash");
     launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
     prof_end(t, pl);
-    sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes);
+    sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes, true);
     finish_unsharded(t);
     prof_end(t, ptot);
     sync(t);
@@ -662,7 +701,7 @@ static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
                          t->s_voff.as<uint64_t>(), keys.n, t->s_dig.as<uint8_t>() + 32 * m, t->st);
         prof_end(t, pl);
     }
-    sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb, true, kbytes);
+    sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb, true, kbytes, true);
     finish_unsharded(t);
     prof_end(t, ptot);
     sync(t);
@@ -971,7 +1010,7 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         size_t pl = prof_begin(t, "leaf_hash");
         launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
         prof_end(t, pl);
-        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes);
+        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes, false);
         prof_end(t, ptot);
         sync(t);
         t->prepared = true;
