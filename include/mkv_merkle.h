@@ -56,8 +56,14 @@ mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values);
 /* Same with device pointers (bytes/offsets already resident in HBM on the tree's device). */
 mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
 
-/* n x insert(k_i, v_i) on the existing contents — merkle.rs:52-56 (sequential semantics, one rebuild). */
+/* n x insert(k_i, v_i) on the existing contents — merkle.rs:52-56 (sequential semantics, one rebuild).
+ * When every key is already a leaf (value-only anti-entropy batch, BASELINE configs[4]) only the changed
+ * leaves and their ancestors are rehashed (dirty path); otherwise the batch is merged and the tree
+ * rebuilt. On a sharded tree only the dirty path is allowed (new keys -> MKV_ESTATE) and the global
+ * root is stale until mkv_shard_fringe + all-gather + mkv_shard_combine. */
 mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values);
+/* Same with device pointers (batch already resident in HBM on the tree's device). */
+mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
 /* n x remove(k_i) — merkle.rs:59-62. Missing keys are ignored. */
 mkv_status mkv_tree_remove(mkv_tree *t, mkv_blob keys);
 /* Mixed batch: record i is remove(k_i) if is_remove[i] else insert(k_i, v_i), applied in order. values
@@ -98,7 +104,10 @@ const char *mkv_last_error(void);
  *   mkv_shard_fringe(buf)                    -> the <= 2 owned nodes per level whose parent is not owned
  *   [host all-gathers the fringe buffers over RCCL]
  *   mkv_shard_combine(all, world, N)         -> global root, identical on every rank (seam nodes hashed
- *                                               on the device). Bit-exact with the unsharded tree. */
+ *                                               on the device). Bit-exact with the unsharded tree.
+ * Incremental: mkv_tree_upsert[_device] of existing keys in the shard's range, then fringe + all-gather +
+ * combine again. mkv_tree_diff of two shards with the same (o_g, n_g, N) walks top-down from the
+ * shard's fringe roots. */
 #define MKV_FRINGE_ENTRY_BYTES 48
 #define MKV_FRINGE_MAX_ENTRIES 130
 #define MKV_FRINGE_BYTES (MKV_FRINGE_ENTRY_BYTES * MKV_FRINGE_MAX_ENTRIES)
@@ -110,7 +119,7 @@ mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes /* world x MKV_
 
 /* ---------------- measurement / test utilities (not part of the reference API) ---------------- */
 /* Per-kernel-group device time accumulated with HIP events on the tree's stream when enabled.
- * Groups: "leaf_hash", "sort", "gather", "reduce", "diff", "total_build". */
+ * Groups: "leaf_hash", "sort", "gather", "reduce", "diff", "update", "total_build". */
 mkv_status mkv_prof_enable(mkv_tree *t, int on);
 mkv_status mkv_prof_reset(mkv_tree *t);
 mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms, uint64_t *count);

@@ -19,7 +19,7 @@ FRINGE_BYTES = FRINGE_ENTRY_BYTES * FRINGE_MAX_ENTRIES
 # Every symbol include/mkv_merkle.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "mkv_tree_create", "mkv_tree_destroy", "mkv_tree_clone", "mkv_tree_build", "mkv_tree_build_device",
-    "mkv_tree_upsert", "mkv_tree_remove", "mkv_tree_apply", "mkv_tree_root", "mkv_tree_len",
+    "mkv_tree_upsert", "mkv_tree_upsert_device", "mkv_tree_remove", "mkv_tree_apply", "mkv_tree_root", "mkv_tree_len",
     "mkv_tree_node_count", "mkv_tree_level_count", "mkv_tree_level", "mkv_tree_leaves", "mkv_tree_diff",
     "mkv_tree_prefix_root", "mkv_keylist_get", "mkv_keylist_free", "mkv_last_error", "mkv_shard_prepare",
     "mkv_shard_reduce", "mkv_shard_fringe", "mkv_shard_combine", "mkv_prof_enable", "mkv_prof_reset",
@@ -57,6 +57,7 @@ def lib():
         "mkv_tree_build": ([vp, Blob, Blob], i32),
         "mkv_tree_build_device": ([vp, Blob, Blob], i32),
         "mkv_tree_upsert": ([vp, Blob, Blob], i32),
+        "mkv_tree_upsert_device": ([vp, Blob, Blob], i32),
         "mkv_tree_remove": ([vp, Blob], i32),
         "mkv_tree_apply": ([vp, Blob, Blob, vp], i32),
         "mkv_tree_root": ([vp, vp, P(i32)], i32),

@@ -260,25 +260,32 @@ __global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, 
 // ---- top-down diff (equal leaf counts): expand the divergent frontier one level down ----
 // frontier_in holds node indices of level l whose digests differ between the trees; children (l-1)
 // whose digests differ are appended to frontier_out (wave-aggregated: one atomic per wave).
+// One level of the top-down walk. fin: divergent parents (local indices of the owned parent range,
+// global index = local + a_par); their children (global 2p, 2p+1, local = global - a_child) are
+// compared and the divergent ones appended to fout. r0/r1: local child-level indices of owned nodes
+// whose parent is not owned (the tree's own root at the top level; a shard's fringe roots below it),
+// compared as extra frontier candidates (UINT64_MAX = none).
 __global__ __launch_bounds__(256) void k_topdown_level(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
-                                                      uint64_t child_count, const uint32_t *__restrict__ fin,
+                                                      uint64_t child_count, uint64_t a_par, uint64_t a_child,
+                                                      uint64_t r0, uint64_t r1, const uint32_t *__restrict__ fin,
                                                       const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
                                                       uint32_t *__restrict__ nout) {
     const uint32_t cnt = *nin;
     const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < 2ull * cnt; base += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t t = base + threadIdx.x;  // two candidate children per frontier node
+    const uint64_t tot = 2ull * cnt + 2;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;  // two candidate children per frontier node, then r0, r1
         bool d = false;
-        uint32_t c = 0;
-        if (t < 2ull * cnt) {
-            c = 2u * fin[t >> 1] + (uint32_t)(t & 1);
-            if (c < child_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
-        }
+        uint64_t c = UINT64_MAX;
+        if (t < 2ull * cnt) c = 2 * ((uint64_t)fin[t >> 1] + a_par) + (t & 1) - a_child;
+        else if (t == 2ull * cnt) c = r0;
+        else if (t == 2ull * cnt + 1) c = r1;
+        if (c < child_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
         const uint64_t m = __ballot(d);
         uint32_t slot = 0;
         if (lane == 0 && m) slot = atomicAdd(nout, (uint32_t)__popcll(m));
         slot = __shfl(slot, 0);
-        if (d) fout[slot + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = c;
+        if (d) fout[slot + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)c;
     }
 }
 
@@ -342,11 +349,12 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     MKV_LAUNCH_CHECK();
 }
 
-void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, const uint32_t *fin,
-                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_frontier, hipStream_t st) {
-    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * (max_frontier ? max_frontier : 1), 256), 2048);
-    hipLaunchKernelGGL(k_topdown_level, dim3((uint32_t)blocks), dim3(256), 0, st, ca, cb, child_count, fin, nin, fout,
-                       nout);
+void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, uint64_t a_par, uint64_t a_child,
+                          uint64_t r0, uint64_t r1, const uint32_t *fin, const uint32_t *nin, uint32_t *fout,
+                          uint32_t *nout, uint64_t max_frontier, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2, 256), 2048);
+    hipLaunchKernelGGL(k_topdown_level, dim3((uint32_t)blocks), dim3(256), 0, st, ca, cb, child_count, a_par, a_child,
+                       r0, r1, fin, nin, fout, nout);
     MKV_LAUNCH_CHECK();
 }
 

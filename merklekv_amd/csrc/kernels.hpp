@@ -102,8 +102,11 @@ size_t diff_scratch_bytes(uint64_t nmerged);
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
                  hipStream_t st);
 // Top-down diff for trees with equal leaf counts (identical level shapes).
-void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, const uint32_t *fin,
-                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_frontier, hipStream_t st);
+// fin/fout: local indices; a_par/a_child: global index of local 0 at the parent/child level; r0/r1:
+// extra child-level candidates (owned nodes with an unowned parent; UINT64_MAX = none).
+void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, uint64_t a_par, uint64_t a_child,
+                          uint64_t r0, uint64_t r1, const uint32_t *fin, const uint32_t *nin, uint32_t *fout,
+                          uint32_t *nout, uint64_t max_frontier, hipStream_t st);
 void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
                            uint32_t *nbad, hipStream_t st);
 void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
@@ -112,6 +115,25 @@ void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const
                       uint8_t *out, hipStream_t st);
 // Prefix range [lo, hi) of sorted keys starting with prefix (single-thread binary search).
 void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t plen, uint64_t *lohi, hipStream_t st);
+
+// ---- incremental dirty-path update (k_update.hip) ----
+// pos[i] = sorted leaf position of batch key i (UINT64_MAX if it is not a leaf), idx[i] = i;
+// *missing += keys that are not leaves.
+void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, uint64_t *pos,
+                   uint32_t *idx, uint32_t *missing, hipStream_t st);
+// (pos, bidx) sorted by pos (stable): scatter the last write per position into level 0, mark dirty.
+void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
+                         uint32_t *bm, uint32_t *list, uint32_t *count, hipStream_t st);
+// Level l of the local plan: owned global range [a, a+c) stored at node offset off, global size S;
+// parent level (l+1) and child level (l-1) ranges for ownership tests and bit clearing.
+struct DirtyLevel {
+    uint64_t a, c, off, S;
+    uint64_t a_par, c_par, off_par;
+    uint64_t a_child, c_child, off_child;
+    int has_parent, has_child;
+};
+void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
+                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, hipStream_t st);
 
 // ---- synthetic generator (k_gen.hip) — bench/test utility, not part of the reference API ----
 void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,

@@ -62,6 +62,7 @@ struct mkv_tree {
     bool sharded = false;
     bool gather_pending = false;  // sorted leaf level not yet materialised (fused into the reduce)
     bool prepared = false;  // shard_prepare done, reduce pending
+    bool combine_pending = false;  // sharded tree updated in place: global root stale until shard_combine
 
     // ---- scratch (device) ----
     DevBuf s_kb, s_koff, s_vb, s_voff, s_dig, s_tomb;
@@ -73,6 +74,10 @@ struct mkv_tree {
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf d_seam, d_S, d_fr;
+    // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
+    DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
+    uint64_t bm_bits = 0;
+    bool bm_dirty = false;
     uint64_t *h_small = nullptr;  // pinned host scalars
 
     // ---- profiling ----
@@ -452,6 +457,7 @@ uint64_t pack_sorted_keys(mkv_tree *t, DevBuf &dst_kb, DevBuf &dst_koff, uint64_
 
 void finish_unsharded(mkv_tree *t) {
     t->sharded = false;
+    t->combine_pending = false;
     t->goff = 0;
     t->gN = t->n;
     plan_levels(t, 0, t->n, t->n);
@@ -640,6 +646,7 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         dst->gN = src->gN;
         dst->sharded = src->sharded;
         dst->prepared = false;
+        dst->combine_pending = src->combine_pending;
     });
 }
 
@@ -707,6 +714,89 @@ static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     sync(t);
 }
 
+static DiffSide side_of(const mkv_tree *t);
+
+// Dirty-path update (k_update.hip) for a batch whose keys are all leaves already: same key order and
+// level plan, so only changed leaves and their ancestors are rehashed. Batch records are device
+// pointers. Returns false, having changed nothing, when some key is not a leaf.
+static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
+                         const uint64_t *voff, uint64_t m) {
+    if (t->n == 0 || t->prepared || m == 0) return m == 0 && t->n > 0;
+    const size_t L = t->lev_S.size();
+    const uint64_t nn = total_nodes(t);
+    hipStream_t st = t->st;
+    size_t ptot = prof_begin(t, "update");
+    // bitmap: one bit per stored node, zero between calls
+    const uint64_t words = (nn + 63) / 32 + 2;
+    uint32_t *bm = ens<uint32_t>(t->u_bm, words);
+    if (t->bm_bits < nn || t->bm_dirty) {
+        MKV_HIP(hipMemsetAsync(bm, 0, words * 4, st));
+        t->bm_bits = words * 32 - 64;
+    }
+    uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);  // cnt[l]: dirty entries at level l; cnt[L+1]: missing
+    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, st));
+    uint64_t *pos = ens<uint64_t>(t->u_pos, m + 1), *pos2 = ens<uint64_t>(t->u_pos2, m + 1);
+    uint32_t *idx = ens<uint32_t>(t->u_idx, m + 1), *idx2 = ens<uint32_t>(t->u_idx2, m + 1);
+    launch_locate(kb, koff, m, side_of(t), pos, idx, cnt + L + 1, st);
+    if (d2h_u32(t, cnt + L + 1, st) != 0) {
+        prof_end(t, ptot);
+        sync(t);
+        return false;
+    }
+    uint8_t *bdig = ens<uint8_t>(t->u_dig, m * 32);
+    launch_leaf_hash(kb, koff, vb, voff, m, bdig, st);
+    void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
+    const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, m, 0, std::max(8, bits_for(t->n)), radix, st);
+    uint32_t *l0 = ens<uint32_t>(t->u_l0, m + 1), *l1 = ens<uint32_t>(t->u_l1, m + 1);
+    t->bm_dirty = true;
+    uint8_t *nodes = t->nodes.as<uint8_t>();
+    launch_dirty_leaves(sw ? pos2 : pos, sw ? idx2 : idx, m, bdig, nodes, bm, l0, cnt, st);
+    for (size_t l = 0; l < L; ++l) {
+        DirtyLevel D{};
+        D.a = t->lev_base[l];
+        D.c = t->lev_cnt[l];
+        D.off = t->lev_off[l];
+        D.S = t->lev_S[l];
+        D.has_parent = l + 1 < L && t->lev_cnt[l + 1] > 0;
+        if (D.has_parent) {
+            D.a_par = t->lev_base[l + 1];
+            D.c_par = t->lev_cnt[l + 1];
+            D.off_par = t->lev_off[l + 1];
+        }
+        D.has_child = l > 0;
+        if (l > 0) {
+            D.a_child = t->lev_base[l - 1];
+            D.c_child = t->lev_cnt[l - 1];
+            D.off_child = t->lev_off[l - 1];
+        }
+        launch_dirty_level(D, m, nodes, bm, l0, cnt + l, l1, cnt + l + 1, st);
+        std::swap(l0, l1);
+        if (!D.has_parent) break;  // every entry at this level cleared its own bit: bitmap is zero again
+    }
+    if (!t->sharded) {
+        MKV_HIP(hipMemcpyAsync(t->root, nodes + 32 * t->lev_off[L - 1], 32, hipMemcpyDeviceToHost, st));
+        t->has_root = true;
+    } else {
+        t->has_root = false;
+        t->combine_pending = true;  // the seam and the global root: mkv_shard_fringe + all-gather + combine
+    }
+    prof_end(t, ptot);
+    sync(t);
+    t->bm_dirty = false;
+    return true;
+}
+
+// Stage a host batch on the device for dirty_update.
+static void upload_update_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob &values) {
+    const uint64_t m = keys.n;
+    ens<uint8_t>(t->u_kb, keys.offsets[m] - keys.offsets[0] + 16);
+    ens<uint64_t>(t->u_koff, m + 1);
+    ens<uint8_t>(t->u_vb, values.offsets[m] - values.offsets[0] + 16);
+    ens<uint64_t>(t->u_voff, m + 1);
+    upload_blob(t, keys, t->u_kb, t->u_koff);
+    upload_blob(t, values, t->u_vb, t->u_voff);
+}
+
 mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values) {
     MKV_TRY({
         NEED(t, "tree is null");
@@ -715,7 +805,45 @@ mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         check_blob(values, "values");
         DevGuard g(t->dev);
         if (keys.n == 0) return MKV_OK;
+        NEED(!t->prepared, "shard_reduce pending");
+        if (t->n) {
+            upload_update_batch(t, keys, values);
+            if (dirty_update(t, t->u_kb.as<uint8_t>(), t->u_koff.as<uint64_t>(), t->u_vb.as<uint8_t>(),
+                             t->u_voff.as<uint64_t>(), keys.n))
+                return MKV_OK;
+        }
+        if (t->sharded) throw Error(ST_ESTATE, "upsert of new keys on a sharded tree: rebuild the shard");
         apply_batch(t, keys, &values, nullptr);
+    });
+}
+
+mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        NEED(keys.n < 0xFFFFFFF0ull, "too many records");
+        NEED(keys.n == 0 || (keys.offsets && values.offsets), "null offsets");
+        DevGuard g(t->dev);
+        if (keys.n == 0) return MKV_OK;
+        NEED(!t->prepared, "shard_reduce pending");
+        if (dirty_update(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n)) return MKV_OK;
+        if (t->sharded) throw Error(ST_ESTATE, "upsert of new keys on a sharded tree: rebuild the shard");
+        // key-set change: bring the batch to the host and take the general (re-sort) path
+        std::vector<uint64_t> ko(keys.n + 1), vo(keys.n + 1);
+        MKV_HIP(hipMemcpy(ko.data(), keys.offsets, ko.size() * 8, hipMemcpyDeviceToHost));
+        MKV_HIP(hipMemcpy(vo.data(), values.offsets, vo.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> kbh(ko.back() - ko[0] + 1), vbh(vo.back() - vo[0] + 1);
+        if (ko.back() > ko[0])
+            MKV_HIP(hipMemcpy(kbh.data(), keys.bytes + ko[0], ko.back() - ko[0], hipMemcpyDeviceToHost));
+        if (vo.back() > vo[0])
+            MKV_HIP(hipMemcpy(vbh.data(), values.bytes + vo[0], vo.back() - vo[0], hipMemcpyDeviceToHost));
+        const uint64_t k0 = ko[0], v0 = vo[0];
+        for (auto &x : ko) x -= k0;
+        for (auto &x : vo) x -= v0;
+        mkv_blob hk{kbh.data(), ko.data(), keys.n}, hv{vbh.data(), vo.data(), values.n};
+        check_blob(hk, "keys");
+        check_blob(hv, "values");
+        apply_batch(t, hk, &hv, nullptr);
     });
 }
 
@@ -749,6 +877,7 @@ mkv_status mkv_tree_root(const mkv_tree *t, uint8_t out32[32], int *has_root) {
     MKV_TRY({
         NEED(t && out32 && has_root, "null argument");
         NEED(!t->prepared, "shard_reduce pending");
+        NEED(!t->combine_pending, "shard_combine pending (sharded tree updated in place)");
         *has_root = t->has_root ? 1 : 0;
         if (t->has_root) std::memcpy(out32, t->root, 32);
         else std::memset(out32, 0, 32);
@@ -819,26 +948,53 @@ mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *diges
     });
 }
 
-// Top-down diff of two unsharded trees with equal leaf counts. Returns false (caller falls back to the
-// merge-join) when a divergent leaf position holds different keys, i.e. the key sets differ there.
+// Owned nodes of level l whose parent is not owned: the local roots of a shard's forest (the tree root
+// at the top level of an unsharded tree). At most two per level: the first and the last owned node.
+static void level_roots(const mkv_tree *t, size_t l, uint64_t r[2]) {
+    r[0] = r[1] = UINT64_MAX;
+    const size_t L = t->lev_S.size();
+    const uint64_t a = t->lev_base[l], c = t->lev_cnt[l];
+    if (!c) return;
+    const uint64_t cand[2] = {a, a + c - 1};
+    for (int q = 0; q < 2; ++q) {
+        if (q == 1 && cand[1] == cand[0]) break;
+        bool parent_owned = false;
+        if (l + 1 < L) {
+            const uint64_t p = cand[q] / 2, a2 = t->lev_base[l + 1], c2 = t->lev_cnt[l + 1];
+            parent_owned = p >= a2 && p < a2 + c2;
+        }
+        if (!parent_owned) r[q] = cand[q] - a;
+    }
+}
+
+static bool same_plan(const mkv_tree *a, const mkv_tree *b) {
+    return a->n == b->n && a->lev_base == b->lev_base && a->lev_cnt == b->lev_cnt && a->lev_S == b->lev_S;
+}
+
+// Top-down diff of two trees with identical level plans (equal leaf counts, and for shards the same
+// global offset and size): node (l, j) covers the same leaf positions in both. Equal digests prune
+// whole subtrees; only the divergent frontier is expanded, level by level, starting from the local
+// roots (the root, or a shard's fringe roots). Returns false (caller falls back to the merge-join)
+// when a divergent leaf position holds different keys, i.e. the key sets differ there.
 static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, const DiffSide &A, const DiffSide &B,
                          uint64_t *refs, uint64_t *m_out) {
     *m_out = 0;
-    if (std::memcmp(a->root, b->root, 32) == 0) return true;  // equal roots: identical leaves
+    const bool roots_valid = !a->combine_pending && !b->combine_pending && a->has_root && b->has_root;
+    if (roots_valid && std::memcmp(a->root, b->root, 32) == 0) return true;  // equal roots: identical leaves
     const size_t L = a->lev_S.size();
     const uint64_t n = a->n;
-    uint32_t *f0 = ens<uint32_t>(t->td_f0, n + 1);
-    uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 1);
-    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 1);
-    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 1) * 4, t->st));
-    MKV_HIP(hipMemsetAsync(f0, 0, 4, t->st));            // frontier at the top level: the root (index 0)
-    const uint32_t one = 1;
-    MKV_HIP(hipMemcpyAsync(cnt + (L - 1), &one, 4, hipMemcpyHostToDevice, t->st));
+    uint32_t *f0 = ens<uint32_t>(t->td_f0, n + 2);
+    uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 2);
+    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2);  // cnt[l]: frontier size at level l; cnt[L] = 0 (seed)
+    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
-    for (size_t l = L - 1; l >= 1; --l) {
-        launch_topdown_level(na + 32 * a->lev_off[l - 1], nb + 32 * b->lev_off[l - 1], a->lev_cnt[l - 1], fin, cnt + l,
-                             fout, cnt + (l - 1), a->lev_cnt[l], t->st);
+    for (size_t l = L; l >= 1; --l) {  // parents at level l (none at l == L) -> children at level l-1
+        uint64_t r[2];
+        level_roots(a, l - 1, r);
+        const uint64_t a_par = l < L ? a->lev_base[l] : 0, max_par = l < L ? a->lev_cnt[l] : 0;
+        launch_topdown_level(na + 32 * a->lev_off[l - 1], nb + 32 * b->lev_off[l - 1], a->lev_cnt[l - 1], a_par,
+                             a->lev_base[l - 1], r[0], r[1], fin, cnt + l, fout, cnt + (l - 1), max_par, t->st);
         std::swap(fin, fout);
     }
     const uint64_t m = d2h_u32(t, cnt);
@@ -850,7 +1006,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
         launch_widen_positions(fin, m, k1, v1, t->st);
         const bool sw = radix_sort_pairs(k1, v1, k2, v2, m, 0, std::max(8, bits_for(n)), radix, t->st);
         const uint64_t *pos = sw ? k2 : k1;
-        uint32_t *nbad = cnt + L;
+        uint32_t *nbad = cnt + L + 1;
         launch_topdown_leaves(pos, m, A, B, refs, nbad, t->st);
         if (d2h_u32(t, nbad) != 0) return false;
     }
@@ -884,9 +1040,8 @@ mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out
         uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
         uint64_t m = 0;
         bool done = false;
-        if (A.n == B.n && A.n > 0 && !a->sharded && !b->sharded) {
-            // Top-down: identical level shapes, so node (l, j) covers the same leaf positions in both trees.
-            // Equal digests prune whole subtrees; only the divergent frontier is expanded, level by level.
+        if (A.n > 0 && same_plan(a, b)) {
+            // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
             size_t pd = prof_begin(t, "diff");
             done = topdown_diff(t, a, b, A, B, refs, &m);
             prof_end(t, pd);
@@ -1016,6 +1171,7 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         t->prepared = true;
         t->sharded = true;
         t->has_root = false;
+        t->combine_pending = false;
         *n_local = t->n;
     });
 }
@@ -1141,6 +1297,7 @@ mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes, uint32_t world
         *has_root = 1;
         std::memcpy(t->root, out32, 32);
         t->has_root = true;
+        t->combine_pending = false;
     });
 }
 

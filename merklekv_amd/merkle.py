@@ -149,6 +149,13 @@ class MerkleTree:
         pk, pv = pack_blob(keys), pack_blob(values)
         check(lib().mkv_tree_upsert(self._h, pk.blob(), pv.blob()))
 
+    def upsert_device(self, kb_ptr: int, koff_ptr: int, vb_ptr: int, voff_ptr: int, n: int) -> None:
+        """upsert() of a batch already resident in HBM (device pointers). A batch of existing keys takes
+        the dirty path (only changed leaves and their ancestors are rehashed)."""
+        self._flush()
+        self._cache.clear()
+        check(lib().mkv_tree_upsert_device(self._h, Blob(kb_ptr, koff_ptr, n), Blob(vb_ptr, voff_ptr, n)))
+
     def remove_many(self, keys) -> None:
         self._flush()
         self._cache.clear()

@@ -39,3 +39,11 @@ def sharded_root(tree, keys, values, dist, device="cpu", group=None, on_device: 
     fringes = _all_gather_bytes(dist, tree.shard_fringe(), device, group)
     root = tree.shard_combine(b"".join(fringes), world, total)
     return root, counts
+
+
+def shard_recombine(tree, dist, total: int, device="cpu", group=None):
+    """After an in-place update of this rank's shard (MerkleTree.upsert / upsert_device of keys in its
+    range: the dirty path), all-gather the new fringes and recompute the seam nodes and global root."""
+    world = dist.get_world_size(group)
+    fringes = _all_gather_bytes(dist, tree.shard_fringe(), device, group)
+    return tree.shard_combine(b"".join(fringes), world, total)

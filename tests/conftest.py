@@ -39,3 +39,16 @@ def oracle_lib():
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")])
     from oracle import coracle
     return coracle
+
+
+def pytest_collection_finish(session):
+    """GPU sessions: bring up torch's HIP runtime before libmerklekv_hip.so's. torch ships its own
+    libamdhip64; when the in-tree library (linked to /opt/rocm's) initialises the device first, torch's
+    later init reports no device. Tests that stage device buffers with torch need it the other way round."""
+    if any(item.get_closest_marker("gpu") for item in session.items):
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:
+            pass

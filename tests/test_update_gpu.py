@@ -1,0 +1,174 @@
+"""Incremental anti-entropy update (BASELINE configs[4]): value-only upsert batches take the dirty path
+(k_update.hip) and must equal the reference's insert-then-rebuild (merkle.rs:52-56) bit-exactly: root,
+every level array, and diffs against the pre-update tree. Sharded trees: in-place shard updates +
+fringe/combine give the unsharded root; top-down diff from the shard's fringe roots equals the
+unsharded diff restricted to the shard. Checked against the C oracle (oracle/merkle_oracle.c)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from merklekv_amd import MerkleTree  # noqa: E402
+from oracle import coracle  # noqa: E402
+from oracle.merkle_oracle import DEFAULT_SEED, pack, split_blob  # noqa: E402
+
+
+def _levels(t: MerkleTree):
+    return [b"".join(t.level_digests(l)) for l in range(t.level_count())]
+
+
+def _oracle_levels(o):
+    return [o.level(l).tobytes() for l in range(o.nlevels())]
+
+
+def _batch(keys, idx, tag):
+    """Update records for keys[idx] (in the given order, duplicates allowed) with fresh values."""
+    ks = [keys[int(i)] for i in idx]
+    vs = [b"upd-%s-%d-%d" % (tag.encode(), j, int(i)) for j, i in enumerate(idx)]
+    return ks, vs
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 17, 64, 1000, 4097, 65537])
+def test_dirty_path_matches_rebuild(n):
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    rng = np.random.default_rng(n)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    base = t.clone()
+    m = max(1, n // 7)
+    idx = list(rng.integers(0, n, size=m))
+    idx += [n - 1, 0] + idx[: max(1, m // 3)]  # last leaf (R5 promotion path), first, duplicates
+    ks, vs = _batch(keys, idx, "a")
+    t.upsert(ks, vs)
+    kb2, ko2 = pack(ks)
+    vb2, vo2 = pack(vs)
+    o2 = o.upsert(kb2, ko2, vb2, vo2)
+    assert t.get_root_hash() == o2.root()
+    assert _levels(t) == _oracle_levels(o2)
+    assert base.diff_keys_bytes(t) == o.diff(o2)
+    # a second batch on the updated tree (bitmap must be clean again)
+    idx2 = list(rng.integers(0, n, size=max(1, n // 3)))
+    ks3, vs3 = _batch(keys, idx2, "b")
+    t.upsert(ks3, vs3)
+    kb3, ko3 = pack(ks3)
+    vb3, vo3 = pack(vs3)
+    o3 = o2.upsert(kb3, ko3, vb3, vo3)
+    assert t.get_root_hash() == o3.root()
+    assert _levels(t) == _oracle_levels(o3)
+
+
+def test_dirty_path_same_value_is_noop():
+    n = 1000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    want = t.get_root_hash()
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    t.upsert(keys[10:20], vals[10:20])
+    assert t.get_root_hash() == want
+
+
+def test_batch_with_new_key_falls_back_exactly():
+    n = 3000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    ks = [keys[5], b"zz-new-key", keys[5], keys[2999]]
+    vs = [b"1", b"2", b"3", b"4"]
+    t.upsert(ks, vs)
+    o2 = o.upsert(*pack(ks), *pack(vs))
+    assert len(t) == n + 1
+    assert t.get_root_hash() == o2.root()
+    assert _levels(t) == _oracle_levels(o2)
+
+
+def test_upsert_device_dirty_and_fallback():
+    import torch
+    n = 20000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    for tag, ks in (("dirty", [keys[i] for i in range(0, n, 97)] + [keys[3]]),
+                    ("fallback", [keys[1], b"brand-new"])):
+        vs = [b"v-%s-%d" % (tag.encode(), i) for i in range(len(ks))]
+        bk, bo = pack(ks)
+        bv, bvo = pack(vs)
+        dk = torch.from_numpy(bk.copy()).cuda()
+        dko = torch.from_numpy(bo.astype(np.int64)).cuda()
+        dv = torch.from_numpy(bv.copy()).cuda()
+        dvo = torch.from_numpy(bvo.astype(np.int64)).cuda()
+        torch.cuda.synchronize()
+        t.upsert_device(dk.data_ptr(), dko.data_ptr(), dv.data_ptr(), dvo.data_ptr(), len(ks))
+        o = o.upsert(bk, bo, bv, bvo)
+        assert t.get_root_hash() == o.root(), tag
+    assert _levels(t) == _oracle_levels(o)
+
+
+def _shard_trees(kb, ko, vb, vo, cuts):
+    """Sorted records split at cuts -> prepared+reduced+combined shard trees."""
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    order = sorted(range(len(keys)), key=lambda i: keys[i])
+    ks = [keys[i] for i in order]
+    vs = [vals[i] for i in order]
+    bounds = [0] + list(cuts) + [len(ks)]
+    trees = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        t = MerkleTree()
+        t.shard_prepare(ks[a:b], vs[a:b])
+        trees.append(t)
+    N = len(ks)
+    fr = b""
+    for r, t in enumerate(trees):
+        t.shard_reduce(bounds[r], N)
+        fr += t.shard_fringe()
+    roots = [t.shard_combine(fr, len(trees), N) for t in trees]
+    return trees, ks, bounds, roots
+
+
+def _recombine(trees, N):
+    fr = b"".join(t.shard_fringe() for t in trees)
+    return [t.shard_combine(fr, len(trees), N) for t in trees]
+
+
+@pytest.mark.parametrize("n,cuts", [(1001, (333, 700)), (40000, (1, 16384, 16385, 39999)), (7, (3,))])
+def test_sharded_dirty_update_and_topdown_diff(n, cuts):
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    trees, ks, bounds, roots = _shard_trees(kb, ko, vb, vo, cuts)
+    full = MerkleTree()
+    full.build((kb, ko), (vb, vo))
+    assert all(r == full.get_root_hash() for r in roots)
+    base = [t.clone() for t in trees]
+    base_full = full.clone()
+    rng = np.random.default_rng(n)
+    idx = sorted(set(int(i) for i in rng.integers(0, n, size=max(2, n // 50)))) + [n - 1]
+    upd_k = [ks[i] for i in idx]
+    upd_v = [b"new-%d" % i for i in idx]
+    full.upsert(upd_k, upd_v)
+    for r, t in enumerate(trees):
+        a, b = bounds[r], bounds[r + 1]
+        sel = [j for j, i in enumerate(idx) if a <= i < b]
+        if sel:
+            t.upsert([upd_k[j] for j in sel], [upd_v[j] for j in sel])
+    roots2 = _recombine(trees, n)
+    assert all(r == full.get_root_hash() for r in roots2)
+    want = base_full.diff_keys_bytes(full)
+    assert want == sorted(set(upd_k))
+    got = []
+    for b0, t in zip(base, trees):
+        got += b0.diff_keys_bytes(t)
+    assert got == want
+
+
+def test_sharded_upsert_new_key_rejected():
+    n = 100
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    trees, ks, bounds, roots = _shard_trees(kb, ko, vb, vo, (50,))
+    from merklekv_amd import MerkleError
+    with pytest.raises(MerkleError):
+        trees[0].upsert([b"not-a-leaf"], [b"x"])
