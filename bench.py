@@ -1,13 +1,24 @@
 #!/usr/bin/env python3
 """Benchmark: Merkle build leaves/s (+ diff keys/s) on MI355X — BASELINE.json configs[1] (10M keys, 1 GPU).
 
-A step = one full tree build (leaf hashing + key ordering + dedup + gathers + level reduction) over
-n synthetic records (32-B keys, 100-B values, generated on the device, already resident in HBM when
-the timed region starts). With N>1 ranks (torch.distributed.run, one process per GPU) each rank owns
-a contiguous key range of n records (weak scaling); the step adds the RCCL all-gathers of shard leaf
-counts and seam fringes and the on-device seam combine that yields the global root on every rank.
+Default workload (`--workload build`, what the driver runs): a step = one full tree build (leaf hashing
++ key ordering + dedup + gathers + level reduction + root readback) over n synthetic records (32-B
+keys, 100-B values, generated on the device, already resident in HBM when the timed region starts).
+With N>1 ranks (torch.distributed.run, one process per GPU) each rank owns a contiguous key range of n
+records (weak scaling); the step adds the RCCL all-gathers of shard leaf counts and seam fringes and
+the on-device seam combine that yields the global root on every rank. `--n 125000000` at N=8 is
+configs[3] (1B keys over 8 GPUs); at N=1 it is one shard of it.
 
-Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+Other BASELINE configs (run explicitly; their JSON lines are committed under profiles/):
+  --workload diff         configs[2]: two 100M-key replicas, (a) 0.1 % value-only divergence (top-down
+                          walk) and (b) 0.1 % mixed 80/10/10 change/delete/insert (merge-join); a step =
+                          one diff_keys incl. compaction and the D2H of the divergent key list.
+  --workload incremental  configs[4]: a 1B-key tree (125M keys per GPU at N=8; --n per GPU), 8 replicas
+                          = base + 7 variants; a step = each variant applies its own 1M-key value-update
+                          batch (125K per GPU; dirty-path rehash + fringe/seam recombine) and the base is
+                          diffed against all 7 (top-down).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 """
 from __future__ import annotations
 
@@ -26,89 +37,139 @@ LEAF_BYTES = 8 + KLEN + VLEN + 32   # algorithmic bytes per leaf for Kernel A: 1
 HBM_PEAK_GBS = 8000.0                # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 SHA_OPS_PER_LEAF = 3 * 1450          # model: 3 compressions x ~1450 VALU lane-ops
+DIFF_BYTES_PER_KEY = 2 * (8 + 32)    # top-down/merge: prefix + digest per side, per union key
+ALPHA = b"-0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ_abcdefghijklmnopqrstuvwxyz"  # sorted URL-safe base64
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=10_000_000, help="records per GPU")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
-    ap.add_argument("--no-diff", action="store_true")
-    args = ap.parse_args()
+class Ctx:
+    """Process-group + device plumbing shared by the workloads."""
 
-    import torch
+    def __init__(self):
+        import torch
+        self.torch = torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist_mod
+            self.dist = dist_mod
+            torch.cuda.set_device(self.local)
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        self.dev = torch.device("cuda", self.local)
+        torch.cuda.set_device(self.local)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist_mod
-        dist = dist_mod
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(local)
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
 
-    from merklekv_amd import MerkleTree
-    from merklekv_amd.merkle import gen_records_device
-    from merklekv_amd.shard import sharded_root
+    def max_over_ranks(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
 
-    n = args.n
-    kb = torch.empty(n * KLEN + 64, dtype=torch.uint8, device=dev)
-    vb = torch.empty(n * VLEN + 64, dtype=torch.uint8, device=dev)
-    ko = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    vo = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    gen_records_device(local, SEED, rank * n, n, KLEN, VLEN, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
-                       vo.data_ptr(), shard=rank, nshards=world)
-    torch.cuda.synchronize()
+    def sum_over_ranks(self, x: int) -> int:
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.int64, device=self.dev)
+        self.dist.all_reduce(t)
+        return int(t.item())
 
-    tree = MerkleTree(local)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    def records(self, n, idx0=None, vfield=1):
+        """n records of this rank's key range, generated on the device (same generator as the oracle)."""
+        torch = self.torch
+        from merklekv_amd.merkle import gen_records_device
+        kb = torch.empty(n * KLEN + 64, dtype=torch.uint8, device=self.dev)
+        vb = torch.empty(n * VLEN + 64, dtype=torch.uint8, device=self.dev)
+        ko = torch.empty(n + 1, dtype=torch.int64, device=self.dev)
+        vo = torch.empty(n + 1, dtype=torch.int64, device=self.dev)
+        gen_records_device(self.local, SEED, self.rank * n if idx0 is None else idx0, n, KLEN, VLEN,
+                           kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), shard=self.rank,
+                           nshards=self.world, vfield=vfield)
         torch.cuda.synchronize()
+        return kb, ko, vb, vo
 
-    def step():
-        if world == 1:
+    def build(self, tree, kb, ko, vb, vo, n):
+        """Full build of this rank's records; returns the global root (all ranks agree)."""
+        if self.world == 1:
             tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
-            return tree.get_root_hash()
-        root, _ = sharded_root(tree, (kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), None,
-                               dist, device=dev, on_device=True)
-        return root
+            return tree.get_root_hash(), n
+        from merklekv_amd.shard import sharded_root
+        root, counts = sharded_root(tree, (kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), None,
+                                    self.dist, device=self.dev, on_device=True)
+        return root, sum(counts)
 
-    for _ in range(args.warmup):
-        root = step()
-    tree.prof_enable(True)
-    tree.prof_reset()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        root = step()
-    barrier()
-    t1 = time.perf_counter()
-    tree.prof_enable(False)
-    elapsed = t1 - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        rt = torch.frombuffer(bytearray(root), dtype=torch.uint8).to(dev)
-        allr = torch.empty(world * 32, dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(allr, rt)
-        roots = allr.cpu().numpy().reshape(world, 32)
+    def check_roots_agree(self, root: bytes):
+        if self.dist is None or root is None:
+            return
+        torch = self.torch
+        rt = torch.frombuffer(bytearray(root), dtype=torch.uint8).to(self.dev)
+        allr = torch.empty(self.world * 32, dtype=torch.uint8, device=self.dev)
+        self.dist.all_gather_into_tensor(allr, rt)
+        roots = allr.cpu().numpy().reshape(self.world, 32)
         assert (roots == roots[0]).all(), "ranks disagree on the global root"
 
+    def finish(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def base_line(ctx, args, metric, value, unit, ms_per_step, workload, dtype="u32", higher=True, scaling="weak"):
+    return {
+        "metric": metric,
+        "value": value,
+        "unit": unit,
+        "n_gpus": ctx.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": higher,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic (on-device splitmix64 generator, seed 0x4D65726B6C654B56)",
+        "config": {"workload": workload, "keys_per_gpu": args.n, "key_bytes": KLEN, "value_bytes": VLEN,
+                   "parallelism": f"key-range shards x{ctx.world}" if ctx.world > 1 else "single GPU"},
+    }
+
+
+def random_values(torch, m, dev, gen):
+    """m x VLEN value bytes from the base64 alphabet (device)."""
+    alpha = torch.frombuffer(bytearray(ALPHA), dtype=torch.uint8).to(dev)
+    return alpha[torch.randint(0, 64, (m, VLEN), device=dev, generator=gen)]
+
+
+# ============================================================================================ build
+def wl_build(ctx, args):
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    n = args.n
+    kb, ko, vb, vo = ctx.records(n)
+    tree = MerkleTree(ctx.local)
+
+    for _ in range(args.warmup):
+        root, N = ctx.build(tree, kb, ko, vb, vo, n)
+    tree.prof_enable(True)
+    tree.prof_reset()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        root, N = ctx.build(tree, kb, ko, vb, vo, n)
+    ctx.barrier()
+    t1 = time.perf_counter()
+    tree.prof_enable(False)
+    elapsed = ctx.max_over_ranks(t1 - t0)
+    ctx.check_roots_agree(root)
+
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * n * args.steps / elapsed
+    value = ctx.world * n * args.steps / elapsed
     leaf_ms, leaf_cnt = tree.prof_read("leaf_hash")
     groups = {g: tree.prof_read(g) for g in ("leaf_hash", "sort", "keycopy", "gather", "reduce", "total_build")}
     leaf_avg_ms = leaf_ms / max(leaf_cnt, 1)
@@ -126,69 +187,230 @@ def main():
         except Exception:
             traffic = None
 
-    # ---------------- diff (secondary: keys/s over the union, value-only 0.1% divergence) -------------
-    diff_info = None
-    if not args.no_diff and world == 1:
+    # ---------------- secondary, 1 GPU only: diff and incremental update on the same tree -------------
+    diff_info = upd_info = None
+    if not args.no_diff and ctx.world == 1:
         # replica B: same keys, value byte 0 flipped in every 1000th record (0.1 % value-only divergence)
         vb2 = vb.clone()
         v2 = vb2[: n * VLEN].view(n, VLEN)
-        idx = torch.arange(0, n, 1000, device=dev)
+        idx = torch.arange(0, n, 1000, device=ctx.dev)
         v2[idx, 0] = v2[idx, 0] ^ 1
         torch.cuda.synchronize()
-        treeB = MerkleTree(local)
+        treeB = MerkleTree(ctx.local)
         treeB.build_device(kb.data_ptr(), ko.data_ptr(), vb2.data_ptr(), vo.data_ptr(), n)
         tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
-        d = tree.diff_keys_bytes(treeB)  # warm
+        d = tree.diff_keys_packed(treeB)  # warm
         reps = 5
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            d = tree.diff_keys_bytes(treeB)
+            d = tree.diff_keys_packed(treeB)
         dt = (time.perf_counter() - t0) / reps
-        diff_info = {"union_keys": n, "divergent": len(d), "expected_divergent": int(idx.numel()),
-                     "ms": dt * 1e3, "keys_per_s": n / dt, "mode": "merge-join, value-only 0.1%"}
+        diff_info = {"union_keys": n, "divergent": len(d[1]) - 1, "expected_divergent": int(idx.numel()),
+                     "ms": dt * 1e3, "keys_per_s": n / dt,
+                     "mode": "top-down (equal key sets), value-only 0.1%, incl. key-list D2H"}
+        # incremental: 0.1 % value-update batch of existing keys (dirty path), configs[4]'s ratio
+        m = max(1, n // 1000)
+        g = torch.Generator(device=ctx.dev)
+        g.manual_seed(7)
+        sel = torch.randint(0, n, (m,), device=ctx.dev, generator=g)
+        ukb = kb[: n * KLEN].view(n, KLEN)[sel].contiguous().view(-1)
+        uvb = random_values(torch, m, ctx.dev, g).contiguous().view(-1)
+        uko = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * KLEN
+        uvo = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * VLEN
+        torch.cuda.synchronize()
+        tree.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)  # warm
+        tree.prof_enable(True)
+        tree.prof_reset()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            tree.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
+        dt = (time.perf_counter() - t0) / reps
+        tree.prof_enable(False)
+        ums, ucnt = tree.prof_read("update")
+        upd_info = {"tree_keys": n, "batch": m, "ms": dt * 1e3, "device_ms": ums / max(ucnt, 1),
+                    "update_keys_per_s": m / dt, "mode": "dirty-path rehash (value-only batch)"}
         del treeB, vb2
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_build(args.cpu_seconds)
 
-    if rank == 0:
-        out = {
-            "metric": "Merkle build leaves/s (10M keys, full tree: hash+sort+reduce)",
-            "value": value,
-            "unit": "leaves/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (on-device splitmix64 generator, seed 0x4D65726B6C654B56)",
-            "config": {"workload": "configs[1]: 10M keys x 1 MI355X per rank, 32-B keys / 100-B values",
-                       "keys_per_gpu": n, "key_bytes": KLEN, "value_bytes": VLEN,
-                       "parallelism": f"key-range shards x{world}" if world > 1 else "single GPU"},
-            "root": root.hex() if root else None,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_leaf_hash", "bytes_per_leaf": LEAF_BYTES,
-                         "avg_launch_ms": leaf_avg_ms, "launches": leaf_cnt,
-                         "gb_per_s_hashed": hashed_gbs,
-                         "valu_frac_model": valu_frac,
-                         "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): HBM frac ceiling ~0.39"},
-            "stage_ms_per_step": {g: (v[0] / max(v[1], 1) if g == "leaf_hash" else v[0] / args.steps)
-                                  for g, v in groups.items()},
-            "diff": diff_info,
-            "cpu_baseline": cpu,
-        }
+    if ctx.rank == 0:
+        wl = ("configs[1]: 10M keys x 1 MI355X per rank, 32-B keys / 100-B values" if n == 10_000_000
+              else f"{n} keys per rank (configs[3] = 125M x 8 ranks), 32-B keys / 100-B values")
+        out = base_line(ctx, args, "Merkle build leaves/s (10M keys, full tree: hash+sort+reduce)", value,
+                        "leaves/s", ms_per_step, wl)
+        out["root"] = root.hex() if root else None
+        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                           "kernel": "k_leaf_hash", "bytes_per_leaf": LEAF_BYTES,
+                           "avg_launch_ms": leaf_avg_ms, "launches": leaf_cnt,
+                           "gb_per_s_hashed": hashed_gbs,
+                           "valu_frac_model": valu_frac,
+                           "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): HBM frac ceiling ~0.39; "
+                                   "avg_launch_ms is measured while the sort co-runs on the aux stream"}
+        out["stage_ms_per_step"] = {g: (v[0] / max(v[1], 1) if g == "leaf_hash" else v[0] / args.steps)
+                                    for g, v in groups.items()}
+        out["diff"] = diff_info
+        out["incremental"] = upd_info
+        out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
 
 
-def cpu_baseline(target_s: float):
+# ============================================================================================= diff
+def wl_diff(ctx, args):
+    """configs[2]: two replicas with 0.1 % divergence; diff keys/s over the union of keys."""
+    torch = ctx.torch
+    import numpy as np
+    from merklekv_amd import MerkleTree
+    n = args.n
+    kb, ko, vb, vo = ctx.records(n)
+    A = MerkleTree(ctx.local)
+    ctx.build(A, kb, ko, vb, vo, n)
+    ndiv = max(1, n // 1000)
+    g = torch.Generator(device=ctx.dev)
+    g.manual_seed(11 + ctx.rank)
+    perm = torch.randperm(n, device=ctx.dev, generator=g)
+    res = {}
+    for mode in ("value_only", "mixed"):
+        kv, vv = kb[: n * KLEN].view(n, KLEN), vb[: n * VLEN].view(n, VLEN)
+        vb2 = vv.clone()
+        if mode == "value_only":
+            chg, rm, new = perm[:ndiv], perm[:0], 0
+        else:  # 80 % value changes, 10 % deletions, 10 % new keys (SURVEY §8d configs[2b])
+            c, r = ndiv * 8 // 10, ndiv // 10
+            chg, rm, new = perm[:c], perm[c:c + r], ndiv - c - r
+        vb2[chg, 0] ^= 1
+        keep = torch.ones(n, dtype=torch.bool, device=ctx.dev)
+        keep[rm] = False
+        kB, vB = kv[keep], vb2[keep]
+        if new:
+            nk, _, nv, _ = ctx.records(new, idx0=10**12 + ctx.rank * new)
+            kB = torch.cat([kB, nk[: new * KLEN].view(new, KLEN)])
+            vB = torch.cat([vB, nv[: new * VLEN].view(new, VLEN)])
+        nB = kB.shape[0]
+        kBf, vBf = kB.contiguous().view(-1), vB.contiguous().view(-1)
+        koB = torch.arange(0, nB + 1, device=ctx.dev, dtype=torch.int64) * KLEN
+        voB = torch.arange(0, nB + 1, device=ctx.dev, dtype=torch.int64) * VLEN
+        # expected divergent keys: changed + removed + new (keys are unique)
+        exp = torch.cat([kv[chg], kv[rm]] + ([kB[-new:]] if new else []))
+        exp_np = exp.cpu().numpy()
+        exp_sorted = exp_np[np.lexsort(exp_np.T[::-1])]
+        del vb2, kB, vB, exp
+        B = MerkleTree(ctx.local)
+        ctx.build(B, kBf, koB, vBf, voB, nB)
+        torch.cuda.synchronize()
+        for _ in range(args.warmup):
+            d = A.diff_keys_packed(B)
+        A.prof_enable(True)
+        A.prof_reset()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            d = A.diff_keys_packed(B)
+        ctx.barrier()
+        el = ctx.max_over_ranks(time.perf_counter() - t0)
+        A.prof_enable(False)
+        dms, dcnt = A.prof_read("diff")
+        got = d[0].reshape(-1, KLEN)
+        exact = got.shape == exp_sorted.shape and bool((got == exp_sorted).all())
+        union = ctx.sum_over_ranks(n + new)
+        res[mode] = {"union_keys": union, "divergent": ctx.sum_over_ranks(len(d[1]) - 1),
+                     "expected_divergent": ctx.sum_over_ranks(int(exp_sorted.shape[0])),
+                     "exact_vs_construction": exact, "ms": el / args.steps * 1e3,
+                     "device_ms": dms / max(args.steps, 1),
+                     "keys_per_s": union * args.steps / el,
+                     "path": "top-down" if mode == "value_only" else "merge-join"}
+        del B, kBf, vBf
+        torch.cuda.empty_cache()
+    cpu = None
+    if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_diff()
+    if ctx.rank == 0:
+        v = res["value_only"]
+        wl = (f"configs[2]: {n // 1_000_000}M keys x 2 replicas per rank, 0.1% divergence; value = value-only "
+              f"(top-down) union keys/s; 'mixed' = 80/10/10 change/delete/insert (merge-join)")
+        out = base_line(ctx, args, "Merkle diff keys/s (union keys compared, 2 replicas, 0.1% divergence)",
+                        v["keys_per_s"], "keys/s", v["ms"], wl)
+        achieved = DIFF_BYTES_PER_KEY * res["mixed"]["union_keys"] / (res["mixed"]["device_ms"] * 1e-3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "merge-join diff (mixed)",
+                           "bytes_per_union_key": DIFF_BYTES_PER_KEY}
+        out["diff"] = res
+        out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    del A
+
+
+# ====================================================================================== incremental
+def wl_incremental(ctx, args):
+    """configs[4]: 8 replicas (base + 7 variants) of a 1B-key tree (per-GPU shard of n keys); a step =
+    each variant applies its own value-update batch (dirty path + seam recombine) + base diffed vs all 7."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.shard import shard_recombine
+    n = args.n
+    m = args.batch
+    R = args.replicas
+    kb, ko, vb, vo = ctx.records(n)
+    base = MerkleTree(ctx.local)
+    root, N = ctx.build(base, kb, ko, vb, vo, n)
+    del vb, vo
+    torch.cuda.empty_cache()
+    variants = [base.clone() for _ in range(R - 1)]
+    batches = []
+    for r in range(R - 1):
+        g = torch.Generator(device=ctx.dev)
+        g.manual_seed(1000 * r + ctx.rank)
+        sel = torch.randint(0, n, (m,), device=ctx.dev, generator=g)
+        ukb = kb[: n * KLEN].view(n, KLEN)[sel].contiguous().view(-1)
+        uvb = random_values(torch, m, ctx.dev, g).contiguous().view(-1)
+        batches.append((ukb, torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * KLEN,
+                        uvb, torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * VLEN,
+                        int(torch.unique(sel).numel())))
+    torch.cuda.synchronize()
+
+    def step():
+        for t, (ukb, uko, uvb, uvo, _) in zip(variants, batches):
+            t.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
+            if ctx.world > 1:
+                shard_recombine(t, ctx.dist, N, device=ctx.dev)
+        return [base.diff_keys_packed(t) for t in variants]
+
+    for _ in range(args.warmup):
+        diffs = step()
+    for t in [base] + variants:
+        t.prof_enable(True)
+        t.prof_reset()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        diffs = step()
+    ctx.barrier()
+    el = ctx.max_over_ranks(time.perf_counter() - t0)
+    upd_ms = sum(t.prof_read("update")[0] for t in variants) / (args.steps * (R - 1))
+    diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))
+    ok = all(len(d[1]) - 1 == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else
+    total_updates = ctx.sum_over_ranks(m) * (R - 1)
+    roots = []
+    if ctx.world == 1:
+        roots = [t.get_root_hash().hex() for t in variants[:2]]
+    if ctx.rank == 0:
+        wl = (f"configs[4]: {N} keys ({n} per rank), {R} replicas (base + {R - 1} variants), "
+              f"{m} value updates per variant per rank; step = {R - 1} dirty-path batches + 1-vs-{R - 1} diff")
+        out = base_line(ctx, args, "Incremental anti-entropy: update keys/s (dirty-path rehash + 8-replica diff)",
+                        total_updates * args.steps / el, "keys/s", el / args.steps * 1e3, wl)
+        out["incremental"] = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
+                              "update_device_ms_per_batch": upd_ms, "diff_device_ms_per_pair": diff_ms,
+                              "diff_sizes_match_unique_updates": ok,
+                              "divergent_per_pair_rank0": [len(d[1]) - 1 for d in diffs], "variant_roots": roots}
+        out["cpu_baseline"] = None if (args.no_cpu_baseline or ctx.world > 1) else cpu_baseline_update()
+        print(json.dumps(out), flush=True)
+
+
+# ===================================================================================== CPU baselines
+def cpu_baseline_build(target_s: float):
     """Oracle (C restatement of merkle.rs, single thread, SHA-NI like sha2 0.10.9) on a bounded sample."""
     import ctypes
 
@@ -210,6 +432,49 @@ def cpu_baseline(target_s: float):
         co.set_backend(0)
 
 
+def cpu_baseline_diff(n: int = 2_000_000):
+    """Oracle diff_keys (merkle.rs:171-196 restated: merge of the sorted leaf lists) on two n-key trees."""
+    from oracle import coracle as co
+    kb, ko, vb, vo = co.gen_records(SEED, 0, n)
+    vb2 = vb.copy()
+    vb2[::100 * 1000] ^= 1  # 0.1 % value-only divergence (every 1000th record's value byte 0)
+    a = co.OracleTree.build(kb, ko, vb, vo)
+    b = co.OracleTree.build(kb, ko, vb2, vo)
+    t0 = time.perf_counter()
+    d = a.diff(b)
+    secs = time.perf_counter() - t0
+    return {"value": n / secs, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"diff of two {n}-key trees, 0.1% value-only ({len(d)} keys), {secs:.2f} s",
+            "cpu_model": _cpu_model()}
+
+
+def cpu_baseline_update(n: int = 2_000_000, m: int = 2_000):
+    """The reference's way to apply a batch: upsert into the leaf map + full rebuild (merkle.rs:52-56),
+    done once per batch (the reference does it once per insert)."""
+    import numpy as np
+
+    from oracle import coracle as co
+    from oracle.merkle_oracle import pack, split_blob
+    shani = co.set_backend(1)
+    try:
+        kb, ko, vb, vo = co.gen_records(SEED, 0, n)
+        a = co.OracleTree.build(kb, ko, vb, vo)
+        keys = split_blob(kb, ko)
+        sel = np.random.default_rng(5).integers(0, n, size=m)
+        ks = [keys[int(i)] for i in sel]
+        vs = [b"u%099d" % j for j in range(m)]
+        bk, bo = pack(ks)
+        bv, bvo = pack(vs)
+        t0 = time.perf_counter()
+        a.upsert(bk, bo, bv, bvo)
+        secs = time.perf_counter() - t0
+        return {"value": m / secs, "unit": "keys/s", "cores": 1, "kind": "port",
+                "sample": f"{m}-key value batch on a {n}-key tree: upsert + one full rebuild, {secs:.2f} s",
+                "cpu_model": _cpu_model()}
+    finally:
+        co.set_backend(0)
+
+
 def _cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -218,6 +483,27 @@ def _cpu_model():
     except OSError:
         pass
     return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=("build", "diff", "incremental"), default="build")
+    ap.add_argument("--n", type=int, default=None,
+                    help="records per GPU (default: 10M build, 100M diff, 125M incremental)")
+    ap.add_argument("--batch", type=int, default=125_000, help="incremental: updates per variant per GPU")
+    ap.add_argument("--replicas", type=int, default=8, help="incremental: base + variants")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
+    ap.add_argument("--no-diff", action="store_true")
+    args = ap.parse_args()
+    if args.n is None:
+        args.n = {"build": 10_000_000, "diff": 100_000_000, "incremental": 125_000_000}[args.workload]
+    ctx = Ctx()
+    {"build": wl_build, "diff": wl_diff, "incremental": wl_incremental}[args.workload](ctx, args)
+    ctx.finish()
 
 
 if __name__ == "__main__":

@@ -50,6 +50,20 @@ __device__ __forceinline__ bool digest_eq(const uint8_t *a, const uint8_t *b) {
            x1.z == y1.z && x1.w == y1.w;
 }
 
+// Key order between A[i] and B[j] for the merge. Equal 8-byte prefixes first try the leaf digests:
+// equal digests mean equal encoded leaves (u32 |k| || k || u32 |v| || v), hence equal keys, unless
+// SHA-256 collides — the same assumption the top-down walk and the reference's anti-entropy make when
+// equal subtree hashes are taken as equal contents. Replicas agree on almost every key, so this skips
+// the dependent perm -> koff -> key-bytes gathers for nearly every comparison; only keys whose
+// prefixes tie and whose digests differ (changed values, or distinct keys sharing 8 bytes) pay the
+// full compare.
+__device__ __forceinline__ int cmp_merge(const DiffSide &A, uint64_t i, uint64_t pa, const DiffSide &B, uint64_t j,
+                                         uint64_t pb) {
+    if (pa != pb) return pa < pb ? -1 : 1;
+    if (digest_eq(A.dig + 32 * i, B.dig + 32 * j)) return 0;
+    return cmp_ab(A, i, pa, B, j, pb);
+}
+
 // Merge-path split of diagonal d over the full arrays: number of A elements among the first d outputs
 // (A before B on equal keys).
 __device__ uint64_t split_global(const DiffSide &A, const DiffSide &B, uint64_t d) {
@@ -57,7 +71,7 @@ __device__ uint64_t split_global(const DiffSide &A, const DiffSide &B, uint64_t 
     while (lo < hi) {
         uint64_t mid = (lo + hi) >> 1;
         uint64_t jb = d - 1 - mid;
-        if (cmp_ab(A, mid, A.pfx[mid], B, jb, B.pfx[jb]) <= 0) lo = mid + 1;
+        if (cmp_merge(A, mid, A.pfx[mid], B, jb, B.pfx[jb]) <= 0) lo = mid + 1;
         else hi = mid;
     }
     return lo;
@@ -108,7 +122,7 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
     while (lo < hi) {
         uint64_t mid = (lo + hi) >> 1;
         uint64_t jb = dl - 1 - mid;
-        if (cmp_ab(A, c.a0 + mid, pa[1 + mid], B, c.b0 + jb, pb[jb]) <= 0) lo = mid + 1;
+        if (cmp_merge(A, c.a0 + mid, pa[1 + mid], B, c.b0 + jb, pb[jb]) <= 0) lo = mid + 1;
         else hi = mid;
     }
     const uint32_t isplit = (uint32_t)lo;
@@ -123,7 +137,7 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
         if (i >= c.a1) takeA = false;
         else if (j >= B.n) takeA = true;
         else {
-            cab = cmp_ab(A, i, pa[1 + li], B, j, pb[lj]);
+            cab = cmp_merge(A, i, pa[1 + li], B, j, pb[lj]);
             takeA = (j >= c.b1) ? true : (cab <= 0);
             // j == b1 < B.n: the tile's B slice is exhausted, so A[i] < B[b1] or equal (then matched)
         }
@@ -137,7 +151,7 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
             bool matched = false;
             if (i > 0) {
                 const uint64_t pprev = pa[li];  // A[i-1]: li-1+1
-                matched = cmp_ab(A, i - 1, pprev, B, j, pb[lj]) == 0;
+                matched = cmp_merge(A, i - 1, pprev, B, j, pb[lj]) == 0;
             }
             d = !matched;
             ++j;

@@ -58,18 +58,29 @@ def pack_blob(items: Sequence[bytes] | tuple) -> _Packed:
     return _Packed(np.frombuffer(raw, dtype=np.uint8) if raw else np.zeros(0, np.uint8), off)
 
 
-def _keylist(handle) -> list[bytes]:
+def _keylist_packed(handle) -> tuple[np.ndarray, np.ndarray]:
+    """(bytes, offsets[n+1]) copies of a library-owned key list (one memcpy each)."""
     n = C.c_uint64()
     bp = C.c_void_p()
     op = C.c_void_p()
     check(lib().mkv_keylist_get(handle, C.byref(n), C.byref(bp), C.byref(op)))
     cnt = n.value
     if cnt == 0:
-        return []
+        return np.zeros(0, np.uint8), np.zeros(1, np.uint64)
     offs = np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_uint64)), shape=(cnt + 1,)).copy()
-    raw = C.string_at(bp, int(offs[-1])) if offs[-1] else b""
+    nb = int(offs[-1])
+    raw = (np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(nb,)).copy() if nb
+           else np.zeros(0, np.uint8))
+    return raw, offs
+
+
+def _keylist(handle) -> list[bytes]:
+    raw, offs = _keylist_packed(handle)
+    if len(offs) == 1:
+        return []
+    b = raw.tobytes()
     o = offs.tolist()
-    return [raw[o[i]:o[i + 1]] for i in range(cnt)]
+    return [b[o[i]:o[i + 1]] for i in range(len(o) - 1)]
 
 
 class NodeView:
@@ -295,6 +306,17 @@ class MerkleTree:
         check(lib().mkv_tree_diff(self._h, other._h, C.byref(kl)))
         try:
             return _keylist(kl)
+        finally:
+            lib().mkv_keylist_free(kl)
+
+    def diff_keys_packed(self, other: "MerkleTree") -> tuple[np.ndarray, np.ndarray]:
+        """diff_keys as the C ABI returns it: packed key bytes + offsets[n+1] (numpy copies)."""
+        self._flush()
+        other._flush()
+        kl = C.c_void_p()
+        check(lib().mkv_tree_diff(self._h, other._h, C.byref(kl)))
+        try:
+            return _keylist_packed(kl)
         finally:
             lib().mkv_keylist_free(kl)
 
