@@ -53,7 +53,10 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst);
 /* new() + n x insert(k_i, v_i) in order — merkle.rs:52-56 called by sync.rs:110-115, :130-134 and
  * server.rs:664-667. Replaces the tree's contents. Duplicate keys: last write wins (merkle.rs:54). */
 mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values);
-/* Same with device pointers (bytes/offsets already resident in HBM on the tree's device). */
+/* Same with device pointers (bytes/offsets already resident in HBM on the tree's device). The caller
+ * must have completed the work that produced them (the library runs on its own non-blocking streams
+ * and does not order itself after other streams or runtimes, e.g. torch's); offsets must be monotone
+ * with offsets[n] inside the allocation — they are trusted, not validated. */
 mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
 
 /* n x insert(k_i, v_i) on the existing contents — merkle.rs:52-56 (sequential semantics, one rebuild).
@@ -62,7 +65,7 @@ mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
  * rebuilt. On a sharded tree only the dirty path is allowed (new keys -> MKV_ESTATE) and the global
  * root is stale until mkv_shard_fringe + all-gather + mkv_shard_combine. */
 mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values);
-/* Same with device pointers (batch already resident in HBM on the tree's device). */
+/* Same with device pointers (batch already resident in HBM; same contract as mkv_tree_build_device). */
 mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
 /* n x remove(k_i) — merkle.rs:59-62. Missing keys are ignored. */
 mkv_status mkv_tree_remove(mkv_tree *t, mkv_blob keys);

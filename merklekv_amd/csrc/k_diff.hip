@@ -128,31 +128,39 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
     const uint32_t isplit = (uint32_t)lo;
     uint64_t i = c.a0 + lo, j = c.b0 + (dl - lo);
     uint32_t fromA = 0, div = 0;
+    // A key equal to B[j] is always emitted just before B[j] (A first on ties), so a B step right after
+    // an A step with the same j reuses that comparison: nearly identical replicas (the anti-entropy
+    // case) then pay one prefix compare + one digest compare per union key, not three.
+    bool prevA_matched = false;
 #pragma unroll
     for (int s = 0; s < DI; ++s) {
         if (dl + s >= na + nb) break;
         const uint64_t li = i - c.a0, lj = j - c.b0;
         bool takeA;
         int cab = 1;
+        bool deq = false;
         if (i >= c.a1) takeA = false;
         else if (j >= B.n) takeA = true;
         else {
-            cab = cmp_merge(A, i, pa[1 + li], B, j, pb[lj]);
+            const uint64_t xa = pa[1 + li], xb = pb[lj];
+            if (xa != xb) cab = xa < xb ? -1 : 1;
+            else if (digest_eq(A.dig + 32 * i, B.dig + 32 * j)) cab = 0, deq = true;  // see cmp_merge
+            else cab = cmp_ab(A, i, xa, B, j, xb);
             takeA = (j >= c.b1) ? true : (cab <= 0);
             // j == b1 < B.n: the tile's B slice is exhausted, so A[i] < B[b1] or equal (then matched)
         }
         bool d;
         if (takeA) {
-            bool matched = (j < B.n) && cab == 0;
-            d = !matched || !digest_eq(A.dig + 32 * i, B.dig + 32 * j);
+            const bool matched = (j < B.n) && cab == 0;
+            d = !matched || !deq;
+            prevA_matched = matched;
             fromA |= 1u << s;
             ++i;
         } else {
-            bool matched = false;
-            if (i > 0) {
-                const uint64_t pprev = pa[li];  // A[i-1]: li-1+1
-                matched = cmp_merge(A, i - 1, pprev, B, j, pb[lj]) == 0;
-            }
+            bool matched;
+            if (s > 0 && ((fromA >> (s - 1)) & 1u)) matched = prevA_matched;  // A[i-1] vs this B[j]: done
+            else matched = i > 0 && cmp_merge(A, i - 1, pa[li], B, j, pb[lj]) == 0;
+            prevA_matched = false;
             d = !matched;
             ++j;
         }
@@ -303,6 +311,19 @@ __global__ __launch_bounds__(256) void k_topdown_level(const uint8_t *__restrict
     }
 }
 
+// Key-set screen before a top-down walk: compares the sorted 8-byte key prefixes of both trees at
+// `samples` evenly spaced positions. Equal key sets never differ there; an insertion or deletion
+// shifts every later position, so a handful of samples detect it (then the merge-join runs directly).
+__global__ __launch_bounds__(256) void k_sample_pfx(const uint64_t *__restrict__ pa, const uint64_t *__restrict__ pb,
+                                                   uint64_t n, uint32_t samples, uint32_t *__restrict__ count) {
+    uint32_t bad = 0;
+    for (uint32_t k = threadIdx.x; k < samples; k += blockDim.x) {
+        const uint64_t i = samples > 1 ? (uint64_t)((unsigned __int128)k * (n - 1) / (samples - 1)) : 0;
+        bad += pa[i] != pb[i];
+    }
+    if (bad) atomicAdd(count, bad);
+}
+
 // Divergent leaf positions (sorted): refs of keys equal on both sides; counts positions whose keys
 // differ (then the key sets differ there and the caller falls back to the merge-join).
 __global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, DiffSide A, DiffSide B,
@@ -369,6 +390,13 @@ void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_c
     const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2, 256), 2048);
     hipLaunchKernelGGL(k_topdown_level, dim3((uint32_t)blocks), dim3(256), 0, st, ca, cb, child_count, a_par, a_child,
                        r0, r1, fin, nin, fout, nout);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_sample_pfx(const uint64_t *pa, const uint64_t *pb, uint64_t n, uint32_t samples, uint32_t *count,
+                       hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_sample_pfx, dim3(1), dim3(256), 0, st, pa, pb, n, samples, count);
     MKV_LAUNCH_CHECK();
 }
 

@@ -107,6 +107,9 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
 void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, uint64_t a_par, uint64_t a_child,
                           uint64_t r0, uint64_t r1, const uint32_t *fin, const uint32_t *nin, uint32_t *fout,
                           uint32_t *nout, uint64_t max_frontier, hipStream_t st);
+// *count += sampled positions whose sorted key prefixes differ (key-set screen for the top-down walk).
+void launch_sample_pfx(const uint64_t *pa, const uint64_t *pb, uint64_t n, uint32_t samples, uint32_t *count,
+                       hipStream_t st);
 void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
                            uint32_t *nbad, hipStream_t st);
 void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,

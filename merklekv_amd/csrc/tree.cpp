@@ -997,6 +997,8 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 2);
     uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2);  // cnt[l]: frontier size at level l; cnt[L] = 0 (seed)
     MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
+    launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
+    if (d2h_u32(t, cnt + L + 1) != 0) return false;  // key sets differ: straight to the merge-join
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
     for (size_t l = L; l >= 1; --l) {  // parents at level l (none at l == L) -> children at level l-1
