@@ -50,12 +50,15 @@ struct DevBuf {
         cap = 0;
     }
     // Contents are NOT preserved on growth. 256 B of tail padding keeps wide over-reads in bounds.
+    // Growth leaves 1/16 headroom (64 KiB granules) so sizes that fluctuate call to call (diff and
+    // update outputs) do not reallocate — each reallocation is a device-wide sync + free + malloc.
     void *ensure(size_t bytes) {
         if (bytes <= cap && p) return p;
         release();
-        size_t want = bytes + 256;
-        MKV_HIP(hipMalloc(&p, want));
-        cap = bytes;
+        size_t c = bytes + bytes / 16;
+        c = (c + 65535) & ~size_t(65535);
+        MKV_HIP(hipMalloc(&p, c + 256));
+        cap = c;
         return p;
     }
     template <class T> T *as() const { return reinterpret_cast<T *>(p); }
