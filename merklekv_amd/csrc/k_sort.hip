@@ -12,6 +12,8 @@
 // wave-load is 64 consecutive pairs). Pass = per-tile 256-bin histogram -> exclusive scan of the
 // digit-major count matrix -> stable scatter, with in-wave ranks from 8 ballots (peer mask of lanes
 // with the same digit) and per-wave LDS digit counters.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "dev_util.hpp"
 #include "kernels.hpp"
@@ -29,9 +31,19 @@ constexpr int SC_THREADS = 256;
 constexpr int SC_IPT = 8;
 constexpr int SC_TILE = SC_THREADS * SC_IPT;
 
+// Issue priority of the ordering kernels against co-resident leaf-hash waves (MKV_SORT_PRIO, default 3):
+// a uniform scalar load + branch at kernel entry, since s_setprio takes an immediate.
+__device__ int g_sort_prio = 3;
+__device__ __forceinline__ void sort_prio() {
+    const int p = __builtin_amdgcn_readfirstlane(g_sort_prio);
+    if (p >= 3) __builtin_amdgcn_s_setprio(3);
+    else if (p == 2) __builtin_amdgcn_s_setprio(2);
+    else if (p == 1) __builtin_amdgcn_s_setprio(1);
+}
+
 __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                  uint64_t n, uint64_t *__restrict__ pfx, uint32_t *__restrict__ idx) {
-    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
+    sort_prio();
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint64_t a = koff[i], b = koff[i + 1];
@@ -47,7 +59,7 @@ constexpr uint32_t LB_SPIN_LIMIT = 1u << 26;  // bounded spin: sets an error fla
 // Global digit counts of every pass in one read of the keys (counts[p*256 + d]).
 __global__ __launch_bounds__(RS_THREADS) void k_os_hist(const uint64_t *__restrict__ keys, uint64_t n, int bit0,
                                                        int npass, uint32_t *__restrict__ counts) {
-    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
+    sort_prio();
     __shared__ uint32_t h[8][256];
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
     __syncthreads();
@@ -74,7 +86,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                        uint64_t n, int shift, const uint32_t *__restrict__ gcount,
                                                        uint32_t *__restrict__ lookback, uint32_t *__restrict__ ctl) {
-    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
+    sort_prio();
     __shared__ uint64_t sk[RS_TILE];
     __shared__ uint32_t sv[RS_TILE];
     __shared__ uint32_t wcnt[4][256];
@@ -245,13 +257,13 @@ template <class T> void scan_impl(const T *in, T *out, uint64_t n, T *total, voi
 }
 
 // ---- ties / refinement ----
-__global__ void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, uint8_t *__restrict__ tie,
+__global__ void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, int shift, uint8_t *__restrict__ tie,
                             uint32_t *__restrict__ count) {
-    __builtin_amdgcn_s_setprio(3);  // memory-bound: win VALU issue against co-resident leaf-hash waves
+    sort_prio();
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool t = false;
     if (i < n) {
-        t = i > 0 && pfx[i] == pfx[i - 1];
+        t = i > 0 && (pfx[i] >> shift) == (pfx[i - 1] >> shift);
         tie[i] = t;
     } else if (i == n) {
         tie[n] = 0;
@@ -322,6 +334,67 @@ __global__ void k_refine_apply(const uint32_t *__restrict__ pos, uint64_t m, con
     }
     uint64_t bm = __ballot(t);
     if ((threadIdx.x & 63) == 0 && bm) atomicAdd(count, (uint32_t)__popcll(bm));
+}
+
+// Tie runs of at most RS_SMALL_RUN positions (the common case: a few keys sharing every sorted digit)
+// are ordered by one thread each, in place: insertion sort on (8-byte prefix, full key, input index).
+// The input index keeps equal keys in insertion order (stability, merkle.rs:54 last write wins).
+// tie[] becomes full-key equality for those runs; count[0] += equal-key positions (duplicates),
+// count[1] += longer runs, which are left untouched for the general refinement.
+constexpr uint32_t RS_SMALL_RUN = 16;
+__global__ __launch_bounds__(256) void k_refine_small(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                     uint64_t n, uint32_t *__restrict__ perm,
+                                                     uint64_t *__restrict__ pfx, uint8_t *__restrict__ tie,
+                                                     uint32_t *__restrict__ count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || tie[i] || !tie[i + 1]) return;  // run heads only
+    uint64_t j = i + 1;
+    while (j < n && tie[j] && j - i <= RS_SMALL_RUN) ++j;
+    if (j - i > RS_SMALL_RUN) {
+        atomicAdd(&count[1], 1u);
+        return;
+    }
+    auto less = [&](uint64_t pa, uint32_t oa, uint64_t pb, uint32_t ob) {
+        if (pa != pb) return pa < pb;
+        const uint64_t a0 = koff[oa], b0 = koff[ob];
+        const int c = key_cmp(kb + a0, koff[oa + 1] - a0, pa, kb + b0, koff[ob + 1] - b0, pb);
+        return c != 0 ? c < 0 : oa < ob;
+    };
+    for (uint64_t x = i + 1; x < j; ++x) {
+        const uint64_t px = pfx[x];
+        const uint32_t ox = perm[x];
+        uint64_t y = x;
+        while (y > i && less(px, ox, pfx[y - 1], perm[y - 1])) {
+            pfx[y] = pfx[y - 1];
+            perm[y] = perm[y - 1];
+            --y;
+        }
+        pfx[y] = px;
+        perm[y] = ox;
+    }
+    uint32_t dups = 0;
+    for (uint64_t x = i + 1; x < j; ++x) {
+        const uint32_t oa = perm[x - 1], ob = perm[x];
+        const uint64_t pa = pfx[x - 1], pb = pfx[x];
+        bool eq = pa == pb;
+        if (eq) {
+            const uint64_t a0 = koff[oa], b0 = koff[ob];
+            eq = key_cmp(kb + a0, koff[oa + 1] - a0, pa, kb + b0, koff[ob + 1] - b0, pb) == 0;
+        }
+        tie[x] = eq ? 1 : 0;
+        dups += eq;
+    }
+    if (dups) atomicAdd(&count[0], dups);
+}
+
+// After a refinement that started at chunk 0: the prefixes of re-ordered tie-run positions follow.
+__global__ void k_fix_pfx(const uint32_t *__restrict__ pos, uint64_t m, const uint32_t *__restrict__ perm,
+                          const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff, uint64_t *__restrict__ pfx) {
+    uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint32_t p = pos[k], o = perm[p];
+    const uint64_t a = koff[o];
+    pfx[p] = key_chunk(kb + a, koff[o + 1] - a, 0);
 }
 
 __global__ void k_keep_flags(const uint8_t *__restrict__ tie, const uint32_t *__restrict__ perm, uint64_t n,
@@ -416,9 +489,22 @@ inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_d
 
 }  // namespace
 
+static void init_sort_prio() {
+    static bool done = [] {
+        const char *e = getenv("MKV_SORT_PRIO");
+        if (e) {
+            const int v = atoi(e);
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_prio), &v, sizeof(int));
+        }
+        return true;
+    }();
+    (void)done;
+}
+
 void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, uint32_t *idx,
                      hipStream_t st) {
     if (!n) return;
+    init_sort_prio();
     hipLaunchKernelGGL(k_prefix64, grid1d(n), dim3(256), 0, st, kb, koff, n, pfx, idx);
     MKV_LAUNCH_CHECK();
 }
@@ -468,9 +554,57 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
     scan_impl<uint64_t>(in, out, n, total, scratch, st);
 }
 
-void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st) {
-    hipLaunchKernelGGL(k_mark_ties, grid1d(n + 1), dim3(256), 0, st, pfx, n, tie, count);
+void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st, int shift) {
+    hipLaunchKernelGGL(k_mark_ties, grid1d(n + 1), dim3(256), 0, st, pfx, n, shift, tie, count);
     MKV_LAUNCH_CHECK();
+}
+void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint64_t *pfx,
+                         uint8_t *tie, uint32_t *count, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_refine_small, grid1d(n), dim3(256), 0, st, kb, koff, n, perm, pfx, tie, count);
+    MKV_LAUNCH_CHECK();
+}
+void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *kb, const uint64_t *koff,
+                    uint64_t *pfx, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_fix_pfx, grid1d(m), dim3(256), 0, st, pos, m, perm, kb, koff, pfx);
+    MKV_LAUNCH_CHECK();
+}
+
+void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st) {
+    uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
+    MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
+    if (!n) return;
+    const uint32_t hist_blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 16), 2048);
+    hipLaunchKernelGGL(k_os_hist, dim3(hist_blocks), dim3(RS_THREADS), 0, st, k, n, 0, 8, counts);
+    MKV_LAUNCH_CHECK();
+}
+
+bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
+                         void *scratch, hipStream_t st) {
+    if (n <= 1 || !digit_mask) return false;
+    if (n >= (1ull << 30)) throw Error(ST_EINVAL, "radix sort: more than 2^30 - 1 keys per device");
+    const uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
+    uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
+    uint32_t *ctl = counts + 8 * 256;
+    uint32_t *lookback = ctl + 64;
+    const int np = __builtin_popcount(digit_mask);
+    MKV_HIP(hipMemsetAsync(lookback, 0, (size_t)np * nb * 256 * sizeof(uint32_t), st));
+    uint64_t *ki = k, *ko = k2;
+    uint32_t *vi = v, *vo = v2;
+    bool swapped = false;
+    int q = 0;
+    for (int p = 0; p < 8; ++p) {
+        if (!((digit_mask >> p) & 1u)) continue;
+        hipLaunchKernelGGL(k_os_pass, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p, counts + 256 * p,
+                           lookback + (size_t)q * nb * 256, ctl + 4 * p);
+        MKV_LAUNCH_CHECK();
+        ++q;
+        std::swap(ki, ko);
+        std::swap(vi, vo);
+        swapped = !swapped;
+    }
+    return swapped;
 }
 void launch_active_flags(const uint8_t *tie, uint64_t n, uint32_t *flags, hipStream_t st) {
     hipLaunchKernelGGL(k_active_flags, grid1d(n), dim3(256), 0, st, tie, n, flags);

@@ -28,7 +28,22 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
 
 // tie[i] = (pfx[i] == pfx[i-1]) for i>0, tie[0] = 0; *count += number of ties. tie has n+1 entries
 // (tie[n] = 0 sentinel).
-void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st);
+void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st,
+                      int shift = 0);
+// Adaptive prefix sort (tree builds): one histogram read gives all eight byte-digit histograms
+// (counts[p*256+d], p = 0 the least significant byte) in `scratch`; the host then picks the digits
+// worth a pass (radix_prefix_passes: bit p of digit_mask = sort on byte p). Digits below the chosen
+// ones are left to the tie refinement; constant digits are skipped outright.
+void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st);
+bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
+                         void *scratch, hipStream_t st);
+// Orders every tie run of <= 16 positions on the full key in place (one thread per run); tie[] becomes
+// full-key equality there. count[0] += duplicate positions, count[1] += longer runs (left as they are).
+void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint64_t *pfx,
+                         uint8_t *tie, uint32_t *count, hipStream_t st);
+// pfx[pos[k]] = 8-byte prefix of sorted key pos[k] (after a refinement that re-ordered tie runs).
+void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *kb, const uint64_t *koff,
+                    uint64_t *pfx, hipStream_t st);
 // Refinement helpers (see tree.cpp refine_ties for the algorithm).
 void launch_active_flags(const uint8_t *tie, uint64_t n, uint32_t *flags, hipStream_t st);
 void launch_compact_positions(const uint32_t *flags, const uint32_t *scan, uint64_t n, uint32_t *out, hipStream_t st);

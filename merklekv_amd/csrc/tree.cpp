@@ -4,6 +4,7 @@
 #include "mkv_merkle.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -67,7 +68,7 @@ struct mkv_tree {
     // ---- scratch (device) ----
     DevBuf s_kb, s_koff, s_vb, s_voff, s_dig, s_tomb;
     DevBuf s_k1, s_k2, s_v1, s_v2;
-    DevBuf s_tie, s_flags, s_scan, s_pos, s_lens;
+    DevBuf s_tie, s_flags, s_scan, s_pos, s_pos0, s_lens;
     DevBuf s_radix, s_misc;
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
     DevBuf s_nodes2;  // prefix-root scratch levels
@@ -79,6 +80,7 @@ struct mkv_tree {
     uint64_t bm_bits = 0;
     bool bm_dirty = false;
     uint64_t *h_small = nullptr;  // pinned host scalars
+    uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
 
     // ---- profiling ----
     bool prof = false;
@@ -291,7 +293,10 @@ void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, co
 // Tie refinement (R3 on full keys): see k_sort.hip header. perm: sorted order (u32 input indices),
 // tie[i] = position i equals position i-1 on everything compared so far.
 // ---------------------------------------------------------------------------------------------
-void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint8_t *tie) {
+// start_depth 0: the sort covered only the top bits of chunk 0 (ties were marked on those bits), so
+// chunk 0 is compared again and the re-ordered positions' prefixes are rewritten into pfx afterwards.
+void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint8_t *tie,
+                 uint32_t start_depth, uint64_t *pfx) {
     hipStream_t st = t->st2;
     uint32_t *flags = ens<uint32_t>(t->s_flags, n + 1);
     uint32_t *scan = ens<uint32_t>(t->s_scan, n + 1);
@@ -307,14 +312,20 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
     };
     uint64_t m = active();
     if (m == 0) return;
+    const uint64_t m0 = m;
+    uint32_t *pos0 = nullptr;
+    if (start_depth == 0) {  // keep the initial tie-run positions for the prefix rewrite
+        pos0 = ens<uint32_t>(t->s_pos0, m0 + 1);
+        MKV_HIP(hipMemcpyAsync(pos0, pos, m0 * 4, hipMemcpyDeviceToDevice, st));
+    }
     MKV_HIP(hipMemsetAsync(misc + 1, 0, 4, st));
     launch_max_keylen(pos, m, perm, koff, misc + 1, st);
     const uint32_t maxlen = d2h_u32(t, misc + 1, st);
-    const uint32_t D = (maxlen + 7) / 8;  // chunks; chunk 0 already sorted
+    const uint32_t D = (maxlen + 7) / 8;  // chunks
 
-    for (uint32_t depth = 1;; ++depth) {
+    for (uint32_t depth = start_depth;; ++depth) {
         const int use_len = depth >= D;
-        if (depth > 1) {
+        if (depth > start_depth) {
             m = active();
             if (m == 0) break;
         }
@@ -343,6 +354,37 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
         const uint32_t left = d2h_u32(t, misc + 2, st);
         if (left == 0 || use_len) break;
     }
+    if (pos0) launch_fix_pfx(pos0, m0, perm, kb, koff, pfx, st);
+}
+
+// Digits of the 8-byte prefix worth a radix pass, from the one-read histograms (counts[p*256+d],
+// p = 0 least significant). Going down from the most significant byte, digits are added until the
+// summed marginal entropies exceed log2(n) + 8 bits: below that, keys sharing every sorted digit are
+// rare (~n/256 for independent bytes) and the tie refinement orders them on the full key. Constant
+// digits carry no order and are skipped. Returns the digit mask; *lo_bit = lowest sorted bit.
+uint32_t choose_prefix_digits(const uint32_t *counts, uint64_t n, int *lo_bit) {
+    const double need = std::log2((double)(n > 1 ? n : 2)) + 8.0;
+    double cum = 0;
+    int p0 = 0;
+    uint32_t mask = 0;
+    for (int p = 7; p >= 0; --p) {
+        double h = 0;
+        uint32_t mx = 0;
+        for (int d = 0; d < 256; ++d) {
+            const uint32_t c = counts[p * 256 + d];
+            mx = std::max(mx, c);
+            if (c) {
+                const double f = (double)c / (double)n;
+                h -= f * std::log2(f);
+            }
+        }
+        if (mx < n) mask |= 1u << p;
+        cum += h;
+        p0 = p;
+        if (cum >= need) break;
+    }
+    *lo_bit = 8 * p0;
+    return mask;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -366,22 +408,40 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
 
     size_t ps = prof_begin(t, "sort", st);
     launch_prefix64(kb, koff, n_in, k1, v1, st);
-    const bool sw = radix_sort_pairs(k1, v1, k2, v2, n_in, 0, 64, radix, st);
+    int lo_bit = 0;
+    uint32_t digits = 0xFF;
+    if (n_in > 1) {
+        radix_prefix_hist(k1, n_in, radix, st);
+        MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        wait_stream(t, st);
+        digits = choose_prefix_digits(t->h_counts, n_in, &lo_bit);
+    }
+    const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, radix, st);
     DevBuf *pkbuf = sw ? &t->s_k2 : &t->s_k1, *pkalt = sw ? &t->s_k1 : &t->s_k2;
     DevBuf *pmbuf = sw ? &t->s_v2 : &t->s_v1, *pmalt = sw ? &t->s_v1 : &t->s_v2;
     uint64_t *pk = pkbuf->as<uint64_t>();
     uint32_t *perm = pmbuf->as<uint32_t>();
     MKV_HIP(hipMemsetAsync(misc, 0, 4, st));
-    launch_mark_ties(pk, n_in, tie, misc, st);
+    launch_mark_ties(pk, n_in, tie, misc, st, lo_bit);
     prof_end(t, ps);
     const uint32_t nties = n_in ? d2h_u32(t, misc, st) : 0;
+    bool dedup = false;
     if (nties) {
         size_t pr = prof_begin(t, "sort", st);
-        refine_ties(t, kb, koff, n_in, perm, tie);  // reorders perm inside equal-prefix runs only
+        // short tie runs: one in-place pass; longer ones: the general chunk-by-chunk refinement, which
+        // reorders perm (and, when chunk 0 was sorted only in part, pk) inside tie runs only
+        MKV_HIP(hipMemsetAsync(misc + 4, 0, 8, st));
+        launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, st);
+        MKV_HIP(hipMemcpyAsync(t->h_small, misc + 4, 8, hipMemcpyDeviceToHost, st));
+        wait_stream(t, st);
+        const uint32_t dups = reinterpret_cast<uint32_t *>(t->h_small)[0];
+        const uint32_t long_runs = reinterpret_cast<uint32_t *>(t->h_small)[1];
+        if (long_runs) refine_ties(t, kb, koff, n_in, perm, tie, lo_bit ? 0 : 1, pk);
+        dedup = long_runs || dups;
         prof_end(t, pr);
     }
     uint64_t n = n_in;
-    if (nties || tomb) {
+    if (dedup || tomb) {
         size_t pd = prof_begin(t, "sort", st);
         uint32_t *flags = ens<uint32_t>(t->s_flags, n_in + 1);
         uint32_t *scan = ens<uint32_t>(t->s_scan, n_in + 1);
@@ -404,19 +464,8 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
     // a readback there would hold the host until the gather finishes and delay the reduce launches)
     const uint64_t kbytes = staged_inputs ? staged_kbytes : (n_in ? d2h_u64(t, koff + n_in, st) : 0);
-    MKV_HIP(hipEventRecord(t->ev_join, st));
-    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
-    // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
-    // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
-    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
-    t->gather_pending = defer_gather;
-    if (!defer_gather) {
-        size_t pg = prof_begin(t, "gather");
-        launch_gather_digests(perm, dig, n, nodes, t->st);
-        prof_end(t, pg);
-    }
-    // own the keys (storage order): adopt staged uploads, copy borrowed device inputs. The copy is
-    // not needed until the call returns, so it runs on st2 beside the (VALU-bound) reduction.
+    // own the keys (storage order): adopt staged uploads, copy borrowed device inputs. The copy runs on
+    // st2 while the (VALU-bound) leaf hashing still occupies st, ahead of the join.
     t->nstore = n_in;
     t->kbytes = kbytes;
     if (staged_inputs) {
@@ -429,6 +478,17 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         if (kbytes) MKV_HIP(hipMemcpyAsync(dkb, kb, kbytes, hipMemcpyDeviceToDevice, st));
         MKV_HIP(hipMemcpyAsync(dko, koff, (n_in + 1) * 8, hipMemcpyDeviceToDevice, st));
         prof_end(t, pc);
+    }
+    MKV_HIP(hipEventRecord(t->ev_join, st));
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
+    // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
+    // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
+    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
+    t->gather_pending = defer_gather;
+    if (!defer_gather) {
+        size_t pg = prof_begin(t, "gather");
+        launch_gather_digests(perm, dig, n, nodes, t->st);
+        prof_end(t, pg);
     }
 }
 
@@ -575,6 +635,8 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             throw Error(ST_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e2));
         }
         e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 256, hipHostMallocDefault);
+        if (e2 == hipSuccess)
+            e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_counts), 8 * 256 * sizeof(uint32_t), hipHostMallocDefault);
         if (e2 == hipSuccess) {
             int lo = 0, hi = 0;  // aux (ordering) stream at the highest priority: its WGs dispatch first
             (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
@@ -605,6 +667,7 @@ void mkv_tree_destroy(mkv_tree *t) {
         (void)hipEventDestroy(p.b);
     }
     if (t->h_small) (void)hipHostFree(t->h_small);
+    if (t->h_counts) (void)hipHostFree(t->h_counts);
     if (t->st) (void)hipStreamDestroy(t->st);
     delete t;
     (void)hipGetLastError();

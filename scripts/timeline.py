@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
-"""Print the kernel timeline of one build step from a rocprofv3 kernel trace (gpurun_out/prof/trace).
-A step is delimited by k_leaf_hash/k_leaf_persist dispatches. Usage: python scripts/timeline.py [step]"""
+"""Print the kernel timeline of one step from a rocprofv3 kernel trace (gpurun_out/prof/trace).
+A step is delimited by dispatches of the marker kernel(s) (default: the leaf hash).
+Usage: python scripts/timeline.py [step] [marker,marker2] [trace_dir]"""
 import csv
 import os
 import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-rows = list(csv.DictReader(open(os.path.join(ROOT, "gpurun_out", "prof", "trace", "run_kernel_trace.csv"))))
+tdir = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "gpurun_out", "prof", "trace")
+rows = list(csv.DictReader(open(os.path.join(tdir, "run_kernel_trace.csv"))))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 
 
@@ -16,7 +18,8 @@ def name(r):
     return m.group(1) if m else r["Kernel_Name"][:28]
 
 
-starts = [i for i, r in enumerate(rows) if name(r) in ("k_leaf_hash", "k_leaf_persist")]
+markers = sys.argv[2].split(",") if len(sys.argv) > 2 else ["k_leaf_hash", "k_leaf_persist"]
+starts = [i for i, r in enumerate(rows) if name(r) in markers]
 step = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 i0 = starts[step]
 i1 = starts[step + 1] if step + 1 < len(starts) else len(rows)
