@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void k_topdown_level(const uint8_t *__restrict
 __global__ __launch_bounds__(256) void k_sample_pfx(const uint64_t *__restrict__ pa, const uint64_t *__restrict__ pb,
                                                    uint64_t n, uint32_t samples, uint32_t *__restrict__ count) {
     uint32_t bad = 0;
-    for (uint32_t k = threadIdx.x; k < samples; k += blockDim.x) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < samples; k += gridDim.x * blockDim.x) {
         const uint64_t i = samples > 1 ? (uint64_t)((unsigned __int128)k * (n - 1) / (samples - 1)) : 0;
         bad += pa[i] != pb[i];
     }
@@ -396,7 +396,7 @@ void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_c
 void launch_sample_pfx(const uint64_t *pa, const uint64_t *pb, uint64_t n, uint32_t samples, uint32_t *count,
                        hipStream_t st) {
     if (!n) return;
-    hipLaunchKernelGGL(k_sample_pfx, dim3(1), dim3(256), 0, st, pa, pb, n, samples, count);
+    hipLaunchKernelGGL(k_sample_pfx, dim3((samples + 255) / 256), dim3(256), 0, st, pa, pb, n, samples, count);
     MKV_LAUNCH_CHECK();
 }
 

@@ -32,7 +32,20 @@ class ModelShardTree:
         for k, v in zip(keys, values):
             t.insert(k, v)
         self.leaves = [h for _, h in t.leaves()]
+        self.keys = [k for k, _ in t.leaves()]
         return len(self.leaves)
+
+    def upsert(self, keys, values):
+        """Value-only batch on keys already in this shard (the dirty path's contract): leaves change in
+        place, the owned levels are recomputed with the same plan."""
+        t = PyMerkleTree()
+        for k, h in zip(self.keys, self.leaves):
+            t.leaf_map[k] = h
+        for k, v in zip(keys, values):
+            assert k in t.leaf_map, "dirty path: key must already be a leaf"
+            t.insert(k, v)
+        self.leaves = [h for _, h in t.leaves()]
+        self.shard_reduce(self.plan[0][0], self.plan[0][2])
 
     def shard_reduce(self, offset, total):
         self.plan = plan_levels(offset, len(self.leaves), total)

@@ -77,6 +77,55 @@ def test_sharded_root_matches_unsharded_gloo(world, n, cuts):
         assert root == ref.get_root_hash(), rank
 
 
+def _worker_update(rank, world, port, shards, values, updates, q):
+    import torch.distributed as dist
+
+    from merklekv_amd.shard import shard_recombine, sharded_root
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        keys = shards[rank]
+        t = ModelShardTree()
+        root0, counts = sharded_root(t, keys, [values[k] for k in keys], dist, device="cpu")
+        mine = [(k, v) for k, v in updates if k in set(keys)]
+        if mine:
+            t.upsert([k for k, _ in mine], [v for _, v in mine])
+        root1 = shard_recombine(t, dist, sum(counts), device="cpu")
+        q.put((rank, root0, root1))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,cuts", [(2, 1001, [333]), (3, 777, [1, 400]), (3, 50, [0, 49])])
+def test_sharded_update_recombine_gloo(world, n, cuts):
+    """Incremental anti-entropy on shards (configs[4]): each rank applies the value updates of its own
+    key range, then shard_recombine (fringe all-gather + seam combine) gives the updated global root."""
+    keys = [b"key%05d" % i for i in range(n)]
+    values = {k: b"val" + k for k in keys}
+    updates = [(keys[i], b"new%d" % i) for i in range(0, n, 7)] + [(keys[-1], b"last"), (keys[0], b"first")]
+    ref = PyMerkleTree()
+    for k in keys:
+        ref.insert(k, values[k])
+    root0 = ref.get_root_hash()
+    for k, v in updates:
+        ref.insert(k, v)
+    shards = _split(keys, cuts)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_update, args=(r, world, port, shards, values, updates, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, r0, r1 in res:
+        assert r0 == root0 and r1 == ref.get_root_hash(), rank
+
+
 def test_seam_model_exhaustive_small():
     """Every split point of every size up to 40 into 2 and 3 shards (no processes)."""
     import itertools
