@@ -158,6 +158,141 @@ __global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, uint8_t *__re
     wave_append(act, qloc, lout, nout);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Batch merge (key-set changes): the tree's sorted leaves A and a sorted unique batch B
+// (last write per key already chosen, tombstones flagged) merged into the new sorted leaf set. An A
+// leaf survives unless B's cursor holds the same key (replaced or removed, merkle.rs:52-62); a B
+// record survives unless it is a remove. Same merge-path tiling as the diff (k_diff.hip): one binary
+// search per 2048-output tile, 8 outputs per lane, two passes around a scan of the kept counts.
+// ---------------------------------------------------------------------------------------------
+constexpr int UM_THREADS = 256, UM_ITEMS = 8, UM_TILE = UM_THREADS * UM_ITEMS;
+
+__device__ __forceinline__ int cmp_sides(const DiffSide &A, uint64_t i, const DiffSide &B, uint64_t j) {
+    const uint64_t pa = A.pfx[i], pb = B.pfx[j];
+    if (pa != pb) return pa < pb ? -1 : 1;
+    uint64_t la, lb;
+    const uint8_t *ka = tree_key(A, i, &la), *kb = tree_key(B, j, &lb);
+    return key_cmp(ka, la, pa, kb, lb, pb);
+}
+
+// Number of A elements among the first d outputs of the merge (A first on equal keys).
+__device__ uint64_t um_split(const DiffSide &A, const DiffSide &B, uint64_t d, uint64_t lo, uint64_t hi) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (cmp_sides(A, mid, B, d - 1 - mid) <= 0) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void k_umerge_partition(DiffSide A, DiffSide B, uint64_t ntiles, uint64_t *__restrict__ split) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    const uint64_t M = A.n + B.n;
+    const uint64_t d = t * UM_TILE < M ? t * UM_TILE : M;
+    split[t] = um_split(A, B, d, d > B.n ? d - B.n : 0, d < A.n ? d : A.n);
+}
+
+struct UmLane {
+    uint64_t i, j;   // cursors at the lane's first output
+    uint32_t fromA, keep, cnt;
+};
+
+__device__ __forceinline__ UmLane um_lane(const DiffSide &A, const DiffSide &B, const uint8_t *tomb,
+                                          const uint64_t *split) {
+    UmLane r{0, 0, 0, 0, 0};
+    const uint64_t M = A.n + B.n;
+    const uint64_t t = blockIdx.x;
+    const uint64_t d0 = t * UM_TILE + (uint64_t)threadIdx.x * UM_ITEMS;
+    if (d0 >= M) return r;
+    const uint64_t a0 = split[t], a1 = split[t + 1];
+    const uint64_t b0 = t * UM_TILE - a0;
+    const uint64_t dt1 = (t + 1) * UM_TILE < M ? (t + 1) * UM_TILE : M;
+    const uint64_t b1 = dt1 - a1;
+    // lane diagonal inside the tile window [a0, a1) x [b0, b1)
+    const uint64_t dl = d0 - t * UM_TILE, na = a1 - a0, nb = b1 - b0;
+    const uint64_t lo = dl > nb ? dl - nb : 0, hi = dl < na ? dl : na;
+    uint64_t l = lo, h = hi;
+    while (l < h) {
+        const uint64_t mid = (l + h) >> 1;
+        if (cmp_sides(A, a0 + mid, B, b0 + dl - 1 - mid) <= 0) l = mid + 1;
+        else h = mid;
+    }
+    uint64_t i = a0 + l, j = b0 + (dl - l);
+    r.i = i;
+    r.j = j;
+    for (int s = 0; s < UM_ITEMS; ++s) {
+        if (d0 + s >= M) break;
+        bool takeA;
+        int c = 1;
+        if (i >= A.n) takeA = false;
+        else if (j >= B.n) takeA = true;
+        else {
+            c = cmp_sides(A, i, B, j);
+            takeA = c <= 0;
+        }
+        bool keep;
+        if (takeA) {
+            keep = !(j < B.n && c == 0);  // B holds the same key: replaced or removed
+            r.fromA |= 1u << s;
+            ++i;
+        } else {
+            keep = !(tomb && tomb[B.perm[j]]);
+            ++j;
+        }
+        if (keep) r.keep |= 1u << s;
+    }
+    r.cnt = (uint32_t)__popc(r.keep);
+    return r;
+}
+
+__global__ __launch_bounds__(UM_THREADS) void k_umerge_count(DiffSide A, DiffSide B, const uint8_t *__restrict__ tomb,
+                                                            const uint64_t *__restrict__ split,
+                                                            uint64_t *__restrict__ tilecnt) {
+    __shared__ uint64_t lds[16];
+    const UmLane r = um_lane(A, B, tomb, split);
+    uint64_t tot;
+    (void)block_excl_scan<uint64_t>((uint64_t)r.cnt, lds, &tot);
+    if (threadIdx.x == 0) tilecnt[blockIdx.x] = tot;
+}
+
+// Outputs: pfx_out / perm_out (storage index; batch records stored after the tree's nstore_a) and the
+// new leaf level dig_out (32 B per leaf).
+__global__ __launch_bounds__(UM_THREADS) void k_umerge_write(DiffSide A, DiffSide B, const uint8_t *__restrict__ tomb,
+                                                            const uint64_t *__restrict__ split,
+                                                            const uint64_t *__restrict__ tileoff, uint32_t nstore_a,
+                                                            uint64_t *__restrict__ pfx_out,
+                                                            uint32_t *__restrict__ perm_out,
+                                                            uint8_t *__restrict__ dig_out) {
+    __shared__ uint64_t lds[16];
+    const UmLane r = um_lane(A, B, tomb, split);
+    uint64_t o = block_excl_scan<uint64_t>((uint64_t)r.cnt, lds, nullptr) + tileoff[blockIdx.x];
+    uint64_t i = r.i, j = r.j;
+    for (int s = 0; s < UM_ITEMS; ++s) {
+        const bool fa = (r.fromA >> s) & 1u;
+        const bool kp = (r.keep >> s) & 1u;
+        if (kp) {
+            const uint4 *src;
+            if (fa) {
+                pfx_out[o] = A.pfx[i];
+                perm_out[o] = A.perm[i];
+                src = reinterpret_cast<const uint4 *>(A.dig + 32 * i);
+            } else {
+                const uint32_t bs = B.perm[j];
+                pfx_out[o] = B.pfx[j];
+                perm_out[o] = nstore_a + bs;
+                src = reinterpret_cast<const uint4 *>(B.dig + 32ull * bs);
+            }
+            uint4 *dst = reinterpret_cast<uint4 *>(dig_out + 32 * o);
+            dst[0] = src[0];
+            dst[1] = src[1];
+            ++o;
+        }
+        if (fa) ++i;
+        else ++j;
+    }
+}
+
 inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_div(n ? n : 1, bs)); }
 
 }  // namespace
@@ -180,6 +315,31 @@ void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *node
                         const uint32_t *nin, uint32_t *lout, uint32_t *nout, hipStream_t st) {
     if (!max_entries) return;
     hipLaunchKernelGGL(k_dirty_level, grid1d(max_entries), dim3(256), 0, st, L, nodes, bm, lin, nin, lout, nout);
+    MKV_LAUNCH_CHECK();
+}
+
+size_t umerge_scratch_bytes(uint64_t M) {
+    const uint64_t nt = ceil_div(M ? M : 1, UM_TILE);
+    return (nt + 2) * sizeof(uint64_t) * 2 + scan_scratch_bytes(nt + 1) + 1024;
+}
+
+void launch_umerge(const DiffSide &A, const DiffSide &B, const uint8_t *tomb, uint32_t nstore_a, void *scratch,
+                   uint64_t *pfx_out, uint32_t *perm_out, uint8_t *dig_out, uint64_t *count, hipStream_t st) {
+    const uint64_t M = A.n + B.n;
+    if (M == 0) {
+        MKV_HIP(hipMemsetAsync(count, 0, sizeof(uint64_t), st));
+        return;
+    }
+    const uint64_t nt = ceil_div(M, UM_TILE);
+    uint64_t *split = reinterpret_cast<uint64_t *>(scratch);
+    uint64_t *tcnt = split + (nt + 2);
+    void *sc = tcnt + (nt + 2);
+    hipLaunchKernelGGL(k_umerge_partition, grid1d(nt + 1), dim3(256), 0, st, A, B, nt, split);
+    hipLaunchKernelGGL(k_umerge_count, dim3((uint32_t)nt), dim3(UM_THREADS), 0, st, A, B, tomb, split, tcnt);
+    MKV_LAUNCH_CHECK();
+    exclusive_scan_u64(tcnt, tcnt, nt, count, sc, st);
+    hipLaunchKernelGGL(k_umerge_write, dim3((uint32_t)nt), dim3(UM_THREADS), 0, st, A, B, tomb, split, tcnt, nstore_a,
+                       pfx_out, perm_out, dig_out);
     MKV_LAUNCH_CHECK();
 }
 

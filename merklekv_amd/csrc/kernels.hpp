@@ -153,6 +153,14 @@ struct DirtyLevel {
 void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
                         const uint32_t *nin, uint32_t *lout, uint32_t *nout, hipStream_t st);
 
+// Batch merge (k_update.hip): A = the tree's sorted leaves (dig = leaf level, indexed by position),
+// B = sorted unique batch (perm = batch storage index, dig = batch digests in storage order, tomb =
+// remove flags in batch storage order or null). Writes the surviving leaves' prefixes, storage indices
+// (batch records at nstore_a + index) and digests; *count (device) = new leaf count.
+size_t umerge_scratch_bytes(uint64_t M);
+void launch_umerge(const DiffSide &A, const DiffSide &B, const uint8_t *tomb, uint32_t nstore_a, void *scratch,
+                   uint64_t *pfx_out, uint32_t *perm_out, uint8_t *dig_out, uint64_t *count, hipStream_t st);
+
 // ---- synthetic generator (k_gen.hip) — bench/test utility, not part of the reference API ----
 void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
                         uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb, uint64_t *voff,

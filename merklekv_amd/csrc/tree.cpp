@@ -77,6 +77,8 @@ struct mkv_tree {
     DevBuf d_seam, d_S, d_fr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
+    // batch merge (key-set changes): batch tombstones, merged prefixes / permutation / levels, count
+    DevBuf u_tomb, m_pfx, m_perm, m_nodes, m_cnt;
     uint64_t bm_bits = 0;
     bool bm_dirty = false;
     uint64_t *h_small = nullptr;  // pinned host scalars
@@ -392,12 +394,16 @@ uint32_t choose_prefix_digits(const uint32_t *counts, uint64_t n, int *lo_bit) {
 // Produces sorted unique keys (last write wins), leaf level, and the level plan for [o, o+n) of N
 // (N == UINT64_MAX: unsharded, N = n).
 // ---------------------------------------------------------------------------------------------
-void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
-                       bool staged_inputs, uint64_t staged_kbytes, bool defer_gather) {
-    // Ordering work runs on the aux stream and overlaps the VALU-bound leaf hashing already enqueued on
-    // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
+// Sorted unique view (R3 order, last write wins) of n_in records on the aux stream: returns the scratch
+// buffers holding the sorted 8-byte prefixes and storage indices. drop_tomb: tombstoned records (after
+// dedup) are dropped; otherwise they stay, flagged by tomb[storage index].
+struct SortedSet {
+    DevBuf *pk, *pm;
+    uint64_t n;
+};
+SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
+                      bool drop_tomb) {
     hipStream_t st = t->st2;
-    const uint8_t *dig = t->s_dig.as<uint8_t>();
     uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
     uint64_t *k2 = ens<uint64_t>(t->s_k2, n_in + 1);
     uint32_t *v1 = ens<uint32_t>(t->s_v1, n_in + 1);
@@ -441,12 +447,12 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         prof_end(t, pr);
     }
     uint64_t n = n_in;
-    if (dedup || tomb) {
+    if (dedup || (tomb && drop_tomb)) {
         size_t pd = prof_begin(t, "sort", st);
         uint32_t *flags = ens<uint32_t>(t->s_flags, n_in + 1);
         uint32_t *scan = ens<uint32_t>(t->s_scan, n_in + 1);
         launch_keep_flags(tie, perm, n_in, UINT64_MAX, flags, st);  // dedup: keep the last write
-        if (tomb) launch_clear_tomb(tomb, perm, n_in, flags, st);   // removed keys never survive
+        if (tomb && drop_tomb) launch_clear_tomb(tomb, perm, n_in, flags, st);  // removed keys never survive
         exclusive_scan_u32(flags, scan, n_in, misc + 3, radix, st);
         launch_compact_u32(perm, flags, scan, n_in, pmalt->as<uint32_t>(), st);
         launch_compact_u64(pk, flags, scan, n_in, pkalt->as<uint64_t>(), st);
@@ -456,6 +462,19 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         std::swap(pmbuf, pmalt);
         perm = pmbuf->as<uint32_t>();
     }
+    return SortedSet{pkbuf, pmbuf, n};
+}
+
+void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
+                       bool staged_inputs, uint64_t staged_kbytes, bool defer_gather) {
+    // Ordering work runs on the aux stream and overlaps the VALU-bound leaf hashing already enqueued on
+    // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
+    hipStream_t st = t->st2;
+    const uint8_t *dig = t->s_dig.as<uint8_t>();
+    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true);
+    DevBuf *pkbuf = S.pk, *pmbuf = S.pm;
+    const uint64_t n = S.n;
+    uint32_t *perm;
     t->n = n;
     // adopt the sorted prefixes and the permutation
     swap_buf(t->pfx, *pkbuf);
@@ -759,7 +778,106 @@ mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
     });
 }
 
+static DiffSide side_of(const mkv_tree *t);
+
+static bool merge_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("MKV_UPDATE_MERGE");  // A/B knob: 0 = re-sort everything
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Key-set-changing batch on a non-empty unsharded tree: only the batch is sorted (last
+// write per key wins, tombstones kept as flags), then merged with the tree's sorted leaves (Kernel E
+// merge: replaced / removed leaves drop out, existing digests are reused, never re-hashed), and the
+// levels are reduced again. Batch key records are appended to the key storage; the storage is
+// repacked in sorted order once dead records outnumber live ones.
+static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
+    size_t ptot = prof_begin(t, "total_build");
+    const uint64_t nb = keys.n;
+    const uint64_t kbn = keys.offsets[nb] - keys.offsets[0];
+    ens<uint8_t>(t->u_kb, kbn + 16);
+    ens<uint64_t>(t->u_koff, nb + 1);
+    upload_blob(t, keys, t->u_kb, t->u_koff);
+    if (values) {
+        ens<uint8_t>(t->u_vb, values->offsets[nb] - values->offsets[0] + 16);
+        ens<uint64_t>(t->u_voff, nb + 1);
+        upload_blob(t, *values, t->u_vb, t->u_voff);
+    }
+    const uint8_t *tomb = nullptr;
+    if (is_remove) {
+        uint8_t *tb = ens<uint8_t>(t->u_tomb, nb + 1);
+        MKV_HIP(hipMemcpyAsync(tb, is_remove, nb, hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipStreamSynchronize(t->st));
+        tomb = tb;
+    }
+    fork_streams(t);
+    uint8_t *bdig = nullptr;
+    if (values) {
+        bdig = ens<uint8_t>(t->u_dig, nb * 32);
+        size_t pl = prof_begin(t, "leaf_hash");
+        launch_leaf_hash(t->u_kb.as<uint8_t>(), t->u_koff.as<uint64_t>(), t->u_vb.as<uint8_t>(),
+                         t->u_voff.as<uint64_t>(), nb, bdig, t->st);
+        prof_end(t, pl);
+    }
+    const SortedSet B = sort_unique(t, t->u_kb.as<uint8_t>(), t->u_koff.as<uint64_t>(), nb, tomb, false);
+    MKV_HIP(hipEventRecord(t->ev_join, t->st2));
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
+    const DiffSide A = side_of(t);
+    DiffSide Bs;
+    Bs.kb = t->u_kb.as<uint8_t>();
+    Bs.koff = t->u_koff.as<uint64_t>();
+    Bs.perm = B.pm->as<uint32_t>();
+    Bs.pfx = B.pk->as<uint64_t>();
+    Bs.dig = bdig;
+    Bs.n = B.n;
+    const uint64_t M = A.n + Bs.n;
+    if (t->nstore + nb >= 0xFFFFFFF0ull) throw Error(ST_EINVAL, "too many stored key records");
+    uint64_t *npfx = ens<uint64_t>(t->m_pfx, M + 1);
+    uint32_t *nperm = ens<uint32_t>(t->m_perm, M + 1);
+    uint8_t *nnodes = ens<uint8_t>(t->m_nodes, 32 * (2 * M + 66));
+    uint64_t *cnt = ens<uint64_t>(t->m_cnt, 4);
+    void *scr = t->d_diffscr.ensure(umerge_scratch_bytes(M));
+    size_t pm = prof_begin(t, "merge");
+    launch_umerge(A, Bs, tomb, (uint32_t)t->nstore, scr, npfx, nperm, nnodes, cnt, t->st);
+    prof_end(t, pm);
+    // key storage: the tree's records, then the batch's (offsets shifted by the tree's byte count)
+    const uint64_t nst = t->nstore, kbytes = t->kbytes;
+    uint8_t *nkb = ens<uint8_t>(t->s_kb, kbytes + kbn + 16);
+    uint64_t *nko = ens<uint64_t>(t->s_koff, nst + nb + 1);
+    if (kbytes) MKV_HIP(hipMemcpyAsync(nkb, t->kb.p, kbytes, hipMemcpyDeviceToDevice, t->st));
+    if (kbn) MKV_HIP(hipMemcpyAsync(nkb + kbytes, t->u_kb.p, kbn, hipMemcpyDeviceToDevice, t->st));
+    MKV_HIP(hipMemcpyAsync(nko, t->koff.p, (nst + 1) * 8, hipMemcpyDeviceToDevice, t->st));
+    launch_add_offset_u64(t->u_koff.as<uint64_t>() + 1, nb, kbytes, nko + nst + 1, t->st);
+    const uint64_t n_new = d2h_u64(t, cnt);
+    swap_buf(t->kb, t->s_kb);
+    swap_buf(t->koff, t->s_koff);
+    swap_buf(t->pfx, t->m_pfx);
+    swap_buf(t->perm, t->m_perm);
+    swap_buf(t->nodes, t->m_nodes);
+    t->kbytes = kbytes + kbn;
+    t->nstore = nst + nb;
+    t->n = n_new;
+    t->gather_pending = false;
+    if (t->nstore > 2 * t->n + 4096) {  // repack live keys in sorted order: perm becomes the identity
+        const uint64_t bytes = pack_sorted_keys(t, t->s_kb, t->s_koff, 0, 0);
+        swap_buf(t->kb, t->s_kb);
+        swap_buf(t->koff, t->s_koff);
+        launch_iota_u32(t->perm.as<uint32_t>(), t->n, t->st);
+        t->nstore = t->n;
+        t->kbytes = bytes;
+    }
+    finish_unsharded(t);
+    prof_end(t, ptot);
+    sync(t);
+}
+
 static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
+    if (t->n > 0 && !t->sharded && !t->prepared && merge_enabled()) {
+        merge_batch(t, keys, values, is_remove);
+        return;
+    }
     size_t ptot = prof_begin(t, "total_build");
     uint64_t kbytes = 0;
     const uint64_t tot = stage_batch(t, keys, values, is_remove, &kbytes);
@@ -776,8 +894,6 @@ static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     prof_end(t, ptot);
     sync(t);
 }
-
-static DiffSide side_of(const mkv_tree *t);
 
 // Dirty-path update (k_update.hip) for a batch whose keys are all leaves already: same key order and
 // level plan, so only changed leaves and their ancestors are rehashed. Batch records are device

@@ -167,6 +167,17 @@ class MerkleTree:
         self._cache.clear()
         check(lib().mkv_tree_upsert_device(self._h, Blob(kb_ptr, koff_ptr, n), Blob(vb_ptr, voff_ptr, n)))
 
+    def apply(self, keys, values, is_remove) -> None:
+        """Mixed ordered batch: record i is remove(k_i) if is_remove[i] else insert(k_i, v_i)."""
+        self._flush()
+        self._cache.clear()
+        pk, pv = pack_blob(keys), pack_blob(values)
+        rm = np.ascontiguousarray(np.asarray(is_remove, dtype=np.uint8))
+        if pk.n != pv.n or rm.size != pk.n:
+            raise ValueError("keys, values and is_remove differ in length")
+        if pk.n:
+            check(lib().mkv_tree_apply(self._h, pk.blob(), pv.blob(), rm.ctypes.data))
+
     def remove_many(self, keys) -> None:
         self._flush()
         self._cache.clear()

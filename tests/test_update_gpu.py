@@ -172,3 +172,47 @@ def test_sharded_upsert_new_key_rejected():
     from merklekv_amd import MerkleError
     with pytest.raises(MerkleError):
         trees[0].upsert([b"not-a-leaf"], [b"x"])
+
+
+def test_merge_batches_key_set_changes_vs_oracle():
+    """Key-set-changing batches take the sorted-batch merge: new keys, value updates,
+    removes (present and absent), duplicates within a batch in both orders, and enough rounds that the
+    key storage is repacked. Every round: root + all levels + leaves equal the oracle's."""
+    rng = np.random.default_rng(77)
+    n = 3000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    state = dict(zip(split_blob(kb, ko), split_blob(vb, vo)))
+    for rnd in range(6):
+        keys, vals, rm = [], [], []
+        pool = sorted(state)
+        for _ in range(2500):
+            r = rng.random()
+            if r < 0.35 and pool:
+                k = pool[int(rng.integers(0, len(pool)))]          # update an existing key
+                keys.append(k); vals.append(b"u%d-%d" % (rnd, len(keys))); rm.append(0)
+            elif r < 0.6 and pool:
+                k = pool[int(rng.integers(0, len(pool)))]          # remove an existing key
+                keys.append(k); vals.append(b""); rm.append(1)
+            elif r < 0.65:
+                keys.append(b"absent-%d" % int(rng.integers(0, 10**9))); vals.append(b""); rm.append(1)
+            else:
+                k = b"new-%d-%d" % (rnd, int(rng.integers(0, 10**3)))  # repeats: in-batch duplicates
+                keys.append(k); vals.append(b"n%d" % len(keys)); rm.append(0)
+        # explicit duplicate orders: insert-then-remove and remove-then-insert of the same key
+        keys += [b"dup-a-%d" % rnd, b"dup-a-%d" % rnd, b"dup-b-%d" % rnd, b"dup-b-%d" % rnd]
+        vals += [b"x", b"", b"", b"y"]
+        rm += [0, 1, 1, 0]
+        t.apply(keys, vals, rm)
+        for k, v, r in zip(keys, vals, rm):  # sequential semantics (merkle.rs:52-62)
+            if r:
+                state.pop(k, None)
+            else:
+                state[k] = v
+        items = sorted(state.items())
+        o = coracle.OracleTree.build(*pack([k for k, _ in items]), *pack([v for _, v in items]))
+        assert len(t) == len(o), rnd
+        assert t.get_root_hash() == o.root(), rnd
+        assert _levels(t) == _oracle_levels(o), rnd
+        assert [k.encode("utf-8", "surrogateescape") for k, _ in t.leaves()] == [k for k, _ in items], rnd
