@@ -230,6 +230,31 @@ def wl_build(ctx, args):
         ums, ucnt = tree.prof_read("update")
         upd_info = {"tree_keys": n, "batch": m, "ms": dt * 1e3, "device_ms": ums / max(ucnt, 1),
                     "update_keys_per_s": m / dt, "mode": "dirty-path rehash (value-only batch)"}
+        # key-set change: 0.1 % mixed batch (80 % value updates, 10 % removes, 10 % new keys) through the
+        # host API (mkv_tree_apply: batch sort + merge into the sorted leaves + reduction)
+        import numpy as np
+        sel_h = sel.cpu().numpy()
+        kv_h = kb[: n * KLEN].view(n, KLEN)[sel].cpu().numpy()
+        nnew = m // 10
+        nk, _, _, _ = ctx.records(nnew, idx0=10**12)
+        keys_h = np.concatenate([kv_h[: m - nnew], nk[: nnew * KLEN].view(nnew, KLEN).cpu().numpy()])
+        rm_h = np.zeros(m, np.uint8)
+        rm_h[int(m * 0.8): m - nnew] = 1
+        vals_h = np.frombuffer(bytes(ALPHA * 2)[:VLEN] * m, np.uint8).reshape(m, VLEN)
+        koff_h = np.arange(0, m + 1, dtype=np.uint64) * KLEN
+        voff_h = np.arange(0, m + 1, dtype=np.uint64) * VLEN
+        del sel_h
+        ks_times = []
+        for _ in range(3):
+            tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tree.apply((keys_h.reshape(-1), koff_h), (vals_h.reshape(-1), voff_h), rm_h)
+            ks_times.append(time.perf_counter() - t0)
+        dt = min(ks_times)
+        upd_info["keyset_batch"] = {"batch": m, "new": nnew, "removed": int(rm_h.sum()), "ms": dt * 1e3,
+                                    "keys_per_s": m / dt, "leaves_after": len(tree),
+                                    "mode": "batch sort + merge into sorted leaves + reduction (host blobs)"}
         del treeB, vb2
 
     cpu = None
