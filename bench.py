@@ -6,14 +6,14 @@ Default workload (`--workload build`, what the driver runs): a step = one full t
 keys, 100-B values, generated on the device, already resident in HBM when the timed region starts).
 With N>1 ranks (torch.distributed.run, one process per GPU) each rank owns a contiguous key range of n
 records (weak scaling); the step adds the RCCL all-gathers of shard leaf counts and seam fringes and
-the on-device seam combine that yields the global root on every rank. `--n 125000000` at N=8 is
+the on-device seam combine that yields the global root on every rank. `--records 125000000` at N=8 is
 configs[3] (1B keys over 8 GPUs); at N=1 it is one shard of it.
 
 Other BASELINE configs (run explicitly; their JSON lines are committed under profiles/):
   --workload diff         configs[2]: two 100M-key replicas, (a) 0.1 % value-only divergence (top-down
                           walk) and (b) 0.1 % mixed 80/10/10 change/delete/insert (merge-join); a step =
                           one diff_keys incl. compaction and the D2H of the divergent key list.
-  --workload incremental  configs[4]: a 1B-key tree (125M keys per GPU at N=8; --n per GPU), 8 replicas
+  --workload incremental  configs[4]: a 1B-key tree (125M keys per GPU at N=8; --records per GPU), 8 replicas
                           = base + 7 variants; a step = each variant applies its own 1M-key value-update
                           batch (125K per GPU; dirty-path rehash + fringe/seam recombine) and the base is
                           diffed against all 7 (top-down).
@@ -55,12 +55,21 @@ class Ctx:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.dist = None
+        # Rehearsal knobs for a one-GPU box (never set by the driver): MKV_BENCH_SAME_GPU=1 puts every
+        # rank on device 0, MKV_DIST_BACKEND=gloo runs the collectives on the host.
+        if os.environ.get("MKV_BENCH_SAME_GPU") == "1":
+            self.local = 0
+        backend = os.environ.get("MKV_DIST_BACKEND", "nccl")  # "nccl" is RCCL over xGMI on ROCm
+        self.dev = torch.device("cuda", self.local)
+        self.coll = self.dev if backend == "nccl" else torch.device("cpu")
         if self.world > 1:
             import torch.distributed as dist_mod
             self.dist = dist_mod
             torch.cuda.set_device(self.local)
-            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", self.local))
-        self.dev = torch.device("cuda", self.local)
+            if backend == "nccl":
+                dist_mod.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist_mod.init_process_group(backend)
         torch.cuda.set_device(self.local)
 
     def barrier(self):
@@ -71,14 +80,14 @@ class Ctx:
     def max_over_ranks(self, x: float) -> float:
         if self.dist is None:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.coll)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_over_ranks(self, x: int) -> int:
         if self.dist is None:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.int64, device=self.dev)
+        t = self.torch.tensor([x], dtype=self.torch.int64, device=self.coll)
         self.dist.all_reduce(t)
         return int(t.item())
 
@@ -103,15 +112,15 @@ class Ctx:
             return tree.get_root_hash(), n
         from merklekv_amd.shard import sharded_root
         root, counts = sharded_root(tree, (kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), None,
-                                    self.dist, device=self.dev, on_device=True)
+                                    self.dist, device=self.coll, on_device=True)
         return root, sum(counts)
 
     def check_roots_agree(self, root: bytes):
         if self.dist is None or root is None:
             return
         torch = self.torch
-        rt = torch.frombuffer(bytearray(root), dtype=torch.uint8).to(self.dev)
-        allr = torch.empty(self.world * 32, dtype=torch.uint8, device=self.dev)
+        rt = torch.frombuffer(bytearray(root), dtype=torch.uint8).to(self.coll)
+        allr = torch.empty(self.world * 32, dtype=torch.uint8, device=self.coll)
         self.dist.all_gather_into_tensor(allr, rt)
         roots = allr.cpu().numpy().reshape(self.world, 32)
         assert (roots == roots[0]).all(), "ranks disagree on the global root"
@@ -400,7 +409,7 @@ def wl_incremental(ctx, args):
         for t, (ukb, uko, uvb, uvo, _) in zip(variants, batches):
             t.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
             if ctx.world > 1:
-                shard_recombine(t, ctx.dist, N, device=ctx.dev)
+                shard_recombine(t, ctx.dist, N, device=ctx.coll)
         return [base.diff_keys_packed(t) for t in variants]
 
     for _ in range(args.warmup):
@@ -516,7 +525,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("build", "diff", "incremental"), default="build")
-    ap.add_argument("--n", type=int, default=None,
+    ap.add_argument("--records", dest="n", type=int, default=None,
                     help="records per GPU (default: 10M build, 100M diff, 125M incremental)")
     ap.add_argument("--batch", type=int, default=125_000, help="incremental: updates per variant per GPU")
     ap.add_argument("--replicas", type=int, default=8, help="incremental: base + variants")

@@ -32,8 +32,8 @@ __device__ void gen_field(uint64_t seed, uint64_t idx, uint32_t field, uint32_t 
             if (cc % 10 == 0 || b == 0) w = gen_word(seed, idx, field, cc / 10);
             uint32_t x = (uint32_t)(w >> (6 * (cc % 10))) & 63u;
             if (cc == 0 && field == 0 && nshards > 1) {
-                uint32_t per = 64 / nshards;
-                x = shard * per + (x & (per - 1));
+                const uint32_t lo = shard * 64 / nshards, hi = (shard + 1) * 64 / nshards;
+                x = lo + x % (hi - lo);  // == shard*per + (x & (per-1)) when nshards | 64
             }
             packed |= (uint32_t)(uint8_t)kAlpha[x] << (8 * b);
         }

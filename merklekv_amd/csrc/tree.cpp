@@ -1527,7 +1527,7 @@ mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, 
                                   uint64_t *koff, uint8_t *vb, uint64_t *voff) {
     MKV_TRY({
         NEED(kb && koff && vb && voff, "null buffer");
-        NEED(nshards >= 1 && nshards <= 64 && (64 % nshards) == 0 && shard < nshards, "bad shard spec");
+        NEED(nshards >= 1 && nshards <= 64 && shard < nshards, "bad shard spec");
         DevGuard g(hip_device);
         launch_gen_records(seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb, voff, nullptr);
         MKV_HIP(hipDeviceSynchronize());

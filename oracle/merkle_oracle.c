@@ -501,8 +501,8 @@ static void gen_chars(uint64_t seed, uint64_t idx, uint32_t field, uint32_t len,
         if (c % 10 == 0) w = orc_gen_word(seed, idx, field, c / 10);
         uint32_t x = (uint32_t)(w >> (6 * (c % 10))) & 63;
         if (c == 0 && field == 0 && nshards > 1) {
-            uint32_t per = 64 / nshards;
-            x = shard * per + (x & (per - 1));
+            const uint32_t lo = shard * 64 / nshards, hi = (shard + 1) * 64 / nshards;
+            x = lo + x % (hi - lo);
         }
         out[c] = (uint8_t)SORTED_ALPHA[x];
     }

@@ -145,8 +145,8 @@ def gen_records(seed: int, idx0: int, n: int, klen: int = 32, vlen: int = 100, r
                 w = gen_word_np(seed, idx, field, c // 10)
             x = ((w >> np.uint64(6 * (c % 10))) & np.uint64(63)).astype(np.int64)
             if c == 0 and restrict and nshards > 1:
-                per = 64 // nshards
-                x = shard * per + (x & (per - 1))
+                lo, hi = shard * 64 // nshards, (shard + 1) * 64 // nshards
+                x = lo + x % (hi - lo)
             out[:, c] = alpha[x]
         mask = np.arange(max(maxlen, 1))[None, :] < lens[:, None]
         return out[mask]

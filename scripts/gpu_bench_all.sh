@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 if [ -n "$FULL" ]; then
   B=""; D=""; I=""
 else
-  B="--n 1000000"; D="--n 1000000"; I="--n 2000000 --batch 2000"
+  B="--records 1000000"; D="--records 1000000"; I="--records 2000000 --batch 2000"
 fi
 set -o pipefail
 timeout -k 10 300 python bench.py --steps 3 --warmup 1 $B > gpurun_out/bench_build.json 2> gpurun_out/bench_build.err || { tail -20 gpurun_out/bench_build.err; exit 1; }

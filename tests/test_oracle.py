@@ -82,7 +82,7 @@ def test_synthetic_c_oracle(oracle_lib, fixtures):
 
 def test_generator_c_matches_numpy(oracle_lib):
     for args in [dict(ragged=False), dict(ragged=True, klen=20, vlen=64), dict(nshards=8, shard=5),
-                 dict(nshards=2, shard=1, vfield=2)]:
+                 dict(nshards=2, shard=1, vfield=2), dict(nshards=3, shard=2), dict(nshards=6, shard=0)]:
         a = gen_records(DEFAULT_SEED, 12345, 300, **args)
         b = oracle_lib.gen_records(DEFAULT_SEED, 12345, 300, **args)
         for x, y in zip(a, b):
