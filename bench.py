@@ -410,7 +410,7 @@ def wl_incremental(ctx, args):
             t.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
             if ctx.world > 1:
                 shard_recombine(t, ctx.dist, N, device=ctx.coll)
-        return [base.diff_keys_packed(t) for t in variants]
+        return base.diff_keys_many_packed(variants)  # one shared top-down walk (mkv_tree_diff_many)
 
     for _ in range(args.warmup):
         diffs = step()
@@ -424,7 +424,7 @@ def wl_incremental(ctx, args):
     ctx.barrier()
     el = ctx.max_over_ranks(time.perf_counter() - t0)
     upd_ms = sum(t.prof_read("update")[0] for t in variants) / (args.steps * (R - 1))
-    diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))
+    diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))  # batched walk: per-pair share
     ok = all(len(d[1]) - 1 == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else
     total_updates = ctx.sum_over_ranks(m) * (R - 1)
     roots = []

@@ -89,11 +89,17 @@ mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *diges
 /* diff_keys(&other) — merkle.rs:171-196: sorted unique keys missing on one side or with different leaf
  * digests. diff_first_key (merkle.rs:199-204) is element 0. Both trees must be on the same device. */
 mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out);
+/* k x diff_keys(a, others[i]) (merkle.rs:171-196), outs[i] as from mkv_tree_diff. Variants with a's level
+ * plan and key set share one top-down walk (configs[4]: a base replica against 7 updated replicas);
+ * the others are diffed pairwise. Results are identical to k separate calls. */
+mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, uint32_t k, mkv_keylist **outs);
 /* HASH <prefix> — server.rs:647-685: root of a fresh tree over the keys starting with prefix
  * (*has_root = 0 when none: the server prints 64 zeros). plen = 0 gives the whole-tree root. */
 mkv_status mkv_tree_prefix_root(const mkv_tree *t, const uint8_t *prefix, uint64_t plen, uint8_t out32[32],
                                 int *has_root);
 
+/* Key i of a list is bytes[offsets[i] .. offsets[i+1]) (offsets has n+1 entries; offsets[0] may be
+ * nonzero). The memory stays valid until mkv_keylist_free. */
 mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets);
 void mkv_keylist_free(mkv_keylist *l);
 

@@ -324,6 +324,57 @@ __global__ __launch_bounds__(256) void k_sample_pfx(const uint64_t *__restrict__
     if (bad) atomicAdd(count, bad);
 }
 
+// ---- batched top-down walk: one base tree against k variants with the same level plan (configs[4]) ----
+// Frontier entries are (variant << 32) | local node index; every level is one launch for all variants.
+__global__ __launch_bounds__(256) void k_topdown_level_batch(const uint8_t *__restrict__ ca, TdVariants V,
+                                                            uint64_t child_off, uint64_t child_count, uint64_t a_par,
+                                                            uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
+                                                            const uint64_t *__restrict__ fin,
+                                                            const uint32_t *__restrict__ nin,
+                                                            uint64_t *__restrict__ fout, uint32_t *__restrict__ nout) {
+    const uint32_t cnt = *nin;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t tot = 2ull * cnt + 2ull * k;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        bool d = false;
+        uint64_t c = UINT64_MAX;
+        uint32_t v = 0;
+        if (t < 2ull * cnt) {
+            const uint64_t e = fin[t >> 1];
+            v = (uint32_t)(e >> 32);
+            c = 2 * ((e & 0xFFFFFFFFull) + a_par) + (t & 1) - a_child;
+        } else if (t < tot) {
+            const uint64_t q = t - 2ull * cnt;
+            v = (uint32_t)(q >> 1);
+            c = (q & 1) ? r1 : r0;
+        }
+        if (c < child_count) d = !digest_eq(ca + 32ull * c, V.nodes[v] + child_off + 32ull * c);
+        const uint64_t m = __ballot(d);
+        uint32_t slot = 0;
+        if (lane == 0 && m) slot = atomicAdd(nout, (uint32_t)__popcll(m));
+        slot = __shfl(slot, 0);
+        if (d) fout[slot + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)v << 32) | c;
+    }
+}
+
+// Sorted (variant, leaf position) entries: keys must be equal on both sides (else that variant's key
+// set differs there: nbad[v]); refs[k] = the base's sorted index; count[v] = first entry of variant v
+// (left untouched — the caller presets all-ones — when v has none).
+__global__ void k_topdown_leaves_batch(const uint64_t *__restrict__ ent, uint64_t m, int pb, DiffSide A,
+                                       const DiffSide *__restrict__ Bs, uint64_t *__restrict__ refs,
+                                       uint32_t *__restrict__ nbad, uint32_t *__restrict__ count) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t e = ent[k];  // (variant << pb) | position
+    const uint32_t v = (uint32_t)(e >> pb);
+    const uint64_t i = e & ((1ull << pb) - 1ull);
+    const DiffSide B = Bs[v];
+    refs[k] = i;
+    if (k == 0 || (uint32_t)(ent[k - 1] >> pb) != v) count[v] = (uint32_t)k;  // segment start of variant v
+    if (cmp_ab(A, i, A.pfx[i], B, i, B.pfx[i]) != 0) atomicAdd(&nbad[v], 1u);
+}
+
 // Divergent leaf positions (sorted): refs of keys equal on both sides; counts positions whose keys
 // differ (then the key sets differ there and the caller falls back to the merge-join).
 __global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, DiffSide A, DiffSide B,
@@ -397,6 +448,37 @@ void launch_sample_pfx(const uint64_t *pa, const uint64_t *pb, uint64_t n, uint3
                        hipStream_t st) {
     if (!n) return;
     hipLaunchKernelGGL(k_sample_pfx, dim3((samples + 255) / 256), dim3(256), 0, st, pa, pb, n, samples, count);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t child_off, uint64_t child_count,
+                                uint64_t a_par, uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
+                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
+                                uint64_t max_frontier, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2 * k, 256), 4096);
+    hipLaunchKernelGGL(k_topdown_level_batch, dim3((uint32_t)blocks), dim3(256), 0, st, ca, V, child_off, child_count,
+                       a_par, a_child, r0, r1, k, fin, nin, fout, nout);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs,
+                                 uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_topdown_leaves_batch, grid1d(m), dim3(256), 0, st, ent, m, pb, A, Bs, refs, nbad, count);
+    MKV_LAUNCH_CHECK();
+}
+
+__global__ void k_pack_entries(const uint64_t *__restrict__ ent, uint64_t m, int pb, uint64_t *__restrict__ key,
+                               uint32_t *__restrict__ val) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t e = ent[k];
+    key[k] = ((e >> 32) << pb) | (e & 0xFFFFFFFFull);
+    val[k] = (uint32_t)k;
+}
+void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_pack_entries, grid1d(m), dim3(256), 0, st, ent, m, pb, key, val);
     MKV_LAUNCH_CHECK();
 }
 

@@ -131,6 +131,20 @@ void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, co
                          hipStream_t st);
 void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,
                       uint8_t *out, hipStream_t st);
+// Batched top-down walk (one base vs up to TD_MAX_VARIANTS trees with the same level plan).
+constexpr int TD_MAX_VARIANTS = 64;
+struct TdVariants {
+    const uint8_t *nodes[TD_MAX_VARIANTS];  // each variant's node array (levels at the base's offsets)
+};
+void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t child_off, uint64_t child_count,
+                                uint64_t a_par, uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
+                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
+                                uint64_t max_frontier, hipStream_t st);
+// ent: sorted (variant << pb) | position.
+void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs,
+                                 uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st);
+// key[k] = (variant << pb) | position of frontier entry (variant << 32) | position; val[k] = k.
+void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st);
 // Prefix range [lo, hi) of sorted keys starting with prefix (single-thread binary search).
 void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t plen, uint64_t *lohi, hipStream_t st);
 

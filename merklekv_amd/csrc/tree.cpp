@@ -8,6 +8,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -37,9 +39,50 @@ struct EvPair {
 
 }  // namespace
 
+// Key lists live in pinned host blocks that the device writes directly (no pageable staging, no extra
+// host copy); a batched diff's per-variant lists are views sharing one block. Blocks are recycled
+// through a small pool because pinning tens of MB costs milliseconds.
+namespace {
+std::mutex g_pool_mu;
+std::vector<std::pair<uint8_t *, size_t>> g_pool;  // free pinned blocks (never released at exit)
+
+struct PinnedBlock {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    explicit PinnedBlock(size_t bytes) {
+        {
+            std::lock_guard<std::mutex> lk(g_pool_mu);
+            size_t best = SIZE_MAX;
+            for (size_t i = 0; i < g_pool.size(); ++i)
+                if (g_pool[i].second >= bytes && (best == SIZE_MAX || g_pool[i].second < g_pool[best].second))
+                    best = i;
+            if (best != SIZE_MAX) {
+                p = g_pool[best].first;
+                cap = g_pool[best].second;
+                g_pool.erase(g_pool.begin() + (long)best);
+                return;
+            }
+        }
+        cap = std::max<size_t>(bytes + bytes / 4, 4096);
+        MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), cap, hipHostMallocDefault));
+    }
+    PinnedBlock(const PinnedBlock &) = delete;
+    PinnedBlock &operator=(const PinnedBlock &) = delete;
+    ~PinnedBlock() {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        if (g_pool.size() < 8) g_pool.emplace_back(p, cap);
+        else (void)hipHostFree(p);
+    }
+};
+}  // namespace
+
 struct mkv_keylist {
-    std::vector<uint8_t> bytes;
-    std::vector<uint64_t> offsets;  // n+1
+    std::shared_ptr<PinnedBlock> blk;  // null for an empty list
+    const uint8_t *bytes = nullptr;
+    const uint64_t *offsets = nullptr;  // n+1 entries; offsets[0] may be nonzero (a view into a shared block)
+    uint64_t n = 0;
+    uint64_t zero = 0;
+    mkv_keylist() { offsets = &zero; }
 };
 
 struct mkv_tree {
@@ -74,6 +117,7 @@ struct mkv_tree {
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
+    DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
     DevBuf d_seam, d_S, d_fr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
@@ -1102,22 +1146,35 @@ mkv_status mkv_tree_level(const mkv_tree *t, uint32_t level, uint64_t *count, ui
     });
 }
 
+// Fill a key list from device offsets (m+1, starting at 0) and key bytes.
+static void keylist_fill(mkv_tree *t, mkv_keylist *l, const uint64_t *d_off, const uint8_t *d_bytes, uint64_t m,
+                         uint64_t bytes) {
+    l->n = m;
+    if (!m) return;
+    l->blk = std::make_shared<PinnedBlock>(8 * (m + 1) + bytes + 16);
+    uint64_t *ho = reinterpret_cast<uint64_t *>(l->blk->p);
+    uint8_t *hb = l->blk->p + 8 * (m + 1);
+    MKV_HIP(hipMemcpyAsync(ho, d_off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st));
+    if (bytes) MKV_HIP(hipMemcpyAsync(hb, d_bytes, bytes, hipMemcpyDeviceToHost, t->st));
+    l->offsets = ho;
+    l->bytes = hb;
+}
+
 mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *digests_out) {
     MKV_TRY({
         NEED(t, "tree is null");
         DevGuard g(t->dev);
         if (keys) {
-            auto *l = new mkv_keylist();
             mkv_tree *tm = const_cast<mkv_tree *>(t);
             const uint64_t bytes = pack_sorted_keys(tm, tm->d_out, tm->d_outoff, 0, 0);
-            l->offsets.resize(t->n + 1, 0);
-            l->bytes.resize(bytes);
-            if (t->n) {
-                MKV_HIP(hipMemcpyAsync(l->offsets.data(), tm->d_outoff.p, (t->n + 1) * 8, hipMemcpyDeviceToHost,
-                                       t->st));
-                if (bytes) MKV_HIP(hipMemcpyAsync(l->bytes.data(), tm->d_out.p, bytes, hipMemcpyDeviceToHost, t->st));
+            auto *l = new mkv_keylist();
+            try {
+                keylist_fill(tm, l, tm->d_outoff.as<uint64_t>(), tm->d_out.as<uint8_t>(), t->n, bytes);
+                MKV_HIP(hipStreamSynchronize(t->st));
+            } catch (...) {
+                delete l;
+                throw;
             }
-            MKV_HIP(hipStreamSynchronize(t->st));
             *keys = l;
         }
         if (digests_out && t->n) {
@@ -1224,54 +1281,210 @@ static DiffSide side_of(const mkv_tree *t) {
     return s;
 }
 
+// Key list of the refs (bit 63 = side B) gathered on the device and copied to the host.
+static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A,
+                                      const DiffSide &B) {
+    auto *l = new mkv_keylist();
+    try {
+        if (m) {
+            size_t pk = prof_begin(t, "diff");
+            uint64_t *lens = ens<uint64_t>(t->s_lens, m + 1);
+            uint64_t *off = ens<uint64_t>(t->d_outoff, m + 1);
+            void *scr = t->d_diffscr.ensure(scan_scratch_bytes(m + 1));
+            launch_diff_keylens(refs, m, A, B, lens, t->st);
+            exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
+            prof_end(t, pk);
+            const uint64_t bytes = d2h_u64(t, off + m);
+            uint8_t *ob = ens<uint8_t>(t->d_out, bytes + 16);
+            launch_diff_keys(refs, m, A, B, off, ob, t->st);
+            keylist_fill(t, l, off, ob, m, bytes);
+        }
+        sync(t);
+    } catch (...) {
+        delete l;
+        throw;
+    }
+    return l;
+}
+
+static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
+    mkv_tree *t = const_cast<mkv_tree *>(a);
+    // b's last work must be complete before a's stream reads it
+    MKV_HIP(hipStreamSynchronize(b->st));
+    DiffSide A = side_of(a), B = side_of(b);
+    const uint64_t M = A.n + B.n;
+    uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
+    uint64_t m = 0;
+    bool done = false;
+    if (A.n > 0 && same_plan(a, b) && topdown_enabled()) {
+        // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
+        size_t pd = prof_begin(t, "diff");
+        done = topdown_diff(t, a, b, A, B, refs, &m);
+        prof_end(t, pd);
+    }
+    if (!done) {
+        size_t pd = prof_begin(t, "diff");
+        void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
+        uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
+        launch_diff(A, B, scr, refs, cnt, t->st);
+        prof_end(t, pd);
+        m = d2h_u64(t, cnt);
+    }
+    return keylist_from_refs(t, refs, m, A, B);
+}
+
+// One top-down walk of base `a` against every variant in vs (same level plan, key sets screened
+// equal): frontier entries carry the variant id, so each level is one launch for all of them.
+// res[i] = keylist, or nullptr when variant i's key set turned out to differ (caller diffs it pairwise).
+// Returns false (nothing decided) when the level-4 frontier says the walk is not worth finishing.
+static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<const mkv_tree *> &vs,
+                          std::vector<mkv_keylist *> &res) {
+    const uint32_t k = (uint32_t)vs.size();
+    const size_t L = a->lev_S.size();
+    const uint64_t n = a->n;
+    TdVariants V{};
+    for (uint32_t i = 0; i < k; ++i) V.nodes[i] = vs[i]->nodes.as<uint8_t>();
+    const uint64_t cap = (L > TD_CHECK_LEVEL + 2 ? k * n / 2 : k * n) + 2ull * k + 64;
+    uint64_t *f0 = ens<uint64_t>(t->tb_f0, cap), *f1 = ens<uint64_t>(t->tb_f1, cap);
+    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2 + 2 * k);  // per level; then nbad[k], count[k]
+    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2 + 2 * k) * 4, t->st));
+    const uint8_t *na = a->nodes.as<uint8_t>();
+    uint64_t *fin = f0, *fout = f1;
+    for (size_t l = L; l >= 1; --l) {
+        uint64_t r[2];
+        level_roots(a, l - 1, r);
+        const uint64_t a_par = l < L ? a->lev_base[l] : 0, max_par = l < L ? k * a->lev_cnt[l] : 0;
+        launch_topdown_level_batch(na + 32 * a->lev_off[l - 1], V, 32 * a->lev_off[l - 1], a->lev_cnt[l - 1], a_par,
+                                   a->lev_base[l - 1], r[0], r[1], k, fin, cnt + l, fout, cnt + (l - 1), max_par,
+                                   t->st);
+        std::swap(fin, fout);
+        if (l - 1 == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
+            const uint64_t c = d2h_u32(t, cnt + (l - 1));
+            if (2 * c > k * a->lev_cnt[l - 1]) return false;
+        }
+    }
+    const uint64_t m = d2h_u32(t, cnt);
+    uint32_t *nbad = cnt + L + 2, *vcount = nbad + k;
+    std::vector<uint32_t> hb(2 * k, 0);
+    uint64_t *refs = ens<uint64_t>(t->d_refs, m + 1);
+    const DiffSide A = side_of(a);
+    if (m) {
+        const int pb = std::max(1, bits_for(n));
+        const int vb = std::max(1, bits_for(k - 1));
+        uint64_t *k1 = ens<uint64_t>(t->td_k1, m + 1), *k2 = ens<uint64_t>(t->td_k2, m + 1);
+        uint32_t *v1 = ens<uint32_t>(t->td_v1, m + 1), *v2 = ens<uint32_t>(t->td_v2, m + 1);
+        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
+        launch_pack_entries(fin, m, pb, k1, v1, t->st);
+        const bool sw = radix_sort_pairs(k1, v1, k2, v2, m, 0, pb + vb, radix, t->st);
+        std::vector<DiffSide> hs(k);
+        for (uint32_t i = 0; i < k; ++i) hs[i] = side_of(vs[i]);
+        DiffSide *ds = reinterpret_cast<DiffSide *>(t->tb_sides.ensure(k * sizeof(DiffSide)));
+        MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
+        launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, refs, nbad, vcount, t->st);
+        MKV_HIP(hipMemcpyAsync(hb.data(), nbad, 2 * k * 4, hipMemcpyDeviceToHost, t->st));
+    }
+    mkv_keylist *all = keylist_from_refs(t, refs, m, A, A);  // syncs: hb is valid after this
+    // segment starts -> per-variant counts (variants appear in ascending order)
+    std::vector<uint64_t> cntv(k, 0);
+    if (m) {
+        uint64_t next = m;
+        for (int64_t i = (int64_t)k - 1; i >= 0; --i) {
+            if (hb[k + i] == 0xFFFFFFFFu) continue;
+            cntv[i] = next - hb[k + i];
+            next = hb[k + i];
+        }
+    }
+    uint64_t at = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+        const uint64_t c = cntv[i];
+        if (hb[i] == 0) {
+            auto *l = new mkv_keylist();  // a view into the shared block
+            if (c) {
+                l->blk = all->blk;
+                l->bytes = all->bytes;
+                l->offsets = all->offsets + at;
+                l->n = c;
+            }
+            res[i] = l;
+        }
+        at += c;
+    }
+    delete all;
+    return true;
+}
+
 mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out) {
     MKV_TRY({
         NEED(a && b && out, "null argument");
         NEED(a->dev == b->dev, "trees on different devices");
         NEED(!a->prepared && !b->prepared, "shard_reduce pending");
         *out = nullptr;
+        DevGuard g(a->dev);
+        *out = diff_pair(a, b);
+    });
+}
+
+mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, uint32_t k, mkv_keylist **outs) {
+    MKV_TRY({
+        NEED(a && (others || k == 0) && (outs || k == 0), "null argument");
+        for (uint32_t i = 0; i < k; ++i) {
+            NEED(others[i], "null tree");
+            NEED(others[i]->dev == a->dev, "trees on different devices");
+            NEED(!others[i]->prepared, "shard_reduce pending");
+            outs[i] = nullptr;
+        }
+        NEED(!a->prepared, "shard_reduce pending");
         mkv_tree *t = const_cast<mkv_tree *>(a);
         DevGuard g(t->dev);
-        // b's last work must be complete before a's stream reads it
-        MKV_HIP(hipStreamSynchronize(b->st));
-        DiffSide A = side_of(a), B = side_of(b);
-        const uint64_t M = A.n + B.n;
-        uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
-        uint64_t m = 0;
-        bool done = false;
-        if (A.n > 0 && same_plan(a, b) && topdown_enabled()) {
-            // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
-            size_t pd = prof_begin(t, "diff");
-            done = topdown_diff(t, a, b, A, B, refs, &m);
-            prof_end(t, pd);
+        std::vector<mkv_keylist *> res(k, nullptr);
+        try {
+            for (uint32_t i = 0; i < k; ++i) MKV_HIP(hipStreamSynchronize(others[i]->st));
+            // candidates for the shared walk: same level plan and a clean key-set screen
+            std::vector<uint32_t> cand;
+            if (a->n > 0 && topdown_enabled()) {
+                for (uint32_t i = 0; i < k; ++i)
+                    if (same_plan(a, others[i])) cand.push_back(i);
+            }
+            const bool roots_a = !a->combine_pending && a->has_root;
+            std::vector<uint32_t> walk;
+            if (!cand.empty()) {
+                uint32_t *scr = ens<uint32_t>(t->tb_screen, cand.size() + 1);
+                MKV_HIP(hipMemsetAsync(scr, 0, cand.size() * 4, t->st));
+                for (size_t c = 0; c < cand.size(); ++c)
+                    launch_sample_pfx(a->pfx.as<uint64_t>(), others[cand[c]]->pfx.as<uint64_t>(), a->n, 4096,
+                                      scr + c, t->st);
+                std::vector<uint32_t> hs(cand.size());
+                MKV_HIP(hipMemcpyAsync(hs.data(), scr, cand.size() * 4, hipMemcpyDeviceToHost, t->st));
+                sync(t);
+                for (size_t c = 0; c < cand.size(); ++c) {
+                    const mkv_tree *o = others[cand[c]];
+                    if (hs[c]) continue;
+                    if (roots_a && !o->combine_pending && o->has_root && std::memcmp(a->root, o->root, 32) == 0) {
+                        res[cand[c]] = new mkv_keylist();  // equal roots: identical leaves
+                    } else {
+                        walk.push_back(cand[c]);
+                    }
+                }
+            }
+            for (size_t s0 = 0; s0 < walk.size(); s0 += TD_MAX_VARIANTS) {
+                const size_t s1 = std::min(walk.size(), s0 + (size_t)TD_MAX_VARIANTS);
+                std::vector<const mkv_tree *> vs;
+                for (size_t i = s0; i < s1; ++i) vs.push_back(others[walk[i]]);
+                std::vector<mkv_keylist *> part(vs.size(), nullptr);
+                size_t pd = prof_begin(t, "diff");
+                const bool ok = topdown_batch(t, a, vs, part);
+                prof_end(t, pd);
+                if (ok)
+                    for (size_t i = s0; i < s1; ++i) res[walk[i]] = part[i - s0];
+            }
+            for (uint32_t i = 0; i < k; ++i)
+                if (!res[i]) res[i] = diff_pair(a, others[i]);
+        } catch (...) {
+            for (auto *l : res) delete l;
+            throw;
         }
-        if (!done) {
-            size_t pd = prof_begin(t, "diff");
-            void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
-            uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
-            launch_diff(A, B, scr, refs, cnt, t->st);
-            prof_end(t, pd);
-            m = d2h_u64(t, cnt);
-        }
-        t->d_diffscr.ensure(diff_scratch_bytes(M));
-        auto *l = new mkv_keylist();
-        l->offsets.assign(m + 1, 0);
-        if (m) {
-            size_t pk = prof_begin(t, "diff");
-            uint64_t *lens = ens<uint64_t>(t->s_lens, m + 1);
-            uint64_t *off = ens<uint64_t>(t->d_outoff, m + 1);
-            launch_diff_keylens(refs, m, A, B, lens, t->st);
-            exclusive_scan_u64(lens, off, m, off + m, t->d_diffscr.p, t->st);
-            prof_end(t, pk);
-            const uint64_t bytes = d2h_u64(t, off + m);
-            uint8_t *ob = ens<uint8_t>(t->d_out, bytes + 16);
-            launch_diff_keys(refs, m, A, B, off, ob, t->st);
-            l->bytes.resize(bytes);
-            MKV_HIP(hipMemcpyAsync(l->offsets.data(), off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st));
-            if (bytes) MKV_HIP(hipMemcpyAsync(l->bytes.data(), ob, bytes, hipMemcpyDeviceToHost, t->st));
-        }
-        sync(t);
-        *out = l;
+        for (uint32_t i = 0; i < k; ++i) outs[i] = res[i];
     });
 }
 
@@ -1318,9 +1531,9 @@ mkv_status mkv_tree_prefix_root(const mkv_tree *tc, const uint8_t *prefix, uint6
 mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets) {
     MKV_TRY({
         NEED(l && n, "null argument");
-        *n = l->offsets.empty() ? 0 : l->offsets.size() - 1;
-        if (bytes) *bytes = l->bytes.data();
-        if (offsets) *offsets = l->offsets.data();
+        *n = l->n;
+        if (bytes) *bytes = l->bytes;
+        if (offsets) *offsets = l->offsets;
     });
 }
 

@@ -68,9 +68,10 @@ def _keylist_packed(handle) -> tuple[np.ndarray, np.ndarray]:
     if cnt == 0:
         return np.zeros(0, np.uint8), np.zeros(1, np.uint64)
     offs = np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_uint64)), shape=(cnt + 1,)).copy()
-    nb = int(offs[-1])
-    raw = (np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(nb,)).copy() if nb
+    o0, o1 = int(offs[0]), int(offs[-1])  # offsets[0] may be nonzero (a view into a shared block)
+    raw = (np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(o1,))[o0:].copy() if o1 > o0
            else np.zeros(0, np.uint8))
+    offs -= np.uint64(o0)
     return raw, offs
 
 
@@ -330,6 +331,33 @@ class MerkleTree:
             return _keylist_packed(kl)
         finally:
             lib().mkv_keylist_free(kl)
+
+    def diff_keys_many_packed(self, others) -> list[tuple[np.ndarray, np.ndarray]]:
+        """[diff_keys_packed(o) for o in others] — one shared top-down walk for replicas with this
+        tree's key set (mkv_tree_diff_many)."""
+        self._flush()
+        for o in others:
+            o._flush()
+        k = len(others)
+        hs = (C.c_void_p * max(k, 1))(*[o._h.value for o in others])
+        outs = (C.c_void_p * max(k, 1))()
+        check(lib().mkv_tree_diff_many(self._h, hs, k, outs))
+        res = []
+        try:
+            for i in range(k):
+                res.append(_keylist_packed(C.c_void_p(outs[i])))
+        finally:
+            for i in range(k):
+                if outs[i]:
+                    lib().mkv_keylist_free(C.c_void_p(outs[i]))
+        return res
+
+    def diff_keys_many(self, others) -> list[list[str]]:
+        out = []
+        for raw, offs in self.diff_keys_many_packed(others):
+            b, o = raw.tobytes(), offs.tolist()
+            out.append([_s(b[o[i]:o[i + 1]]) for i in range(len(o) - 1)])
+        return out
 
     def diff_first_key(self, other: "MerkleTree") -> str | None:
         """diff_first_key(&other) — merkle.rs:199-204."""

@@ -216,3 +216,43 @@ def test_merge_batches_key_set_changes_vs_oracle():
         assert t.get_root_hash() == o.root(), rnd
         assert _levels(t) == _oracle_levels(o), rnd
         assert [k.encode("utf-8", "surrogateescape") for k, _ in t.leaves()] == [k for k, _ in items], rnd
+
+
+def test_diff_many_matches_pairwise_and_oracle():
+    """mkv_tree_diff_many (configs[4]'s 1-vs-7 replica diff): one shared top-down walk for same-key-set
+    replicas, pairwise fallback for the rest; every result equals its own diff_keys and the oracle."""
+    n = 20011
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    obase = coracle.OracleTree.build(kb, ko, vb, vo)
+    rng = np.random.default_rng(5)
+    variants, oracles = [], []
+    for v in range(7):
+        t = base.clone()
+        m = [0, 1, 50, 300, 2000, 5, 100][v]
+        idx = [int(i) for i in rng.integers(0, n, size=m)] + ([n - 1] if v == 4 else [])
+        ks = [keys[i] for i in idx]
+        vs = [b"v%d-%d" % (v, j) for j in range(len(idx))]
+        o = obase
+        if ks:
+            t.upsert(ks, vs)
+            o = obase.upsert(*pack(ks), *pack(vs))
+        if v == 5:  # key-set change: one removal + one insert keeps n but shifts positions
+            t.remove_many([keys[7]])
+            t.upsert([b"zzz-new"], [b"x"])
+            o = o.remove(*pack([keys[7]])).upsert(*pack([b"zzz-new"]), *pack([b"x"]))
+        variants.append(t)
+        oracles.append(o)
+    small = MerkleTree()  # different size: pairwise merge-join
+    small.build((kb[: 32 * 100], ko[:101]), (vb[: 100 * 100], vo[:101]))
+    variants.append(small)
+    oracles.append(coracle.OracleTree.build(kb[: 32 * 100], ko[:101], vb[: 100 * 100], vo[:101]))
+    got = base.diff_keys_many_packed(variants)
+    for i, (t, o) in enumerate(zip(variants, oracles)):
+        raw, offs = got[i]
+        b, oo = raw.tobytes(), offs.tolist()
+        lst = [b[oo[j]:oo[j + 1]] for j in range(len(oo) - 1)]
+        assert lst == base.diff_keys_bytes(t), i
+        assert lst == obase.diff(o), i
