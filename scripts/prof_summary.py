@@ -51,9 +51,10 @@ def main():
             e["issue_stall_frac"] = e["SQ_WAIT_INST_ANY"] / e["SQ_WAVE_CYCLES"]
         summary[k] = e
     json.dump(summary, open(os.path.join(OUT, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    lh = summary.get("k_leaf_hash")
+    lh = summary.get("k_leaf_persist") or summary.get("k_leaf_hash")
     if lh and "hbm_bytes_corrected" in lh:
         json.dump({"n": n, "hbm_bytes_per_launch": lh["hbm_bytes_corrected"], "source": f"{tag}_pmc.json",
+                   "kernel": "k_leaf_persist" if "k_leaf_persist" in summary else "k_leaf_hash",
                    "algorithmic_bytes_per_launch": 172 * n,
                    "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes"},
                   open(os.path.join(OUT, "pmc_leaf_hash.json"), "w"), indent=1)
