@@ -13,6 +13,7 @@
 // digit-major count matrix -> stable scatter, with in-wave ranks from 8 ballots (peer mask of lanes
 // with the same digit) and per-wave LDS digit counters.
 #include <cstdlib>
+#include <string>
 
 #include "common.hpp"
 #include "dev_util.hpp"
@@ -81,6 +82,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_hist(const uint64_t *__restri
 // digit; per-wave LDS counters make them tile ranks. The tile publishes its digit counts, looks back
 // over predecessors' words (agent-scope atomics: coherent across XCD L2s and CU L1s), sorts itself
 // in LDS by digit and writes each digit run contiguously (coalesced) to its global slot.
+// In-wave stable ranks: LDS_RANK = one ds_add_rtn_u32 per item on the wave's digit counter (gfx950 returns
+// the pre-add values of lanes hitting one address in lane order — verified at first use by
+// rank_selftest, tools/lds_atomic_order.hip); otherwise 8 ballots build each lane's peer mask.
+template <bool LDS_RANK>
 __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restrict__ kin,
                                                        const uint32_t *__restrict__ vin,
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
@@ -118,6 +123,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
         const uint64_t i = base + (uint64_t)s * 64;
         const bool ok = i < n;
         const uint32_t d = (uint32_t)(key[s] >> shift) & 255u;
+        if constexpr (LDS_RANK) {
+            rk[s] = ok ? atomicAdd(&wcnt[w][d], 1u) : 0u;
+            continue;
+        }
         uint64_t peers = __ballot(ok);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -489,6 +498,51 @@ inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_d
 
 }  // namespace
 
+__global__ __launch_bounds__(256) void k_rank_selftest(uint32_t trials, uint32_t *bad) {
+    __shared__ uint32_t cnt[4][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t t = blockIdx.x; t < trials; t += gridDim.x) {
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&cnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t x = (t * 2654435761u) ^ (threadIdx.x * 40503u + 12345u);
+        x ^= x >> 13;
+        x *= 0x5bd1e995u;
+        x ^= x >> 15;
+        const uint32_t mode = t & 3;  // uniform 8-bit, 4 distinct, all equal, 2 distinct
+        const uint32_t d = mode == 0 ? (x & 255u) : mode == 1 ? (x & 3u) * 37u : mode == 2 ? 7u : (x & 1u) * 200u;
+        uint64_t peers = ~0ull;
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t ref = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (atomicAdd(&cnt[w][d], 1u) != ref) atomicAdd(bad, 1u);
+        __syncthreads();
+    }
+}
+
+// Decided once per process on the first sort (one small kernel + readback).
+static bool lds_rank_ok(hipStream_t st) {
+    static int ok = -1;
+    if (ok >= 0) return ok == 1;
+    const char *e = getenv("MKV_SORT_RANK");  // "ballot" forces the ballot ranking
+    if (e && std::string(e) == "ballot") {
+        ok = 0;
+        return false;
+    }
+    uint32_t *bad = nullptr;
+    uint32_t hbad = 1;
+    if (hipMalloc(&bad, 4) == hipSuccess) {
+        (void)hipMemsetAsync(bad, 0, 4, st);
+        hipLaunchKernelGGL(k_rank_selftest, dim3(256), dim3(256), 0, st, 8192u, bad);
+        if (hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, st) == hipSuccess) (void)hipStreamSynchronize(st);
+        (void)hipFree(bad);
+    }
+    ok = hbad == 0 ? 1 : 0;
+    return ok == 1;
+}
+
 static void init_sort_prio() {
     static bool done = [] {
         const char *e = getenv("MKV_SORT_PRIO");
@@ -535,8 +589,12 @@ bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint
     uint32_t *vi = v, *vo = v2;
     bool swapped = false;
     for (int p = 0; p < npass; ++p) {
-        hipLaunchKernelGGL(k_os_pass, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
-                           counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
+        if (lds_rank_ok(st))
+            hipLaunchKernelGGL(k_os_pass<true>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
+                               counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
+        else
+            hipLaunchKernelGGL(k_os_pass<false>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
+                               counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
         MKV_LAUNCH_CHECK();
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -596,8 +654,12 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
     int q = 0;
     for (int p = 0; p < 8; ++p) {
         if (!((digit_mask >> p) & 1u)) continue;
-        hipLaunchKernelGGL(k_os_pass, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p, counts + 256 * p,
-                           lookback + (size_t)q * nb * 256, ctl + 4 * p);
+        if (lds_rank_ok(st))
+            hipLaunchKernelGGL(k_os_pass<true>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lookback + (size_t)q * nb * 256, ctl + 4 * p);
+        else
+            hipLaunchKernelGGL(k_os_pass<false>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lookback + (size_t)q * nb * 256, ctl + 4 * p);
         MKV_LAUNCH_CHECK();
         ++q;
         std::swap(ki, ko);
