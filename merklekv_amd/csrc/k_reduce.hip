@@ -16,6 +16,8 @@
 // Ownership (sharded trees): a launch computes only nodes whose leaf span lies inside the shard
 // [o, o+n); plan.a/plan.c give, per level, the owned global index range. With one shard this is the
 // whole tree.
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "sha256.hpp"
@@ -24,16 +26,17 @@ namespace mkv {
 
 namespace {
 
-constexpr int RD_THREADS = 512;
 constexpr int RD_TILE = 512;
 
-template <bool SHORT>
-__global__ __launch_bounds__(RD_THREADS) void k_reduce_fused(FusePlan p) {
+template <bool SHORT, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
     const uint64_t t = p.tile0 + blockIdx.x;
-    const uint32_t i = threadIdx.x;
     for (int k = 1; k <= p.nl; ++k) {
-        const uint64_t Tk = (uint64_t)RD_TILE >> (k - 1);
+      const uint64_t Tk = (uint64_t)RD_TILE >> (k - 1);
+      // THREADS < RD_TILE: a thread takes several parents of the first fused levels, so the upper fused
+      // levels keep a larger share of the workgroup's waves busy
+      for (uint32_t i = threadIdx.x; i < (Tk < (uint64_t)THREADS ? (uint32_t)THREADS : (uint32_t)Tk); i += THREADS) {
         const uint64_t j = t * Tk + i;
         const bool own = i < Tk && j >= p.a[k] && j < p.a[k] + p.c[k];
         if (own) {
@@ -82,7 +85,8 @@ __global__ __launch_bounds__(RD_THREADS) void k_reduce_fused(FusePlan p) {
             for (int q = 0; q < 8; ++q) dst[q] = o[q];
             store_digest(p.out[k - 1] + 32 * (j - p.a[k]), o);
         }
-        __syncthreads();
+      }
+      __syncthreads();
     }
 }
 
@@ -188,10 +192,18 @@ void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
     // chain there; many tiles = throughput-bound: fewer instructions win (profiles/r01_valu_microbench.md).
     const bool latency_bound = p.ntiles < 256;
     const int v = sha_variant();
-    if (v == 0 || (v == 1 && !latency_bound))
-        hipLaunchKernelGGL(k_reduce_fused<false>, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
-    else
-        hipLaunchKernelGGL(k_reduce_fused<true>, dim3((uint32_t)p.ntiles), dim3(RD_THREADS), 0, st, p);
+    static const int thr = [] {
+        const char *e = getenv("MKV_RD_THREADS");  // A/B knob: 512 (one parent per thread) or 256
+        return e && atoi(e) == 256 ? 256 : 512;
+    }();
+    if (v == 0 || (v == 1 && !latency_bound)) {
+        if (thr == 256)
+            hipLaunchKernelGGL((k_reduce_fused<false, 256>), dim3((uint32_t)p.ntiles), dim3(256), 0, st, p);
+        else
+            hipLaunchKernelGGL((k_reduce_fused<false, 512>), dim3((uint32_t)p.ntiles), dim3(512), 0, st, p);
+    } else {
+        hipLaunchKernelGGL((k_reduce_fused<true, 512>), dim3((uint32_t)p.ntiles), dim3(512), 0, st, p);
+    }
     MKV_LAUNCH_CHECK();
 }
 
