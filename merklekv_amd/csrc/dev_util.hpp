@@ -67,4 +67,28 @@ template <class T> __device__ __forceinline__ T block_excl_scan(T x, T *lds, T *
     return pre + inc - x;
 }
 
+// Block-aggregated append of v (when act) to out/count: one device-scope atomic per workgroup call.
+// Same-address atomics serialize across the XCDs, so per-wave appends of large frontiers / dirty lists
+// were bound by that one counter. Every thread of the block must call it (block-uniform control flow);
+// lds: >= 17 u32 of shared scratch. Order within the block follows wave then lane order.
+template <class T>
+__device__ __forceinline__ void block_append(bool act, T v, T *out, uint32_t *count, uint32_t *lds) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    const uint64_t m = __ballot(act);
+    if (lane == 0) lds[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (uint32_t i = 0; i < nw; ++i) {
+            const uint32_t c = lds[i];
+            lds[i] = tot;
+            tot += c;
+        }
+        lds[16] = tot ? atomicAdd(count, tot) : 0u;
+    }
+    __syncthreads();
+    if (act) out[lds[16] + lds[w] + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = v;
+    __syncthreads();  // lds is reused by the next call
+}
+
 }  // namespace mkv

@@ -279,6 +279,8 @@ __global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, 
     lohi[1] = l2;
 }
 
+constexpr int TD_THREADS = 1024;  // frontier kernels: one append atomic per 16 waves
+
 // ---- top-down diff (equal leaf counts): expand the divergent frontier one level down ----
 // frontier_in holds node indices of level l whose digests differ between the trees; children (l-1)
 // whose digests differ are appended to frontier_out (wave-aggregated: one atomic per wave).
@@ -287,13 +289,13 @@ __global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, 
 // compared and the divergent ones appended to fout. r0/r1: local child-level indices of owned nodes
 // whose parent is not owned (the tree's own root at the top level; a shard's fringe roots below it),
 // compared as extra frontier candidates (UINT64_MAX = none).
-__global__ __launch_bounds__(256) void k_topdown_level(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
+__global__ __launch_bounds__(TD_THREADS) void k_topdown_level(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
                                                       uint64_t child_count, uint64_t a_par, uint64_t a_child,
                                                       uint64_t r0, uint64_t r1, const uint32_t *__restrict__ fin,
                                                       const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
                                                       uint32_t *__restrict__ nout) {
+    __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
-    const uint32_t lane = threadIdx.x & 63;
     const uint64_t tot = 2ull * cnt + 2;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;  // two candidate children per frontier node, then r0, r1
@@ -303,11 +305,7 @@ __global__ __launch_bounds__(256) void k_topdown_level(const uint8_t *__restrict
         else if (t == 2ull * cnt) c = r0;
         else if (t == 2ull * cnt + 1) c = r1;
         if (c < child_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
-        const uint64_t m = __ballot(d);
-        uint32_t slot = 0;
-        if (lane == 0 && m) slot = atomicAdd(nout, (uint32_t)__popcll(m));
-        slot = __shfl(slot, 0);
-        if (d) fout[slot + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)c;
+        block_append<uint32_t>(d, (uint32_t)c, fout, nout, sapp);
     }
 }
 
@@ -324,16 +322,64 @@ __global__ __launch_bounds__(256) void k_sample_pfx(const uint64_t *__restrict__
     if (bad) atomicAdd(count, bad);
 }
 
+// ---- top-down walk in jumps of k levels (unsharded plans) ----
+// A divergent node p at level l has its level-(l-k) descendants at [p << k, (p+1) << k) (clipped to the
+// level: R5 promotion keeps the implicit arrays aligned). Comparing those 2^k nodes directly — they are
+// contiguous, so the loads coalesce — replaces k dependent level launches: the walk is latency-bound,
+// and a descendant can only differ when its ancestors do. One thread per (parent, descendant).
+__global__ __launch_bounds__(TD_THREADS) void k_topdown_jump(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
+                                                     uint64_t desc_count, int k, const uint32_t *__restrict__ fin,
+                                                     const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
+                                                     uint32_t *__restrict__ nout) {
+    __shared__ uint32_t sapp[17];
+    const uint32_t cnt = *nin;
+    const uint64_t tot = (uint64_t)cnt << k;
+    const uint64_t mask = (1ull << k) - 1ull;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        bool d = false;
+        uint64_t c = UINT64_MAX;
+        if (t < tot) c = ((uint64_t)fin[t >> k] << k) | (t & mask);
+        if (c < desc_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
+        block_append<uint32_t>(d, (uint32_t)c, fout, nout, sapp);
+    }
+}
+
+// Batched form: entries (variant << 32) | node.
+__global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_batch(const uint8_t *__restrict__ ca, TdVariants V,
+                                                           uint64_t desc_off, uint64_t desc_count, int k,
+                                                           const uint64_t *__restrict__ fin,
+                                                           const uint32_t *__restrict__ nin,
+                                                           uint64_t *__restrict__ fout, uint32_t *__restrict__ nout) {
+    __shared__ uint32_t sapp[17];
+    const uint32_t cnt = *nin;
+    const uint64_t tot = (uint64_t)cnt << k;
+    const uint64_t mask = (1ull << k) - 1ull;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        bool d = false;
+        uint64_t c = UINT64_MAX;
+        uint32_t v = 0;
+        if (t < tot) {
+            const uint64_t e = fin[t >> k];
+            v = (uint32_t)(e >> 32);
+            c = ((e & 0xFFFFFFFFull) << k) | (t & mask);
+        }
+        if (c < desc_count) d = !digest_eq(ca + 32ull * c, V.nodes[v] + desc_off + 32ull * c);
+        block_append<uint64_t>(d, ((uint64_t)v << 32) | c, fout, nout, sapp);
+    }
+}
+
 // ---- batched top-down walk: one base tree against k variants with the same level plan (configs[4]) ----
 // Frontier entries are (variant << 32) | local node index; every level is one launch for all variants.
-__global__ __launch_bounds__(256) void k_topdown_level_batch(const uint8_t *__restrict__ ca, TdVariants V,
+__global__ __launch_bounds__(TD_THREADS) void k_topdown_level_batch(const uint8_t *__restrict__ ca, TdVariants V,
                                                             uint64_t child_off, uint64_t child_count, uint64_t a_par,
                                                             uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
                                                             const uint64_t *__restrict__ fin,
                                                             const uint32_t *__restrict__ nin,
                                                             uint64_t *__restrict__ fout, uint32_t *__restrict__ nout) {
+    __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
-    const uint32_t lane = threadIdx.x & 63;
     const uint64_t tot = 2ull * cnt + 2ull * k;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
@@ -350,11 +396,7 @@ __global__ __launch_bounds__(256) void k_topdown_level_batch(const uint8_t *__re
             c = (q & 1) ? r1 : r0;
         }
         if (c < child_count) d = !digest_eq(ca + 32ull * c, V.nodes[v] + child_off + 32ull * c);
-        const uint64_t m = __ballot(d);
-        uint32_t slot = 0;
-        if (lane == 0 && m) slot = atomicAdd(nout, (uint32_t)__popcll(m));
-        slot = __shfl(slot, 0);
-        if (d) fout[slot + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)v << 32) | c;
+        block_append<uint64_t>(d, ((uint64_t)v << 32) | c, fout, nout, sapp);
     }
 }
 
@@ -438,8 +480,8 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
 void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_count, uint64_t a_par, uint64_t a_child,
                           uint64_t r0, uint64_t r1, const uint32_t *fin, const uint32_t *nin, uint32_t *fout,
                           uint32_t *nout, uint64_t max_frontier, hipStream_t st) {
-    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2, 256), 2048);
-    hipLaunchKernelGGL(k_topdown_level, dim3((uint32_t)blocks), dim3(256), 0, st, ca, cb, child_count, a_par, a_child,
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2, TD_THREADS), 2048);
+    hipLaunchKernelGGL(k_topdown_level, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, child_count, a_par, a_child,
                        r0, r1, fin, nin, fout, nout);
     MKV_LAUNCH_CHECK();
 }
@@ -455,8 +497,8 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
                                 uint64_t a_par, uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
                                 const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
                                 uint64_t max_frontier, hipStream_t st) {
-    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2 * k, 256), 4096);
-    hipLaunchKernelGGL(k_topdown_level_batch, dim3((uint32_t)blocks), dim3(256), 0, st, ca, V, child_off, child_count,
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(2 * max_frontier + 2 * k, TD_THREADS), 2048);
+    hipLaunchKernelGGL(k_topdown_level_batch, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, V, child_off, child_count,
                        a_par, a_child, r0, r1, k, fin, nin, fout, nout);
     MKV_LAUNCH_CHECK();
 }
@@ -479,6 +521,22 @@ __global__ void k_pack_entries(const uint64_t *__restrict__ ent, uint64_t m, int
 void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st) {
     if (!m) return;
     hipLaunchKernelGGL(k_pack_entries, grid1d(m), dim3(256), 0, st, ent, m, pb, key, val);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
+                         const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
+    hipLaunchKernelGGL(k_topdown_jump, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, desc_count, k, fin, nin, fout,
+                       nout);
+    MKV_LAUNCH_CHECK();
+}
+void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
+                               const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
+                               uint64_t max_desc, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
+    hipLaunchKernelGGL(k_topdown_jump_batch, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, V, desc_off, desc_count, k,
+                       fin, nin, fout, nout);
     MKV_LAUNCH_CHECK();
 }
 

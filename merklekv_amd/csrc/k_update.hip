@@ -18,7 +18,7 @@
 //                   level-l launch also clears the level-(l-1) bits of its entries' children, so the
 //                   bitmap is all-zero again after the last level and no clearing pass is needed.
 //
-// Dirty lists are unordered (wave-aggregated atomic append); the dirty bitmap (one bit per stored
+// Dirty lists are unordered (block-aggregated atomic append); the dirty bitmap (one bit per stored
 // node) is what deduplicates parents, so no per-level sort or scan is needed. Parents outside the
 // shard's owned range (sharded trees) stop the climb: their seam is recomputed by the
 // fringe all-gather + mkv_shard_combine exactly as after a full build.
@@ -78,16 +78,6 @@ __device__ __forceinline__ bool get_bit(const uint32_t *bm, uint64_t b) {
     return (__atomic_load_n(bm + (b >> 5), __ATOMIC_RELAXED) >> (b & 31)) & 1u;
 }
 
-// Wave-aggregated append of `v` (when `act`) to list/count.
-__device__ __forceinline__ void wave_append(bool act, uint32_t v, uint32_t *list, uint32_t *count) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t b = __ballot(act);
-    uint32_t base = 0;
-    if (lane == 0 && b) base = atomicAdd(count, (uint32_t)__popcll(b));
-    base = __shfl(base, 0);
-    if (act) list[base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull))] = v;
-}
-
 // Level 0: sorted (position, batch index) pairs; the last entry of each equal-position run is the last
 // write of that key. nodes0: local leaf level; bm bit index of leaf p = p (level 0 starts the bitmap).
 __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict__ pos,
@@ -95,6 +85,7 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
                                                       const uint8_t *__restrict__ bdig, uint8_t *__restrict__ nodes0,
                                                       uint32_t *__restrict__ bm, uint32_t *__restrict__ list,
                                                       uint32_t *__restrict__ count) {
+    __shared__ uint32_t sapp[17];
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = false;
     uint32_t p = 0;
@@ -110,13 +101,14 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
             set_bit(bm, p);
         }
     }
-    wave_append(act, p, list, count);
+    block_append<uint32_t>(act, p, list, count, sapp);
 }
 
 __global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, uint8_t *__restrict__ nodes,
                                                      uint32_t *__restrict__ bm, const uint32_t *__restrict__ lin,
                                                      const uint32_t *__restrict__ nin, uint32_t *__restrict__ lout,
                                                      uint32_t *__restrict__ nout) {
+    __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if ((uint64_t)blockIdx.x * blockDim.x >= cnt) return;  // whole workgroup idle (wave-uniform exit)
@@ -155,7 +147,7 @@ __global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, uint8_t *__re
             act = true;
         }
     }
-    wave_append(act, qloc, lout, nout);
+    block_append<uint32_t>(act, qloc, lout, nout, sapp);
 }
 
 // ---------------------------------------------------------------------------------------------

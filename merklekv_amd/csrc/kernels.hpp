@@ -140,6 +140,13 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
                                 uint64_t a_par, uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
                                 const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
                                 uint64_t max_frontier, hipStream_t st);
+// Jump k levels down from divergent parents (unsharded plans): fout gets every divergent descendant
+// at the target level (desc_count nodes there). max_desc: upper bound on parents << k (grid sizing).
+void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
+                         const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st);
+void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
+                               const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
+                               uint64_t max_desc, hipStream_t st);
 // ent: sorted (variant << pb) | position.
 void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs,
                                  uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st);

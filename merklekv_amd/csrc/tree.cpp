@@ -168,6 +168,15 @@ __global__ void k_widen_positions(const uint32_t *__restrict__ f, uint64_t m, ui
         v[i] = (uint32_t)i;
     }
 }
+__global__ void k_narrow_u64(const uint64_t *__restrict__ k, uint64_t m, uint32_t *__restrict__ f) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) f[i] = (uint32_t)k[i];
+}
+void launch_narrow_u64(const uint64_t *k, uint64_t m, uint32_t *f, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_narrow_u64, dim3((uint32_t)ceil_div(m, 256)), dim3(256), 0, st, k, m, f);
+    MKV_LAUNCH_CHECK();
+}
 void launch_widen_positions(const uint32_t *f, uint64_t m, uint64_t *k, uint32_t *v, hipStream_t st) {
     if (!m) return;
     hipLaunchKernelGGL(k_widen_positions, dim3((uint32_t)ceil_div(m, 256)), dim3(256), 0, st, f, m, k, v);
@@ -1217,6 +1226,13 @@ static bool topdown_enabled() {
     return on;
 }
 
+// Levels the jumping walk lands on: the top level, then every multiple of 4 below it down to 0.
+static std::vector<size_t> jump_targets(size_t L) {
+    std::vector<size_t> T{L - 1};
+    for (int64_t x = (int64_t)((L - 2) / 4) * 4; x >= 0; x -= 4) T.push_back((size_t)x);
+    return T;
+}
+
 // Top-down diff of two trees with identical level plans (equal leaf counts, and for shards the same
 // global offset and size): node (l, j) covers the same leaf positions in both. Equal digests prune
 // whole subtrees; only the divergent frontier is expanded, level by level, starting from the local
@@ -1237,6 +1253,25 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     if (d2h_u32(t, cnt + L + 1) != 0) return false;  // key sets differ: straight to the merge-join
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
+    if (!a->sharded && !b->sharded && L > 1) {
+        // Unsharded: seed with the root, then jump 4 levels per launch (landing on level 4 for the
+        // key-shift check and on level 0).
+        launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
+                             cnt + L, fout, cnt + (L - 1), 0, t->st);
+        std::swap(fin, fout);
+        const std::vector<size_t> T = jump_targets(L);
+        for (size_t q = 1; q < T.size(); ++q) {
+            const size_t l = T[q - 1], lt = T[q];
+            const int k = (int)(l - lt);
+            launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
+                                cnt + lt, std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
+            std::swap(fin, fout);
+            if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
+                const uint64_t c = d2h_u32(t, cnt + lt);
+                if (2 * c > a->lev_cnt[lt]) return false;
+            }
+        }
+    } else
     for (size_t l = L; l >= 1; --l) {  // parents at level l (none at l == L) -> children at level l-1
         uint64_t r[2];
         level_roots(a, l - 1, r);
@@ -1350,6 +1385,25 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2 + 2 * k) * 4, t->st));
     const uint8_t *na = a->nodes.as<uint8_t>();
     uint64_t *fin = f0, *fout = f1;
+    bool sharded = a->sharded;
+    for (auto *v : vs) sharded |= v->sharded;
+    if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
+        launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
+                                   fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
+        std::swap(fin, fout);
+        const std::vector<size_t> T = jump_targets(L);
+        for (size_t q = 1; q < T.size(); ++q) {
+            const size_t l = T[q - 1], lt = T[q];
+            const int kk = (int)(l - lt);
+            launch_topdown_jump_batch(na + 32 * a->lev_off[lt], V, 32 * a->lev_off[lt], a->lev_cnt[lt], kk, fin, cnt + l,
+                                      fout, cnt + lt, std::min<uint64_t>(k * (a->lev_cnt[l] << kk), 1ull << 40), t->st);
+            std::swap(fin, fout);
+            if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
+                const uint64_t c = d2h_u32(t, cnt + lt);
+                if (2 * c > k * a->lev_cnt[lt]) return false;
+            }
+        }
+    } else
     for (size_t l = L; l >= 1; --l) {
         uint64_t r[2];
         level_roots(a, l - 1, r);
