@@ -1226,6 +1226,14 @@ static bool topdown_enabled() {
     return on;
 }
 
+static bool jumps_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("MKV_TD_JUMP");  // A/B knob: 0 = one launch per level
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Levels the jumping walk lands on: the top level, then every multiple of 4 below it down to 0.
 static std::vector<size_t> jump_targets(size_t L) {
     std::vector<size_t> T{L - 1};
@@ -1253,7 +1261,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     if (d2h_u32(t, cnt + L + 1) != 0) return false;  // key sets differ: straight to the merge-join
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
-    if (!a->sharded && !b->sharded && L > 1) {
+    if (!a->sharded && !b->sharded && L > 1 && jumps_enabled()) {
         // Unsharded: seed with the root, then jump 4 levels per launch (landing on level 4 for the
         // key-shift check and on level 0).
         launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
@@ -1387,7 +1395,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     uint64_t *fin = f0, *fout = f1;
     bool sharded = a->sharded;
     for (auto *v : vs) sharded |= v->sharded;
-    if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
+    if (!sharded && L > 1 && jumps_enabled()) {  // seed with every variant's root, then jump 4 levels per launch
         launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
                                    fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
         std::swap(fin, fout);
