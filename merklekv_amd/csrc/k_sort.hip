@@ -161,8 +161,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
         int64_t j = (int64_t)bid - 1;
         uint32_t spins = 0;
         while (j >= 0) {
-            const uint32_t v = __hip_atomic_fetch_add(&lookback[(uint64_t)j * 256 + d], 0u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
+            // coherent (agent-scope) load, not a read-modify-write: no trip through the atomic unit
+            const uint32_t v = __hip_atomic_load(&lookback[(uint64_t)j * 256 + d], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t stt = v >> 30;
             if (stt == 0) {
                 if (++spins > LB_SPIN_LIMIT) {
