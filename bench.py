@@ -405,10 +405,19 @@ def wl_incremental(ctx, args):
                         int(torch.unique(sel).numel())))
     torch.cuda.synchronize()
 
+    # Each replica handle owns its own HIP streams, so the 7 dirty-path updates run concurrently from a
+    # host thread pool (the C ABI releases the GIL; handles are independent).
+    from concurrent.futures import ThreadPoolExecutor
+    pool = ThreadPoolExecutor(max_workers=len(variants))
+
+    def upd(args):
+        t, (ukb, uko, uvb, uvo, _) = args
+        t.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
+
     def step():
-        for t, (ukb, uko, uvb, uvo, _) in zip(variants, batches):
-            t.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
-            if ctx.world > 1:
+        list(pool.map(upd, zip(variants, batches)))
+        if ctx.world > 1:
+            for t in variants:
                 shard_recombine(t, ctx.dist, N, device=ctx.coll)
         return base.diff_keys_many_packed(variants)  # one shared top-down walk (mkv_tree_diff_many)
 
@@ -423,6 +432,7 @@ def wl_incremental(ctx, args):
         diffs = step()
     ctx.barrier()
     el = ctx.max_over_ranks(time.perf_counter() - t0)
+    pool.shutdown()
     upd_ms = sum(t.prof_read("update")[0] for t in variants) / (args.steps * (R - 1))
     diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))  # batched walk: per-pair share
     ok = all(len(d[1]) - 1 == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else

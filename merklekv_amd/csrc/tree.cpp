@@ -1001,7 +1001,7 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
             D.c_child = t->lev_cnt[l - 1];
             D.off_child = t->lev_off[l - 1];
         }
-        launch_dirty_level(D, m, nodes, bm, l0, cnt + l, l1, cnt + l + 1, st);
+        launch_dirty_level(D, std::min<uint64_t>(m, t->lev_cnt[l]), nodes, bm, l0, cnt + l, l1, cnt + l + 1, st);
         std::swap(l0, l1);
         if (!D.has_parent) break;  // every entry at this level cleared its own bit: bitmap is zero again
     }
