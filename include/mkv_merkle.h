@@ -93,6 +93,19 @@ mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out
  * plan and key set share one top-down walk (configs[4]: a base replica against 7 updated replicas);
  * the others are diffed pairwise. Results are identical to k separate calls. */
 mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, uint32_t k, mkv_keylist **outs);
+/* ---- anti-entropy exchange between peers (the top-down protocol of README.md:310-347) ----
+ * A peer serves digests of nodes by (level, index); the requester compares them with its own nodes and
+ * descends only into divergent ones, so only divergent branches cross the network. Both trees must hold
+ * the same key set (equal leaf counts) for the positions to line up; keys at the divergent leaf
+ * positions are then exchanged with mkv_tree_keys_at (merklekv_amd/antientropy.py drives the rounds). */
+/* out[k*32..] = digest of node (level, idx[k]); a node past the level's end reads as 32 zero bytes. */
+mkv_status mkv_tree_node_digests(const mkv_tree *t, uint32_t level, const uint64_t *idx, uint64_t m, uint8_t *out);
+/* out_idx[0..*n_out) = the idx[k] whose local digest differs from peer[k*32..] (order kept). */
+mkv_status mkv_tree_compare_nodes(const mkv_tree *t, uint32_t level, const uint64_t *idx, const uint8_t *peer,
+                                  uint64_t m, uint64_t *out_idx, uint64_t *n_out);
+/* Keys at sorted leaf positions pos[0..m) (inorder_keys()[pos[k]], merkle.rs:126-130). */
+mkv_status mkv_tree_keys_at(const mkv_tree *t, const uint64_t *pos, uint64_t m, mkv_keylist **out);
+
 /* HASH <prefix> — server.rs:647-685: root of a fresh tree over the keys starting with prefix
  * (*has_root = 0 when none: the server prints 64 zeros). plen = 0 gives the whole-tree root. */
 mkv_status mkv_tree_prefix_root(const mkv_tree *t, const uint8_t *prefix, uint64_t plen, uint8_t out32[32],

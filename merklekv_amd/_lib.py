@@ -21,7 +21,7 @@ EXPORTS = [
     "mkv_tree_create", "mkv_tree_destroy", "mkv_tree_clone", "mkv_tree_build", "mkv_tree_build_device",
     "mkv_tree_upsert", "mkv_tree_upsert_device", "mkv_tree_remove", "mkv_tree_apply", "mkv_tree_root", "mkv_tree_len",
     "mkv_tree_node_count", "mkv_tree_level_count", "mkv_tree_level", "mkv_tree_leaves", "mkv_tree_diff",
-    "mkv_tree_diff_many",
+    "mkv_tree_diff_many", "mkv_tree_node_digests", "mkv_tree_compare_nodes", "mkv_tree_keys_at",
     "mkv_tree_prefix_root", "mkv_keylist_get", "mkv_keylist_free", "mkv_last_error", "mkv_shard_prepare",
     "mkv_shard_reduce", "mkv_shard_fringe", "mkv_shard_combine", "mkv_prof_enable", "mkv_prof_reset",
     "mkv_prof_read", "mkv_gen_records_device", "mkv_leaf_digests", "mkv_version",
@@ -69,6 +69,9 @@ def lib():
         "mkv_tree_leaves": ([vp, P(vp), vp], i32),
         "mkv_tree_diff": ([vp, vp, P(vp)], i32),
         "mkv_tree_diff_many": ([vp, P(vp), u32, P(vp)], i32),
+        "mkv_tree_node_digests": ([vp, u32, vp, u64, vp], i32),
+        "mkv_tree_compare_nodes": ([vp, u32, vp, vp, u64, vp, P(u64)], i32),
+        "mkv_tree_keys_at": ([vp, vp, u64, P(vp)], i32),
         "mkv_tree_prefix_root": ([vp, vp, u64, vp, P(i32)], i32),
         "mkv_keylist_get": ([vp, P(u64), P(vp), P(vp)], i32),
         "mkv_keylist_free": ([vp], None),

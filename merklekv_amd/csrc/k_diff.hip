@@ -540,6 +540,42 @@ void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t 
     MKV_LAUNCH_CHECK();
 }
 
+// ---- anti-entropy exchange primitives: node digests by index, peer comparison ----
+__global__ void k_node_digests(const uint8_t *__restrict__ lvl, uint64_t count, const uint64_t *__restrict__ idx,
+                               uint64_t m, uint8_t *__restrict__ out) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t i = idx[k];
+    uint4 x = make_uint4(0, 0, 0, 0), y = x;  // absent node: zero digest (the peer treats it as divergent)
+    if (i < count) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(lvl + 32 * i);
+        x = src[0];
+        y = src[1];
+    }
+    uint4 *dst = reinterpret_cast<uint4 *>(out + 32 * k);
+    dst[0] = x;
+    dst[1] = y;
+}
+__global__ void k_compare_nodes(const uint8_t *__restrict__ lvl, uint64_t count, const uint64_t *__restrict__ idx,
+                                const uint8_t *__restrict__ peer, uint64_t m, uint8_t *__restrict__ flag) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    const uint64_t i = idx[k];
+    flag[k] = (i >= count || !digest_eq(lvl + 32 * i, peer + 32 * k)) ? 1 : 0;
+}
+void launch_node_digests(const uint8_t *lvl, uint64_t count, const uint64_t *idx, uint64_t m, uint8_t *out,
+                         hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_node_digests, grid1d(m), dim3(256), 0, st, lvl, count, idx, m, out);
+    MKV_LAUNCH_CHECK();
+}
+void launch_compare_nodes(const uint8_t *lvl, uint64_t count, const uint64_t *idx, const uint8_t *peer, uint64_t m,
+                          uint8_t *flag, hipStream_t st) {
+    if (!m) return;
+    hipLaunchKernelGGL(k_compare_nodes, grid1d(m), dim3(256), 0, st, lvl, count, idx, peer, m, flag);
+    MKV_LAUNCH_CHECK();
+}
+
 void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
                            uint32_t *nbad, hipStream_t st) {
     if (!m) return;

@@ -152,6 +152,12 @@ void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const 
                                  uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st);
 // key[k] = (variant << pb) | position of frontier entry (variant << 32) | position; val[k] = k.
 void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st);
+// Anti-entropy exchange: digests of level nodes by index (absent -> zeros); flags of indices whose local
+// digest differs from the peer's (absent -> divergent).
+void launch_node_digests(const uint8_t *lvl, uint64_t count, const uint64_t *idx, uint64_t m, uint8_t *out,
+                         hipStream_t st);
+void launch_compare_nodes(const uint8_t *lvl, uint64_t count, const uint64_t *idx, const uint8_t *peer, uint64_t m,
+                          uint8_t *flag, hipStream_t st);
 // Prefix range [lo, hi) of sorted keys starting with prefix (single-thread binary search).
 void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t plen, uint64_t *lohi, hipStream_t st);
 

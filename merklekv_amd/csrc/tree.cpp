@@ -118,6 +118,7 @@ struct mkv_tree {
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
+    DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
     DevBuf d_seam, d_S, d_fr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
@@ -1547,6 +1548,72 @@ mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, 
             throw;
         }
         for (uint32_t i = 0; i < k; ++i) outs[i] = res[i];
+    });
+}
+
+// ---- anti-entropy exchange (README.md:310-347 protocol) ----
+static const uint8_t *level_ptr(const mkv_tree *t, uint32_t level, uint64_t *count) {
+    *count = level < t->lev_cnt.size() ? t->lev_cnt[level] : 0;
+    return *count ? t->nodes.as<uint8_t>() + 32 * t->lev_off[level] : nullptr;
+}
+
+mkv_status mkv_tree_node_digests(const mkv_tree *tc, uint32_t level, const uint64_t *idx, uint64_t m, uint8_t *out) {
+    MKV_TRY({
+        NEED(tc && (m == 0 || (idx && out)), "null argument");
+        NEED(!tc->prepared && !tc->sharded, "node exchange needs an unsharded tree");
+        if (!m) return MKV_OK;
+        mkv_tree *t = const_cast<mkv_tree *>(tc);
+        DevGuard g(t->dev);
+        uint64_t cnt = 0;
+        const uint8_t *lvl = level_ptr(t, level, &cnt);
+        uint64_t *di = ens<uint64_t>(t->x_idx, m);
+        uint8_t *dd = ens<uint8_t>(t->x_dig, 32 * m);
+        MKV_HIP(hipMemcpyAsync(di, idx, m * 8, hipMemcpyHostToDevice, t->st));
+        launch_node_digests(lvl ? lvl : dd, cnt, di, m, dd, t->st);
+        MKV_HIP(hipMemcpyAsync(out, dd, 32 * m, hipMemcpyDeviceToHost, t->st));
+        MKV_HIP(hipStreamSynchronize(t->st));
+    });
+}
+
+mkv_status mkv_tree_compare_nodes(const mkv_tree *tc, uint32_t level, const uint64_t *idx, const uint8_t *peer,
+                                  uint64_t m, uint64_t *out_idx, uint64_t *n_out) {
+    MKV_TRY({
+        NEED(tc && n_out && (m == 0 || (idx && peer && out_idx)), "null argument");
+        NEED(!tc->prepared && !tc->sharded, "node exchange needs an unsharded tree");
+        *n_out = 0;
+        if (!m) return MKV_OK;
+        mkv_tree *t = const_cast<mkv_tree *>(tc);
+        DevGuard g(t->dev);
+        uint64_t cnt = 0;
+        const uint8_t *lvl = level_ptr(t, level, &cnt);
+        uint64_t *di = ens<uint64_t>(t->x_idx, m);
+        uint8_t *dp = ens<uint8_t>(t->x_dig, 32 * m);
+        uint8_t *df = ens<uint8_t>(t->x_flag, m);
+        MKV_HIP(hipMemcpyAsync(di, idx, m * 8, hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipMemcpyAsync(dp, peer, 32 * m, hipMemcpyHostToDevice, t->st));
+        launch_compare_nodes(lvl ? lvl : dp, cnt, di, dp, m, df, t->st);
+        std::vector<uint8_t> hf(m);
+        MKV_HIP(hipMemcpyAsync(hf.data(), df, m, hipMemcpyDeviceToHost, t->st));
+        MKV_HIP(hipStreamSynchronize(t->st));
+        uint64_t k = 0;
+        for (uint64_t i = 0; i < m; ++i)
+            if (hf[i]) out_idx[k++] = idx[i];
+        *n_out = k;
+    });
+}
+
+mkv_status mkv_tree_keys_at(const mkv_tree *tc, const uint64_t *pos, uint64_t m, mkv_keylist **out) {
+    MKV_TRY({
+        NEED(tc && out && (m == 0 || pos), "null argument");
+        NEED(!tc->prepared, "shard_reduce pending");
+        *out = nullptr;
+        mkv_tree *t = const_cast<mkv_tree *>(tc);
+        for (uint64_t i = 0; i < m; ++i) NEED(pos[i] < t->n, "leaf position out of range");
+        DevGuard g(t->dev);
+        uint64_t *refs = ens<uint64_t>(t->x_idx, m + 1);
+        if (m) MKV_HIP(hipMemcpyAsync(refs, pos, m * 8, hipMemcpyHostToDevice, t->st));
+        const DiffSide A = side_of(t);
+        *out = keylist_from_refs(t, refs, m, A, A);
     });
 }
 

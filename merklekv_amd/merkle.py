@@ -359,6 +359,37 @@ class MerkleTree:
             out.append([_s(b[o[i]:o[i + 1]]) for i in range(len(o) - 1)])
         return out
 
+    # ------------------------------------------------------------------ anti-entropy exchange
+    def node_digests(self, level: int, idx) -> bytes:
+        """Digests of nodes (level, idx[k]) — what a peer serves (README.md:310-347)."""
+        self._flush()
+        ia = np.ascontiguousarray(np.asarray(idx, dtype=np.uint64))
+        out = np.zeros(max(ia.size, 1) * 32, np.uint8)
+        check(lib().mkv_tree_node_digests(self._h, level, ia.ctypes.data, ia.size, out.ctypes.data))
+        return out[: 32 * ia.size].tobytes()
+
+    def compare_nodes(self, level: int, idx, peer: bytes) -> np.ndarray:
+        """The idx[k] whose local digest differs from the peer's digest peer[32k:32k+32]."""
+        self._flush()
+        ia = np.ascontiguousarray(np.asarray(idx, dtype=np.uint64))
+        pb = np.frombuffer(peer, dtype=np.uint8) if peer else np.zeros(1, np.uint8)
+        out = np.zeros(max(ia.size, 1), np.uint64)
+        n = C.c_uint64()
+        check(lib().mkv_tree_compare_nodes(self._h, level, ia.ctypes.data, pb.ctypes.data, ia.size, out.ctypes.data,
+                                           C.byref(n)))
+        return out[: n.value]
+
+    def keys_at(self, pos) -> list[bytes]:
+        """Keys at sorted leaf positions (inorder_keys()[p], merkle.rs:126-130)."""
+        self._flush()
+        pa = np.ascontiguousarray(np.asarray(pos, dtype=np.uint64))
+        kl = C.c_void_p()
+        check(lib().mkv_tree_keys_at(self._h, pa.ctypes.data if pa.size else None, pa.size, C.byref(kl)))
+        try:
+            return _keylist(kl)
+        finally:
+            lib().mkv_keylist_free(kl)
+
     def diff_first_key(self, other: "MerkleTree") -> str | None:
         """diff_first_key(&other) — merkle.rs:199-204."""
         d = self.diff_keys(other)

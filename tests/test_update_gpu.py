@@ -256,3 +256,31 @@ def test_diff_many_matches_pairwise_and_oracle():
         lst = [b[oo[j]:oo[j + 1]] for j in range(len(oo) - 1)]
         assert lst == base.diff_keys_bytes(t), i
         assert lst == obase.diff(o), i
+
+
+def test_antientropy_exchange_matches_diff_and_moves_little():
+    """Top-down exchange (README.md:310-347): same result as diff_keys; for a sparse value-only
+    divergence only a small fraction of the tree's digests cross the wire; key-set changes fall back."""
+    from merklekv_amd.antientropy import Peer, exchange_diff
+    n = 50_000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    a = MerkleTree()
+    a.build((kb, ko), (vb, vo))
+    b = a.clone()
+    idx = [3, 777, 4096, 20000, 49999]
+    b.upsert([keys[i] for i in idx], [b"changed"] * len(idx))
+    got, st = exchange_diff(a, Peer(b))
+    assert got == a.diff_keys_bytes(b) == sorted(keys[i] for i in idx)
+    assert not st.fallback and st.digests_sent < n // 20
+    same, st2 = exchange_diff(a, Peer(a.clone()))
+    assert same == [] and st2.digests_sent == 1
+    c = a.clone()
+    c.remove_many([keys[10]])
+    c.upsert([b"zz-extra"], [b"v"])
+    got3, st3 = exchange_diff(a, Peer(c))
+    assert got3 == a.diff_keys_bytes(c) and st3.fallback
+    d = MerkleTree()
+    d.build((kb[: 32 * 1000], ko[:1001]), (vb[: 100 * 1000], vo[:1001]))
+    got4, st4 = exchange_diff(a, Peer(d))
+    assert got4 == a.diff_keys_bytes(d) and st4.fallback
