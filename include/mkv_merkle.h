@@ -59,6 +59,14 @@ mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values);
  * with offsets[n] inside the allocation — they are trusted, not validated. */
 mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
 
+/* SyncManager::build_remote_merkle_snapshot (sync.rs:122-143) straight from the wire bytes: scan = the
+ * SCAN response ("KEYS <n>\r\n" + n key lines, server.rs:580-587), gets = the n GET responses in key order
+ * concatenated ("VALUE <v>\r\n" or "NOT_FOUND\r\n", server.rs:551-552). Parsed on the device with the
+ * client's read_line + trim_end semantics (sync.rs:150-214); NOT_FOUND keys are skipped; malformed
+ * responses -> MKV_EINVAL with the reference's error text. Replaces the tree's contents. */
+mkv_status mkv_tree_build_wire(mkv_tree *t, const uint8_t *scan, uint64_t scan_len, const uint8_t *gets,
+                               uint64_t gets_len);
+
 /* n x insert(k_i, v_i) on the existing contents — merkle.rs:52-56 (sequential semantics, one rebuild).
  * When every key is already a leaf (value-only anti-entropy batch, BASELINE configs[4]) only the changed
  * leaves and their ancestors are rehashed (dirty path); otherwise the batch is merged and the tree

@@ -188,6 +188,22 @@ size_t umerge_scratch_bytes(uint64_t M);
 void launch_umerge(const DiffSide &A, const DiffSide &B, const uint8_t *tomb, uint32_t nstore_a, void *scratch,
                    uint64_t *pfx_out, uint32_t *perm_out, uint8_t *dig_out, uint64_t *count, hipStream_t st);
 
+// ---- wire-format snapshot ingestion (k_wire.hip) ----
+size_t wire_scratch_bytes(uint64_t len);
+// Counts '\n' bytes (tile counts + exclusive scan in scratch; *d_total = line count); returns #tiles.
+uint64_t wire_count_lines(const uint8_t *buf, uint64_t len, void *scratch, uint64_t *d_total, hipStream_t st);
+// nl[j] = position of the j-th '\n' (needs the scratch of wire_count_lines).
+void wire_emit_lines(const uint8_t *buf, uint64_t len, const void *scratch, uint64_t *nl, hipStream_t st);
+// SCAN key i = line i+1 trimmed (str::trim_end); GET line i -> value / NOT_FOUND / malformed (*bad).
+void launch_scan_keys(const uint8_t *buf, const uint64_t *nl, uint64_t n, uint64_t *kstart, uint64_t *klen,
+                      hipStream_t st);
+void launch_get_values(const uint8_t *buf, const uint64_t *nl, uint64_t n, uint64_t *vstart, uint64_t *vlen,
+                       uint32_t *found, uint32_t *bad, hipStream_t st);
+void launch_found_lengths(const uint64_t *len, const uint32_t *found, const uint32_t *rank, uint64_t n, uint64_t *out,
+                          hipStream_t st);
+void launch_pack_records(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint32_t *found,
+                         const uint32_t *rank, const uint64_t *off_out, uint64_t n, uint8_t *dst, hipStream_t st);
+
 // ---- synthetic generator (k_gen.hip) — bench/test utility, not part of the reference API ----
 void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
                         uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb, uint64_t *voff,

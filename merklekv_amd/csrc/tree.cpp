@@ -119,6 +119,7 @@ struct mkv_tree {
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
     DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
+    DevBuf w_scan, w_gets, w_nl1, w_nl2, w_scr, w_ks, w_kl, w_vs, w_vl, w_found, w_rank;  // wire ingestion
     DevBuf d_seam, d_S, d_fr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
@@ -1028,6 +1029,92 @@ static void upload_update_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blo
     ens<uint64_t>(t->u_voff, m + 1);
     upload_blob(t, keys, t->u_kb, t->u_koff);
     upload_blob(t, values, t->u_vb, t->u_voff);
+}
+
+// ---- snapshot ingestion from the SYNC wire format ----
+// Rust str::split_whitespace / trim_end on the ASCII header line.
+static bool parse_keys_header(const uint8_t *p, uint64_t len, uint64_t *n) {
+    std::string h(reinterpret_cast<const char *>(p), len);
+    size_t i = 0;
+    auto ws = [](char c) { return c == ' ' || (c >= 0x09 && c <= 0x0D); };
+    auto tok = [&](std::string *out) {
+        while (i < h.size() && ws(h[i])) ++i;
+        size_t j = i;
+        while (j < h.size() && !ws(h[j])) ++j;
+        *out = h.substr(i, j - i);
+        i = j;
+        return !out->empty();
+    };
+    std::string a, b;
+    if (!tok(&a) || a != "KEYS" || !tok(&b)) return false;
+    if (b.empty() || b.size() > 19) return false;
+    for (char c : b)
+        if (c < '0' || c > '9') return false;
+    *n = std::stoull(b);
+    return true;
+}
+
+// Line-break positions of a host response uploaded to `dst`: returns the line count.
+static uint64_t wire_lines(mkv_tree *t, const uint8_t *host, uint64_t len, DevBuf &dst, DevBuf &nlbuf) {
+    uint8_t *d = ens<uint8_t>(dst, len + 16);
+    if (len) MKV_HIP(hipMemcpyAsync(d, host, len, hipMemcpyHostToDevice, t->st));
+    void *scr = t->w_scr.ensure(wire_scratch_bytes(len));
+    uint64_t *tot = ens<uint64_t>(t->m_cnt, 4);
+    wire_count_lines(d, len, scr, tot, t->st);
+    const uint64_t lines = d2h_u64(t, tot);
+    uint64_t *nl = ens<uint64_t>(nlbuf, lines + 1);
+    if (lines) wire_emit_lines(d, len, scr, nl, t->st);
+    return lines;
+}
+
+mkv_status mkv_tree_build_wire(mkv_tree *t, const uint8_t *scan, uint64_t scan_len, const uint8_t *gets,
+                               uint64_t gets_len) {
+    MKV_TRY({
+        NEED(t && (scan || !scan_len) && (gets || !gets_len), "null argument");
+        DevGuard g(t->dev);
+        const uint8_t *eol = scan_len ? static_cast<const uint8_t *>(std::memchr(scan, '\n', scan_len)) : nullptr;
+        NEED(eol, "peer closed while reading SCAN header");
+        uint64_t n = 0;
+        if (!parse_keys_header(scan, (uint64_t)(eol - scan), &n))
+            throw Error(ST_EINVAL, "unexpected SCAN response (want \"KEYS <n>\")");
+        const uint64_t ls = wire_lines(t, scan, scan_len, t->w_scan, t->w_nl1);
+        NEED(ls >= n + 1, "peer closed while reading key list");
+        const uint64_t lg = wire_lines(t, gets, gets_len, t->w_gets, t->w_nl2);
+        NEED(lg >= n, "peer closed on GET (fewer GET responses than keys)");
+        NEED(n < 0xFFFFFFF0ull, "too many records");
+        uint64_t *ks = ens<uint64_t>(t->w_ks, n + 1), *kl = ens<uint64_t>(t->w_kl, n + 1);
+        uint64_t *vs = ens<uint64_t>(t->w_vs, n + 1), *vl = ens<uint64_t>(t->w_vl, n + 1);
+        uint32_t *found = ens<uint32_t>(t->w_found, n + 1), *rank = ens<uint32_t>(t->w_rank, n + 1);
+        uint32_t *misc = ens<uint32_t>(t->s_misc, 64);
+        MKV_HIP(hipMemsetAsync(misc, 0, 8, t->st));
+        const uint8_t *dscan = t->w_scan.as<uint8_t>(), *dgets = t->w_gets.as<uint8_t>();
+        launch_scan_keys(dscan, t->w_nl1.as<uint64_t>(), n, ks, kl, t->st);
+        launch_get_values(dgets, t->w_nl2.as<uint64_t>(), n, vs, vl, found, misc, t->st);
+        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n + 1), scan_scratch_bytes(n + 2)));
+        exclusive_scan_u32(found, rank, n, misc + 1, radix, t->st);
+        MKV_HIP(hipMemcpyAsync(t->h_small, misc, 8, hipMemcpyDeviceToHost, t->st));
+        wait_stream(t, t->st);
+        const uint32_t bad = reinterpret_cast<uint32_t *>(t->h_small)[0];
+        const uint64_t m = reinterpret_cast<uint32_t *>(t->h_small)[1];
+        NEED(bad == 0, "unexpected GET response (want \"VALUE <v>\" or \"NOT_FOUND\")");
+        // packed keys / values of the found records (keys whose GET said NOT_FOUND are skipped, sync.rs:130-140)
+        uint64_t *koff = ens<uint64_t>(t->s_koff, m + 1), *voff = ens<uint64_t>(t->s_voff, m + 1);
+        uint64_t *lens = ens<uint64_t>(t->s_lens, m + 1);
+        launch_found_lengths(kl, found, rank, n, lens, t->st);
+        exclusive_scan_u64(lens, koff, m, koff + m, radix, t->st);
+        const uint64_t kbytes = m ? d2h_u64(t, koff + m) : 0;
+        if (!m) MKV_HIP(hipMemsetAsync(koff, 0, 8, t->st));
+        uint8_t *kb = ens<uint8_t>(t->s_kb, kbytes + 16);
+        launch_pack_records(dscan, ks, kl, found, rank, koff, n, kb, t->st);
+        launch_found_lengths(vl, found, rank, n, lens, t->st);
+        exclusive_scan_u64(lens, voff, m, voff + m, radix, t->st);
+        const uint64_t vbytes = m ? d2h_u64(t, voff + m) : 0;
+        if (!m) MKV_HIP(hipMemsetAsync(voff, 0, 8, t->st));
+        uint8_t *vb = ens<uint8_t>(t->s_vb, vbytes + 16);
+        launch_pack_records(dgets, vs, vl, found, rank, voff, n, vb, t->st);
+        MKV_HIP(hipStreamSynchronize(t->st));
+        build_from_staged(t, kb, koff, vb, voff, m, true, kbytes);
+    });
 }
 
 mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values) {

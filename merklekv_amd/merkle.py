@@ -154,6 +154,16 @@ class MerkleTree:
             raise ValueError("keys and values differ in length")
         check(lib().mkv_tree_build(self._h, pk.blob(), pv.blob()))
 
+    def build_wire(self, scan_response: bytes, get_responses: bytes) -> None:
+        """build_remote_merkle_snapshot (sync.rs:122-143) from the raw SCAN response and the concatenated
+        GET responses; parsed on the device (mkv_tree_build_wire)."""
+        self._pending.clear()
+        self._cache.clear()
+        sb = np.frombuffer(scan_response, np.uint8) if scan_response else np.zeros(1, np.uint8)
+        gb = np.frombuffer(get_responses, np.uint8) if get_responses else np.zeros(1, np.uint8)
+        check(lib().mkv_tree_build_wire(self._h, sb.ctypes.data, len(scan_response), gb.ctypes.data,
+                                        len(get_responses)))
+
     def upsert(self, keys, values) -> None:
         """Batch of insert() calls on the current contents (one device rebuild)."""
         self._flush()
