@@ -484,11 +484,15 @@ def cpu_baseline_diff(n: int = 2_000_000):
     vb2[::100 * 1000] ^= 1  # 0.1 % value-only divergence (every 1000th record's value byte 0)
     a = co.OracleTree.build(kb, ko, vb, vo)
     b = co.OracleTree.build(kb, ko, vb2, vo)
-    t0 = time.perf_counter()
-    d = a.diff(b)
-    secs = time.perf_counter() - t0
-    return {"value": n / secs, "unit": "keys/s", "cores": 1, "kind": "port",
-            "sample": f"diff of two {n}-key trees, 0.1% value-only ({len(d)} keys), {secs:.2f} s",
+    reps, t0 = 0, time.perf_counter()
+    while True:  # repeat the (fast) diff for a stable figure
+        d = a.diff(b)
+        reps += 1
+        secs = time.perf_counter() - t0
+        if secs >= 3.0:
+            break
+    return {"value": n * reps / secs, "unit": "keys/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} diffs of two {n}-key trees, 0.1% value-only ({len(d)} keys), {secs:.1f} s",
             "cpu_model": _cpu_model()}
 
 
