@@ -44,13 +44,15 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
             const uint64_t c0 = 2 * j;
             const bool pair = c0 + 1 < p.S[k - 1];
             if (k == 1 && p.perm) {
-                // a[0] == 0 here: every leaf is a child of exactly one owned parent
-                uint4 *dst0 = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(p.in) + 32 * c0);
-                const uint4 *s0 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[c0]);
+                // children of owned parents are owned leaves (local index c0 - a[0]); the <= 2 shard-edge
+                // leaves without an owned parent are gathered by the host-side plan (run_reduce)
+                const uint64_t lc = c0 - p.a[0];
+                uint4 *dst0 = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(p.in) + 32 * lc);
+                const uint4 *s0 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[lc]);
                 const uint4 x0 = s0[0], y0 = s0[1];
                 uint4 x1 = make_uint4(0, 0, 0, 0), y1 = x1;
                 if (pair) {
-                    const uint4 *s1 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[c0 + 1]);
+                    const uint4 *s1 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[lc + 1]);
                     x1 = s1[0];
                     y1 = s1[1];
                     dst0[2] = x1;
@@ -100,6 +102,7 @@ struct SeamEntry {
 static_assert(sizeof(SeamEntry) == 48, "seam entry layout");
 
 constexpr int SEAM_MAX = 64;
+constexpr uint32_t SEAM_STAGE = 1024;  // fringe entries staged in LDS (8 ranks x <= 130 fit)
 
 // One wave. Loose nodes of level l (fringes handed over by the shards + seam nodes computed from
 // level l-1) are kept sorted by index in LDS; each lane hashes at most one parent per level.
@@ -111,7 +114,25 @@ __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict
     __shared__ uint64_t nidx[SEAM_MAX];
     __shared__ uint32_t nh[SEAM_MAX][8];
     __shared__ uint32_t ncnt, ccnt, epos;
+    // the fringe entries and level sizes, staged once: the single-lane merge below then reads LDS
+    // instead of issuing dependent global loads (which dominated the combine's latency)
+    __shared__ uint32_t elev[SEAM_STAGE];
+    __shared__ uint64_t eidx[SEAM_STAGE];
+    __shared__ uint32_t eh[SEAM_STAGE][8];
+    __shared__ uint64_t sS[64];
     const uint32_t lane = threadIdx.x;
+    const bool staged = nent <= SEAM_STAGE;
+    if (staged) {
+        for (uint32_t e = lane; e < nent; e += 64) {
+            elev[e] = ent[e].level;
+            eidx[e] = ent[e].idx;
+            const uint8_t *h = ent[e].h;
+            for (int q = 0; q < 8; ++q)
+                eh[e][q] = ((uint32_t)h[4 * q] << 24) | ((uint32_t)h[4 * q + 1] << 16) | ((uint32_t)h[4 * q + 2] << 8) |
+                           (uint32_t)h[4 * q + 3];
+        }
+    }
+    for (uint32_t i = lane; i < L && i < 64; i += 64) sS[i] = S[i];
     if (lane == 0) {
         ccnt = 0;
         epos = 0;
@@ -131,7 +152,7 @@ __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict
                 x = cidx[lane];
                 if ((x & 1) == 0) {
                     act = true;
-                    pair = x + 1 < S[l - 1];
+                    pair = x + 1 < sS[l - 1];
                     for (int q = 0; q < 8; ++q) lw[q] = ch[lane][q];
                     if (pair) {
                         // sibling must be the next loose node
@@ -151,17 +172,53 @@ __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict
             if (lane == 0) ncnt = (uint32_t)__popcll(m);
         }
         __syncthreads();
-        // merge computed (nidx) with this level's fringe entries into cur (single lane, tiny lists)
-        if (lane == 0) {
+        // merge computed (nidx) with this level's fringe entries into cur. Staged: every lane places one
+        // element by its rank in the other sorted list (computed and fringe indices never coincide:
+        // computed nodes are seams, fringe nodes are owned); otherwise a single-lane merge from HBM.
+        if (staged) {
+            const uint32_t e0 = epos;
+            uint32_t e1 = e0;
+            while (e1 < nent && elev[e1] == l) ++e1;  // same bound in every lane (LDS reads)
+            const uint32_t na = ncnt, nb = e1 - e0;
+            if (lane < na + nb) {
+                uint64_t x;
+                const uint32_t *src;
+                uint32_t r = 0;
+                if (lane < na) {
+                    x = nidx[lane];
+                    src = nh[lane];
+                    for (uint32_t j = 0; j < nb; ++j) r += eidx[e0 + j] < x;
+                    r += lane;
+                } else {
+                    const uint32_t j = lane - na;
+                    x = eidx[e0 + j];
+                    src = eh[e0 + j];
+                    for (uint32_t i = 0; i < na; ++i) r += nidx[i] < x;
+                    r += j;
+                }
+                uint32_t w[8];
+                for (int q = 0; q < 8; ++q) w[q] = src[q];
+                if (r < SEAM_MAX) {
+                    cidx[r] = x;
+                    for (int q = 0; q < 8; ++q) ch[r][q] = w[q];
+                }
+            }
+            __syncthreads();
+            if (lane == 0) {
+                ccnt = na + nb < SEAM_MAX ? na + nb : SEAM_MAX;
+                epos = e1;
+            }
+        } else if (lane == 0) {
             uint32_t a = 0, na = ncnt, e = epos, c = 0;
             while (true) {
                 const bool hasE = e < nent && ent[e].level == l;
                 const bool hasA = a < na;
                 if (!hasE && !hasA) break;
-                bool takeE = hasE && (!hasA || ent[e].idx < nidx[a]);
+                const uint64_t ei = hasE ? ent[e].idx : 0;
+                bool takeE = hasE && (!hasA || ei < nidx[a]);
                 if (c < SEAM_MAX) {
                     if (takeE) {
-                        cidx[c] = ent[e].idx;
+                        cidx[c] = ei;
                         const uint8_t *h = ent[e].h;
                         for (int q = 0; q < 8; ++q)
                             ch[c][q] = ((uint32_t)h[4 * q] << 24) | ((uint32_t)h[4 * q + 1] << 16) |

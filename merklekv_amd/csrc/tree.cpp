@@ -129,6 +129,8 @@ struct mkv_tree {
     bool bm_dirty = false;
     uint64_t *h_small = nullptr;  // pinned host scalars
     uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
+    uint8_t *h_seam = nullptr;     // pinned staging of seam-combine inputs
+    size_t h_seam_cap = 0;
 
     // ---- profiling ----
     bool prof = false;
@@ -305,14 +307,21 @@ uint64_t total_nodes(const mkv_tree *t) {
     return s;
 }
 
-// gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch; only for an
-// unsharded plan (every leaf has an owned parent). A single-leaf tree has no launch: plain gather.
+// gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch. Leaves whose
+// parent is not owned (at most the first and the last of a shard) are gathered directly; a plan without
+// an owned level-1 node (single leaf, or a one-leaf shard) gathers everything directly.
 void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, const uint8_t *gdig = nullptr) {
     const size_t L = t->lev_S.size();
     if (gperm) {
-        if (L < 2 || t->lev_base[0] != 0 || t->lev_cnt[0] != t->lev_S[0] || t->lev_cnt[1] == 0) {
+        if (L < 2 || t->lev_cnt[1] == 0) {
             launch_gather_digests(gperm, gdig, L ? t->lev_cnt[0] : 0, nodes, t->st);
             gperm = nullptr;
+        } else {
+            const uint64_t a0 = t->lev_base[0], c0 = t->lev_cnt[0], a1 = t->lev_base[1], c1 = t->lev_cnt[1];
+            auto owned_parent = [&](uint64_t x) { return x / 2 >= a1 && x / 2 < a1 + c1; };
+            if (!owned_parent(a0)) launch_gather_digests(gperm, gdig, 1, nodes, t->st);
+            if (c0 > 1 && !owned_parent(a0 + c0 - 1))
+                launch_gather_digests(gperm + (c0 - 1), gdig, 1, nodes + 32 * (c0 - 1), t->st);
         }
     }
     size_t l = 0;
@@ -742,6 +751,7 @@ void mkv_tree_destroy(mkv_tree *t) {
     }
     if (t->h_small) (void)hipHostFree(t->h_small);
     if (t->h_counts) (void)hipHostFree(t->h_counts);
+    if (t->h_seam) (void)hipHostFree(t->h_seam);
     if (t->st) (void)hipStreamDestroy(t->st);
     delete t;
     (void)hipGetLastError();
@@ -1260,6 +1270,7 @@ static void keylist_fill(mkv_tree *t, mkv_keylist *l, const uint64_t *d_off, con
 mkv_status mkv_tree_leaves(const mkv_tree *t, mkv_keylist **keys, uint8_t *digests_out) {
     MKV_TRY({
         NEED(t, "tree is null");
+        NEED(!t->prepared, "shard_reduce pending");
         DevGuard g(t->dev);
         if (keys) {
             mkv_tree *tm = const_cast<mkv_tree *>(t);
@@ -1793,7 +1804,7 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         size_t pl = prof_begin(t, "leaf_hash");
         launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
         prof_end(t, pl);
-        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes, false);
+        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes, true);  // gather fused into reduce
         prof_end(t, ptot);
         sync(t);
         t->prepared = true;
@@ -1826,7 +1837,11 @@ mkv_status mkv_shard_reduce(mkv_tree *t, uint64_t global_offset, uint64_t global
         }
         size_t ptot = prof_begin(t, "total_build");
         size_t pr = prof_begin(t, "reduce");
-        run_reduce(t, t->nodes.as<uint8_t>());
+        if (t->gather_pending)
+            run_reduce(t, t->nodes.as<uint8_t>(), t->perm.as<uint32_t>(), t->s_dig.as<uint8_t>());
+        else
+            run_reduce(t, t->nodes.as<uint8_t>());
+        t->gather_pending = false;
         prof_end(t, pr);
         prof_end(t, ptot);
         sync(t);
@@ -1912,16 +1927,26 @@ mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes, uint32_t world
             S.push_back(s);
             if (s == 1) break;
         }
-        uint8_t *dent = ens<uint8_t>(t->d_seam, all.size() * sizeof(FringeEntry) + 64);
-        uint64_t *dS = ens<uint64_t>(t->d_S, S.size() + 1);
+        // one pinned staging block: [S (64 x u64) | entries]; the root comes back through h_small
+        const size_t sbytes = 64 * 8, ebytes = all.size() * sizeof(FringeEntry);
+        if (!t->h_seam || t->h_seam_cap < sbytes + ebytes) {
+            if (t->h_seam) MKV_HIP(hipHostFree(t->h_seam));
+            t->h_seam = nullptr;
+            t->h_seam_cap = sbytes + ebytes + 4096;
+            MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&t->h_seam), t->h_seam_cap, hipHostMallocDefault));
+        }
+        NEED(S.size() <= 64, "too many levels");
+        std::memcpy(t->h_seam, S.data(), S.size() * 8);
+        if (ebytes) std::memcpy(t->h_seam + sbytes, all.data(), ebytes);
+        uint8_t *dst = ens<uint8_t>(t->d_seam, sbytes + ebytes + 64);
         uint8_t *droot = ens<uint8_t>(t->d_fr, 64);
-        if (!all.empty())
-            MKV_HIP(hipMemcpyAsync(dent, all.data(), all.size() * sizeof(FringeEntry), hipMemcpyHostToDevice, t->st));
-        MKV_HIP(hipMemcpyAsync(dS, S.data(), S.size() * 8, hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipMemcpyAsync(dst, t->h_seam, sbytes + ebytes, hipMemcpyHostToDevice, t->st));
         MKV_HIP(hipMemsetAsync(droot, 0, 32, t->st));
-        launch_seam_combine(dent, (uint32_t)all.size(), dS, (uint32_t)S.size(), nullptr, droot, t->st);
-        MKV_HIP(hipMemcpyAsync(out32, droot, 32, hipMemcpyDeviceToHost, t->st));
-        MKV_HIP(hipStreamSynchronize(t->st));
+        launch_seam_combine(dst + sbytes, (uint32_t)all.size(), reinterpret_cast<const uint64_t *>(dst),
+                            (uint32_t)S.size(), nullptr, droot, t->st);
+        MKV_HIP(hipMemcpyAsync(t->h_small, droot, 32, hipMemcpyDeviceToHost, t->st));
+        wait_stream(t, t->st);
+        std::memcpy(out32, t->h_small, 32);
         *has_root = 1;
         std::memcpy(t->root, out32, 32);
         t->has_root = true;

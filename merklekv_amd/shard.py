@@ -15,12 +15,18 @@ import numpy as np
 
 
 def _all_gather_bytes(dist, payload: bytes, device, group=None) -> list[bytes]:
+    """All-gather of equal-size byte payloads: one collective into one buffer, one copy back."""
     import torch
     world = dist.get_world_size(group)
     t = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t, group=group)
-    return [bytes(x.cpu().numpy().tobytes()) for x in out]
+    out = torch.empty(world * t.numel(), dtype=torch.uint8, device=device)
+    if hasattr(dist, "all_gather_into_tensor") and (device is None or torch.device(device).type != "cpu"):
+        dist.all_gather_into_tensor(out, t, group=group)
+    else:  # gloo has no all_gather_into_tensor on some versions
+        dist.all_gather(list(out.chunk(world)), t, group=group)
+    raw = out.cpu().numpy().tobytes()
+    k = t.numel()
+    return [raw[r * k:(r + 1) * k] for r in range(world)]
 
 
 def shard_counts(dist, n_local: int, device, group=None) -> list[int]:
