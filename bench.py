@@ -208,14 +208,14 @@ def wl_build(ctx, args):
         treeB = MerkleTree(ctx.local)
         treeB.build_device(kb.data_ptr(), ko.data_ptr(), vb2.data_ptr(), vo.data_ptr(), n)
         tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
-        d = tree.diff_keys_packed(treeB)  # warm
+        d = tree.diff_keys_view(treeB)  # warm
         reps = 5
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            d = tree.diff_keys_packed(treeB)
+            d = tree.diff_keys_view(treeB)
         dt = (time.perf_counter() - t0) / reps
-        diff_info = {"union_keys": n, "divergent": len(d[1]) - 1, "expected_divergent": int(idx.numel()),
+        diff_info = {"union_keys": n, "divergent": len(d), "expected_divergent": int(idx.numel()),
                      "ms": dt * 1e3, "keys_per_s": n / dt,
                      "mode": "top-down (equal key sets), value-only 0.1%, incl. key-list D2H"}
         # incremental: 0.1 % value-update batch of existing keys (dirty path), configs[4]'s ratio
@@ -336,21 +336,21 @@ def wl_diff(ctx, args):
         ctx.build(B, kBf, koB, vBf, voB, nB)
         torch.cuda.synchronize()
         for _ in range(args.warmup):
-            d = A.diff_keys_packed(B)
+            d = A.diff_keys_view(B)
         A.prof_enable(True)
         A.prof_reset()
         ctx.barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            d = A.diff_keys_packed(B)
+            d = A.diff_keys_view(B)
         ctx.barrier()
         el = ctx.max_over_ranks(time.perf_counter() - t0)
         A.prof_enable(False)
         dms, dcnt = A.prof_read("diff")
-        got = d[0].reshape(-1, KLEN)
+        got = d.raw.reshape(-1, KLEN)
         exact = got.shape == exp_sorted.shape and bool((got == exp_sorted).all())
         union = ctx.sum_over_ranks(n + new)
-        res[mode] = {"union_keys": union, "divergent": ctx.sum_over_ranks(len(d[1]) - 1),
+        res[mode] = {"union_keys": union, "divergent": ctx.sum_over_ranks(len(d)),
                      "expected_divergent": ctx.sum_over_ranks(int(exp_sorted.shape[0])),
                      "exact_vs_construction": exact, "ms": el / args.steps * 1e3,
                      "device_ms": dms / max(args.steps, 1),
@@ -419,7 +419,7 @@ def wl_incremental(ctx, args):
         if ctx.world > 1:
             for t in variants:
                 shard_recombine(t, ctx.dist, N, device=ctx.coll)
-        return base.diff_keys_many_packed(variants)  # one shared top-down walk (mkv_tree_diff_many)
+        return base.diff_keys_many_view(variants)  # one shared top-down walk (mkv_tree_diff_many)
 
     for _ in range(args.warmup):
         diffs = step()
@@ -435,7 +435,7 @@ def wl_incremental(ctx, args):
     pool.shutdown()
     upd_ms = sum(t.prof_read("update")[0] for t in variants) / (args.steps * (R - 1))
     diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))  # batched walk: per-pair share
-    ok = all(len(d[1]) - 1 == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else
+    ok = all(len(d) == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else
     total_updates = ctx.sum_over_ranks(m) * (R - 1)
     roots = []
     if ctx.world == 1:
@@ -448,7 +448,7 @@ def wl_incremental(ctx, args):
         out["incremental"] = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
                               "update_device_ms_per_batch": upd_ms, "diff_device_ms_per_pair": diff_ms,
                               "diff_sizes_match_unique_updates": ok,
-                              "divergent_per_pair_rank0": [len(d[1]) - 1 for d in diffs], "variant_roots": roots}
+                              "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
         out["cpu_baseline"] = None if (args.no_cpu_baseline or ctx.world > 1) else cpu_baseline_update()
         print(json.dumps(out), flush=True)
 

@@ -18,7 +18,7 @@ import numpy as np
 
 from ._lib import FRINGE_BYTES, Blob, MerkleError, check, lib
 
-__all__ = ["MerkleTree", "NodeView", "pack_blob", "MerkleError"]
+__all__ = ["MerkleTree", "NodeView", "KeyList", "pack_blob", "MerkleError"]
 
 
 def _b(x) -> bytes:
@@ -73,6 +73,38 @@ def _keylist_packed(handle) -> tuple[np.ndarray, np.ndarray]:
            else np.zeros(0, np.uint8))
     offs -= np.uint64(o0)
     return raw, offs
+
+
+class KeyList:
+    """Zero-copy view of a library-owned key list (pinned host memory written by the device): .raw is
+    the key bytes, .offs the offsets rebased to 0 (n+1). The list is freed with this object."""
+
+    def __init__(self, handle):
+        self._h = handle
+        n = C.c_uint64()
+        bp = C.c_void_p()
+        op = C.c_void_p()
+        check(lib().mkv_keylist_get(handle, C.byref(n), C.byref(bp), C.byref(op)))
+        self.n = n.value
+        if self.n == 0:
+            self.raw, self.offs = np.zeros(0, np.uint8), np.zeros(1, np.uint64)
+            return
+        offs = np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_uint64)), shape=(self.n + 1,))
+        o0, o1 = int(offs[0]), int(offs[-1])
+        self.raw = np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(o1,))[o0:]
+        self.offs = offs if o0 == 0 else offs - np.uint64(o0)
+
+    def __len__(self):
+        return self.n
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().mkv_keylist_free(h)
+            except Exception:
+                pass
+            self._h = None
 
 
 def _keylist(handle) -> list[bytes]:
@@ -341,6 +373,24 @@ class MerkleTree:
             return _keylist_packed(kl)
         finally:
             lib().mkv_keylist_free(kl)
+
+    def diff_keys_view(self, other: "MerkleTree") -> KeyList:
+        """diff_keys as a zero-copy KeyList over the library's pinned result (no host-side copy)."""
+        self._flush()
+        other._flush()
+        kl = C.c_void_p()
+        check(lib().mkv_tree_diff(self._h, other._h, C.byref(kl)))
+        return KeyList(kl)
+
+    def diff_keys_many_view(self, others) -> list[KeyList]:
+        self._flush()
+        for o in others:
+            o._flush()
+        k = len(others)
+        hs = (C.c_void_p * max(k, 1))(*[o._h.value for o in others])
+        outs = (C.c_void_p * max(k, 1))()
+        check(lib().mkv_tree_diff_many(self._h, hs, k, outs))
+        return [KeyList(C.c_void_p(outs[i])) for i in range(k)]
 
     def diff_keys_many_packed(self, others) -> list[tuple[np.ndarray, np.ndarray]]:
         """[diff_keys_packed(o) for o in others] — one shared top-down walk for replicas with this

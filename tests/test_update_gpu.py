@@ -284,3 +284,29 @@ def test_antientropy_exchange_matches_diff_and_moves_little():
     d.build((kb[: 32 * 1000], ko[:1001]), (vb[: 100 * 1000], vo[:1001]))
     got4, st4 = exchange_diff(a, Peer(d))
     assert got4 == a.diff_keys_bytes(d) and st4.fallback
+
+
+def test_keylist_views_zero_copy_and_shared_blocks():
+    """KeyList views over the pinned result blocks: equal to the copied lists; per-variant views of one
+    mkv_tree_diff_many share a block, and freeing one leaves the others valid."""
+    import gc
+    n = 5000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    vs = []
+    for v in range(3):
+        t = base.clone()
+        t.upsert([keys[i] for i in range(v, n, 97)], [b"x%d" % v] * len(range(v, n, 97)))
+        vs.append(t)
+    want = [base.diff_keys_bytes(t) for t in vs]
+    views = base.diff_keys_many_view(vs)
+    del views[0]
+    gc.collect()
+    for w, kl in zip(want[1:], views):
+        b, o = kl.raw.tobytes(), kl.offs.tolist()
+        assert [b[o[i]:o[i + 1]] for i in range(len(kl))] == w
+    one = base.diff_keys_view(vs[2])
+    b, o = one.raw.tobytes(), one.offs.tolist()
+    assert [b[o[i]:o[i + 1]] for i in range(len(one))] == want[2]
