@@ -3,14 +3,15 @@
 // The reference builds a BTreeSet over the union of both leaf maps and looks every key up in both
 // HashMaps. Both trees here already hold their leaves sorted by key (R3), so the same set is a
 // merge-join of two sorted (key, digest) arrays:
-//   pass 0  partition the merged sequence into 2048-output tiles (one merge-path binary search per tile);
-//   pass 1  each 256-thread workgroup stages its A and B prefix slices (u64 BE key prefixes) in LDS,
-//           every lane finds its 8-output diagonal in LDS and merges; an A key is divergent unless the
-//           B cursor holds the same key with the same leaf digest, a B key unless the previous A key is
+//   pass 0  partition the merged sequence into 512-output wave tiles (one merge-path binary search each);
+//   pass 1  one wave per tile, no LDS: near-identical tiles (every A key paired in lockstep with a B key
+//           of the same prefix) compare their digest pairs with coalesced loads and wave ballots; any
+//           other tile runs the general per-lane 8-output merge: an A key is divergent unless the B
+//           cursor holds the same key with the same leaf digest, a B key unless the previous A key is
 //           equal. Lane results are packed to one u32 (split, from-A bits, divergent bits) plus a
 //           per-tile count;
 //   scan    exclusive scan of tile counts;
-//   pass 2  ballot/LDS compaction writes (side, index) refs of divergent keys in merged = sorted order.
+//   pass 2  wave-scan compaction writes (side, index) refs of divergent keys in merged = sorted order.
 // Ties on the 8-byte prefix fall back to a full-key compare in HBM (key_cmp), so any key set is exact.
 #include <algorithm>
 
@@ -22,9 +23,8 @@ namespace mkv {
 
 namespace {
 
-constexpr int DT = DIFF_THREADS;
 constexpr int DI = DIFF_ITEMS;
-constexpr int DTILE = DT * DI;
+constexpr int WTILE = 64 * DI;  // merged outputs per wave tile
 
 // Sorted key i of a side: storage record perm[i].
 __device__ __forceinline__ const uint8_t *key_at(const DiffSide &S, uint64_t i, uint64_t *len) {
@@ -81,7 +81,7 @@ __global__ void k_diff_partition(DiffSide A, DiffSide B, uint64_t ntiles, uint64
     uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t > ntiles) return;
     uint64_t M = A.n + B.n;
-    uint64_t d = t * DTILE;
+    uint64_t d = t * WTILE;
     if (d > M) d = M;
     split[t] = split_global(A, B, d);
 }
@@ -91,38 +91,40 @@ struct TileCtx {
     uint64_t d0;              // first merged output of the tile
 };
 
-// LDS layout: pa[0] = A[a0-1] (if a0 > 0), pa[1 + x] = A[a0 + x]; pb[x] = B[b0 + x], pb[b1-b0] = B[b1].
-__device__ __forceinline__ void stage_tile(const DiffSide &A, const DiffSide &B, const TileCtx &c, uint64_t *pa,
-                                           uint64_t *pb) {
-    const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
-    for (uint64_t x = threadIdx.x; x < na + 1; x += DT) {
-        uint64_t g = c.a0 + x;  // pa[x+1] = A[a0+x], pa[0] = A[a0-1]
-        if (x < na) pa[x + 1] = A.pfx[g];
-    }
-    if (threadIdx.x == 0) pa[0] = c.a0 > 0 ? A.pfx[c.a0 - 1] : 0;
-    for (uint64_t x = threadIdx.x; x <= nb; x += DT) {
-        uint64_t g = c.b0 + x;
-        if (g < B.n) pb[x] = B.pfx[g];
-    }
-    __syncthreads();
+// One 512-output tile per wave: tile t covers merged outputs [t*WTILE, min((t+1)*WTILE, M)).
+__device__ __forceinline__ TileCtx wave_tile(const DiffSide &A, const DiffSide &B, const uint64_t *split, uint64_t t) {
+    TileCtx c;
+    const uint64_t M = A.n + B.n;
+    c.d0 = t * WTILE;
+    uint64_t d1 = c.d0 + WTILE;
+    if (d1 > M) d1 = M;
+    c.a0 = split[t];
+    c.a1 = split[t + 1];
+    c.b0 = c.d0 - c.a0;
+    c.b1 = d1 - c.a1;
+    return c;
 }
 
-// Runs one lane's merge; returns packed (isplit << 16) | (fromA << 8) | div and the div count.
-__device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide &B, const TileCtx &c,
-                                               const uint64_t *pa, const uint64_t *pb, uint32_t *ndiv) {
+// General merge of one lane's 8 outputs; returns packed (isplit << 16) | (fromA << 8) | div and the div
+// count. Prefixes come straight from HBM/L2 (the tile's slices were just touched by the aligned check):
+// pa(0) = A[a0-1], pa(1+x) = A[a0+x], pb(x) = B[b0+x].
+__device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide &B, const TileCtx &c, uint32_t lane,
+                                            uint32_t *ndiv) {
     const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
     const uint64_t M = A.n + B.n;
-    const uint64_t dl = (uint64_t)threadIdx.x * DI;  // local diagonal
+    const uint64_t dl = (uint64_t)lane * DI;  // local diagonal
     if (c.d0 + dl >= M || dl >= na + nb) {
         *ndiv = 0;
         return 0;
     }
+    auto pa = [&](uint64_t x) -> uint64_t { return x ? A.pfx[c.a0 + x - 1] : (c.a0 ? A.pfx[c.a0 - 1] : 0); };
+    auto pb = [&](uint64_t x) -> uint64_t { return c.b0 + x < B.n ? B.pfx[c.b0 + x] : 0; };
     // local merge-path search
     uint64_t lo = dl > nb ? dl - nb : 0, hi = dl < na ? dl : na;
     while (lo < hi) {
         uint64_t mid = (lo + hi) >> 1;
         uint64_t jb = dl - 1 - mid;
-        if (cmp_merge(A, c.a0 + mid, pa[1 + mid], B, c.b0 + jb, pb[jb]) <= 0) lo = mid + 1;
+        if (cmp_merge(A, c.a0 + mid, pa(1 + mid), B, c.b0 + jb, pb(jb)) <= 0) lo = mid + 1;
         else hi = mid;
     }
     const uint32_t isplit = (uint32_t)lo;
@@ -132,7 +134,6 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
     // an A step with the same j reuses that comparison: nearly identical replicas (the anti-entropy
     // case) then pay one prefix compare + one digest compare per union key, not three.
     bool prevA_matched = false;
-#pragma unroll
     for (int s = 0; s < DI; ++s) {
         if (dl + s >= na + nb) break;
         const uint64_t li = i - c.a0, lj = j - c.b0;
@@ -142,7 +143,7 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
         if (i >= c.a1) takeA = false;
         else if (j >= B.n) takeA = true;
         else {
-            const uint64_t xa = pa[1 + li], xb = pb[lj];
+            const uint64_t xa = pa(1 + li), xb = pb(lj);
             if (xa != xb) cab = xa < xb ? -1 : 1;
             else if (digest_eq(A.dig + 32 * i, B.dig + 32 * j)) cab = 0, deq = true;  // see cmp_merge
             else cab = cmp_ab(A, i, xa, B, j, xb);
@@ -159,7 +160,7 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
         } else {
             bool matched;
             if (s > 0 && ((fromA >> (s - 1)) & 1u)) matched = prevA_matched;  // A[i-1] vs this B[j]: done
-            else matched = i > 0 && cmp_merge(A, i - 1, pa[li], B, j, pb[lj]) == 0;
+            else matched = i > 0 && cmp_merge(A, i - 1, pa(li), B, j, pb(lj)) == 0;
             prevA_matched = false;
             d = !matched;
             ++j;
@@ -170,111 +171,157 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
     return (isplit << 16) | (fromA << 8) | div;
 }
 
-__device__ __forceinline__ TileCtx tile_ctx(const DiffSide &A, const DiffSide &B, const uint64_t *split) {
-    TileCtx c;
-    const uint64_t M = A.n + B.n;
-    const uint64_t t = blockIdx.x;
-    c.d0 = t * DTILE;
-    uint64_t d1 = c.d0 + DTILE;
-    if (d1 > M) d1 = M;
-    c.a0 = split[t];
-    c.a1 = split[t + 1];
-    c.b0 = c.d0 - c.a0;
-    c.b1 = d1 - c.a1;
-    return c;
+__device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
+    return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32) | (uint32_t)__shfl((int)(uint32_t)v, src);
 }
+__device__ __forceinline__ uint4 shfl_u4(uint4 v, int src) {
+    return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
+}
+__device__ __forceinline__ bool u4eq(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
 
-__global__ __launch_bounds__(DT) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
-                                                   uint32_t *__restrict__ packed, uint32_t *__restrict__ tilecnt) {
-    __shared__ uint64_t pa[DTILE + 2];
-    __shared__ uint64_t pb[DTILE + 2];
-    __shared__ uint32_t wsum[DT / 64];
-    __shared__ int s_bad;
-    const TileCtx c = tile_ctx(A, B, split);
-    stage_tile(A, B, c, pa, pb);
-    uint32_t nd = 0;
-    uint32_t pk = 0;
-    // Aligned fast path (near-identical replicas): when the tile's A and B slices hold the same prefixes
-    // in lockstep, the merge is A0 B0 A1 B1 ... (phase 0) or, when the tile starts with the partner of the
-    // previous tile's last A, B0 A0 B1 A1 ... (phase 1). Each lane then compares its 4 digest pairs with
-    // coalesced loads instead of walking the merge with dependent loads; a pair with equal prefixes but
-    // different digests gets the full key compare, and if any such keys differ the tile takes the
-    // general merge below.
+// Pass 1, one wave per 512-output tile, no LDS (high occupancy keeps enough loads in flight).
+// Aligned fast path (near-identical replicas): when every A key of the tile has a partner B key with the
+// same prefix in lockstep, the tile's merge is A0 B0 A1 B1 ... (phase 0) or, when the tile starts with
+// the partner of the previous tile's last A, B0 A0 B1 A1 ... (phase 1). Pair x is read by lane x % 64
+// (coalesced: consecutive lanes, consecutive digests), all prefixes and digests are loaded at once, the
+// phase-1 partner comes from the neighbouring lane by shuffle, and per-pair results are gathered into
+// each output lane's 8-output word through wave ballots. A pair with equal prefixes but different
+// digests gets the full key compare; if those keys differ the tile is not aligned and the wave runs the
+// general merge instead (which is exact for any key sets).
+__global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
+                                                    uint64_t nt, uint32_t *__restrict__ packed,
+                                                    uint32_t *__restrict__ tilecnt) {
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= nt) return;  // wave-uniform
+    const uint32_t lane = threadIdx.x & 63;
+    const TileCtx c = wave_tile(A, B, split, t);
     const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
-    int phase = -1;
-    if (na == nb && na > 0) {
-        bool ok0 = true, ok1 = c.a0 > 0;
-        for (uint64_t x = threadIdx.x; x < na; x += DT) {
-            ok0 &= pa[1 + x] == pb[x];
-            ok1 &= pa[x] == pb[x];
-        }
-        const int all0 = __syncthreads_and(ok0 ? 1 : 0);
-        const int all1 = __syncthreads_and(ok1 ? 1 : 0);
-        phase = all0 ? 0 : (all1 ? 1 : -1);
-    }
-    bool general = phase < 0;
-    if (!general) {
-        if (threadIdx.x == 0) {
-            s_bad = 0;
-            // phase 1: the tile's first output B[b0] is the partner of A[a0-1] — same key?
-            if (phase == 1 && !digest_eq(A.dig + 32 * (c.a0 - 1), B.dig + 32 * c.b0) &&
-                cmp_ab(A, c.a0 - 1, pa[0], B, c.b0, pb[0]) != 0)
-                s_bad = 1;
-        }
-        __syncthreads();
-        const uint64_t dl = (uint64_t)threadIdx.x * DI;  // local diagonal: outputs dl .. dl+7
-        uint32_t div = 0;
-        if (c.d0 + dl < A.n + B.n && dl < na + nb) {
-            // A outputs of this lane: phase 0 at even offsets, phase 1 at odd offsets; 4 of them
-            for (int q = 0; q < DI / 2; ++q) {
-                const uint64_t o = dl + 2 * q + (uint64_t)phase;  // output index of the q-th A
-                if (o >= na + nb) break;
-                const uint64_t xa = (o - (uint64_t)phase) / 2;        // A index within the tile
-                const uint64_t i = c.a0 + xa, j = c.b0 + xa + (uint64_t)phase;  // lockstep partner
-                bool d;
-                if (j >= B.n) {
-                    d = true;  // no partner: A key missing on side B
-                } else if (digest_eq(A.dig + 32 * i, B.dig + 32 * j)) {
-                    d = false;
-                } else {
-                    if (cmp_ab(A, i, pa[1 + xa], B, j, A.pfx[i]) != 0) s_bad = 1;  // different keys: misaligned
-                    d = true;
-                }
-                if (d) div |= 1u << (2 * q + phase);
+    uint32_t nd = 0, pk = 0;
+    bool general = true;
+    if (na == nb) {
+        // slot q of lane l holds pair x = l + 64 q (q < 4); B[b0 + 256] and A[a0 - 1] are wave-uniform
+        // (scalar loads)
+        uint64_t pA[4], pB[4];
+        uint4 dA[4][2], dB[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t x = lane + 64 * q;
+            pA[q] = 0;
+            pB[q] = ~0ull;
+            dA[q][0] = dA[q][1] = dB[q][0] = dB[q][1] = make_uint4(0, 0, 0, 0);
+            if (x < na) {
+                pA[q] = A.pfx[c.a0 + x];
+                const uint4 *p = reinterpret_cast<const uint4 *>(A.dig + 32 * (c.a0 + x));
+                dA[q][0] = p[0];
+                dA[q][1] = p[1];
+            }
+            if (x <= nb && c.b0 + x < B.n) {
+                pB[q] = B.pfx[c.b0 + x];
+                const uint4 *p = reinterpret_cast<const uint4 *>(B.dig + 32 * (c.b0 + x));
+                dB[q][0] = p[0];
+                dB[q][1] = p[1];
             }
         }
-        __syncthreads();
-        general = s_bad != 0;
-        if (!general) {
-            nd = (uint32_t)__popc(div);
-            pk = ((uint32_t)(dl / 2) << 16) | ((phase ? 0xAAu : 0x55u) << 8) | div;
+        uint64_t pEnd = ~0ull;  // B[b0 + 256]
+        uint4 dEnd[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        if (nb == 256 && c.b0 + 256 < B.n) {
+            pEnd = B.pfx[c.b0 + 256];
+            const uint4 *p = reinterpret_cast<const uint4 *>(B.dig + 32 * (c.b0 + 256));
+            dEnd[0] = p[0];
+            dEnd[1] = p[1];
+        }
+        uint64_t pPrev = 0;  // A[a0-1], the phase-1 partner of B[b0]
+        uint4 dPrev[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        if (c.a0 > 0) {
+            pPrev = A.pfx[c.a0 - 1];
+            const uint4 *p = reinterpret_cast<const uint4 *>(A.dig + 32 * (c.a0 - 1));
+            dPrev[0] = p[0];
+            dPrev[1] = p[1];
+        }
+        // phase-1 partner of pair x is B[b0 + x + 1]: lane l+1's slot q, or lane 0's slot q+1 for lane 63.
+        // Digest equality is evaluated for both phases right away, so only flags stay live.
+        const int src = (int)((lane + 1) & 63);
+        bool ok0 = true, ok1 = true;
+        uint32_t eq0 = 0, eq1 = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint64_t x = lane + 64 * q;
+            const uint64_t pn = shfl_u64(pB[q], src), pw = q < 3 ? shfl_u64(pB[q + 1], 0) : pEnd;
+            const uint4 n0 = shfl_u4(dB[q][0], src), n1 = shfl_u4(dB[q][1], src);
+            const uint4 w0 = q < 3 ? shfl_u4(dB[q + 1][0], 0) : dEnd[0];
+            const uint4 w1 = q < 3 ? shfl_u4(dB[q + 1][1], 0) : dEnd[1];
+            const uint64_t pN = lane == 63 ? pw : pn;
+            const bool e0 = u4eq(dA[q][0], dB[q][0]) && u4eq(dA[q][1], dB[q][1]);
+            const bool e1 = lane == 63 ? (u4eq(dA[q][0], w0) && u4eq(dA[q][1], w1))
+                                       : (u4eq(dA[q][0], n0) && u4eq(dA[q][1], n1));
+            if (x < na) {
+                ok0 &= pA[q] == pB[q];
+                ok1 &= (c.b0 + x + 1 < B.n) && pA[q] == pN;
+            }
+            eq0 |= (uint32_t)e0 << q;
+            eq1 |= (uint32_t)e1 << q;
+        }
+        const bool eqPrev = u4eq(dPrev[0], dB[0][0]) && u4eq(dPrev[1], dB[0][1]);  // meaningful in lane 0
+        if (lane == 0) ok1 &= c.a0 > 0 && pPrev == pB[0];
+        int phase = -1;
+        if (__ballot(!ok0) == 0) phase = 0;
+        else if (__ballot(!ok1) == 0) phase = 1;
+        if (phase >= 0) {
+            // digest mismatches get the full key compare (equal keys: changed value -> divergent A)
+            const uint32_t eq = phase ? eq1 : eq0;
+            bool bad = false;
+            uint64_t dm[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t x = lane + 64 * q;
+                bool dv = false;
+                if (x < na && !((eq >> q) & 1u)) {
+                    dv = true;
+                    if (cmp_ab(A, c.a0 + x, pA[q], B, c.b0 + x + phase, pA[q]) != 0) bad = true;
+                }
+                dm[q] = __ballot(dv);
+            }
+            if (phase == 1 && lane == 0 && !eqPrev && cmp_ab(A, c.a0 - 1, pPrev, B, c.b0, pPrev) != 0)
+                bad = true;  // B[b0] must be the key of A[a0-1]
+            if (__ballot(bad) == 0) {
+                general = false;
+                // output lane L holds pairs 4L .. 4L+3: A outputs at even (phase 0) / odd (phase 1) bits
+                const uint32_t w = lane >> 4;
+                const uint64_t m = w == 0 ? dm[0] : w == 1 ? dm[1] : w == 2 ? dm[2] : dm[3];
+                const uint32_t nib = (uint32_t)(m >> ((4 * lane) & 63)) & 0xFu;
+                const uint32_t div =
+                    ((nib & 1u) | ((nib & 2u) << 1) | ((nib & 4u) << 2) | ((nib & 8u) << 3)) << phase;
+                const uint64_t dl = (uint64_t)lane * DI;
+                if (dl < na + nb) pk = ((uint32_t)(dl / 2) << 16) | ((phase ? 0xAAu : 0x55u) << 8) | div;
+                if (lane == 0)
+                    tilecnt[t] = (uint32_t)(__popcll(dm[0]) + __popcll(dm[1]) + __popcll(dm[2]) + __popcll(dm[3]));
+            }
         }
     }
-    if (general) pk = merge_lane(A, B, c, pa, pb, &nd);
-    packed[(uint64_t)blockIdx.x * DT + threadIdx.x] = pk;
-    // tile total
-    uint32_t s = nd;
+    if (general) {
+        pk = merge_lane(A, B, c, lane, &nd);
+        uint32_t s = nd;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t tot = 0;
-        for (int w = 0; w < DT / 64; ++w) tot += wsum[w];
-        tilecnt[blockIdx.x] = tot;
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+        if (lane == 0) tilecnt[t] = s;
     }
+    packed[t * 64 + lane] = pk;
 }
 
-__global__ __launch_bounds__(DT) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
-                                                   const uint32_t *__restrict__ packed,
-                                                   const uint64_t *__restrict__ tileoff, uint64_t *__restrict__ refs) {
-    __shared__ uint64_t lds[16];
-    const TileCtx c = tile_ctx(A, B, split);
-    const uint32_t pk = packed[(uint64_t)blockIdx.x * DT + threadIdx.x];
+// Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
+__global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
+                                                    uint64_t nt, const uint32_t *__restrict__ packed,
+                                                    const uint64_t *__restrict__ tileoff, uint64_t *__restrict__ refs) {
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= nt) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t pk = packed[t * 64 + lane];
     const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
-    uint64_t off = block_excl_scan<uint64_t>((uint64_t)__popc(div), lds, nullptr) + tileoff[blockIdx.x];
+    const uint32_t cnt = __popc(div);
+    uint64_t off = tileoff[t] + (wave_incl_scan<uint32_t>(cnt) - cnt);
     if (!div) return;
-    const uint64_t dl = (uint64_t)threadIdx.x * DI;
+    const TileCtx c = wave_tile(A, B, split, t);
+    const uint64_t dl = (uint64_t)lane * DI;
     uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
     for (int s = 0; s < DI; ++s) {
         const bool fa = (fromA >> s) & 1u;
@@ -497,10 +544,10 @@ inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_d
 }  // namespace
 
 size_t diff_scratch_bytes(uint64_t M) {
-    uint64_t nt = ceil_div(M ? M : 1, DTILE);
+    uint64_t nt = ceil_div(M ? M : 1, WTILE);
     size_t b = 0;
     b += (nt + 2) * sizeof(uint64_t);             // split
-    b += nt * DT * sizeof(uint32_t);              // packed
+    b += nt * 64 * sizeof(uint32_t);              // packed
     b += (nt + 2) * sizeof(uint32_t);             // tile counts
     b += (nt + 2) * sizeof(uint64_t);             // tile offsets
     b += scan_scratch_bytes(nt) + 1024;
@@ -514,7 +561,7 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
         MKV_HIP(hipMemsetAsync(count, 0, sizeof(uint64_t), st));
         return;
     }
-    const uint64_t nt = ceil_div(M, DTILE);
+    const uint64_t nt = ceil_div(M, WTILE);
     uint8_t *p = reinterpret_cast<uint8_t *>(scratch);
     auto carve = [&](size_t bytes) {
         uint8_t *r = p;
@@ -522,16 +569,17 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
         return r;
     };
     uint64_t *split = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
-    uint32_t *packed = reinterpret_cast<uint32_t *>(carve(nt * DT * sizeof(uint32_t)));
+    uint32_t *packed = reinterpret_cast<uint32_t *>(carve(nt * 64 * sizeof(uint32_t)));
     uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
     uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     void *sc = carve(scan_scratch_bytes(nt));
     hipLaunchKernelGGL(k_diff_partition, grid1d(nt + 1), dim3(256), 0, st, A, B, nt, split);
-    hipLaunchKernelGGL(k_diff_pass1, dim3((uint32_t)nt), dim3(DT), 0, st, A, B, split, packed, tilecnt);
+    const dim3 wg((uint32_t)ceil_div(nt, 4));
+    hipLaunchKernelGGL(k_diff_pass1, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt);
     MKV_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);
     exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
-    hipLaunchKernelGGL(k_diff_pass2, dim3((uint32_t)nt), dim3(DT), 0, st, A, B, split, packed, tileoff, refs);
+    hipLaunchKernelGGL(k_diff_pass2, wg, dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs);
     MKV_LAUNCH_CHECK();
 }
 

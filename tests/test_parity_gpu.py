@@ -235,6 +235,49 @@ def test_diff_shared_long_prefixes_vs_oracle(oracle_lib):
     assert a.diff_keys_bytes(b) == oa.diff(ob)
 
 
+def _near_identical(rng, n, shared_prefix, events):
+    """Base replica + variant with 0.2 % value changes and the given structural events."""
+    pre = b"tenant/0001/obj/" if shared_prefix else b""
+    keys = sorted({pre + b"%016x" % rng.getrandbits(64) for _ in range(n)})
+    base = [(k, b"v" + k[-6:]) for k in keys]
+    var = [(k, v + b"!" if rng.random() < 0.002 else v) for k, v in base]
+    for ev in events:
+        if ev == "insert_first":  # odd shift at the start: every later tile pairs in phase 1
+            var.append((pre + b"0", b"new"))
+        elif ev == "insert_last":
+            var.append((pre + b"\xff", b"new"))
+        elif ev == "random":  # sparse inserts + deletes
+            drop = set(rng.sample(range(len(var)), n // 1000))
+            var = [p for i, p in enumerate(var) if i not in drop]
+            var += [(pre + b"%016x" % rng.getrandbits(64) + b"+", b"ins") for _ in range(n // 1000)]
+    return base, var
+
+
+@pytest.mark.parametrize("n,shared_prefix,events", [
+    (300_000, False, ("insert_last",)),
+    (300_000, False, ("insert_first",)),
+    (300_017, False, ("random",)),
+    (257, False, ("insert_first",)),
+    (100_000, True, ("insert_first",)),
+    (100_003, True, ("random",)),
+])
+def test_merge_join_near_identical_vs_oracle(oracle_lib, n, shared_prefix, events):
+    """Merge-join (unequal leaf counts) on near-identical replicas: the aligned wave-tile fast path in
+    both pairing phases, partial last tiles, and shared 8-byte prefixes (aligned check passes on the
+    prefixes, the full key compare rejects misaligned pairs and the general merge takes over)."""
+    rng = random.Random(hash((n, shared_prefix, events)) & 0xFFFF)
+    base, var = _near_identical(rng, n, shared_prefix, events)
+    a, b = MerkleTree(), MerkleTree()
+    a.build([k for k, _ in base], [v for _, v in base])
+    b.build([k for k, _ in var], [v for _, v in var])
+    oa = oracle_lib.OracleTree.from_pairs(base)
+    ob = oracle_lib.OracleTree.from_pairs(var)
+    expect = oa.diff(ob)
+    assert expect  # the variant always differs
+    assert a.diff_keys_bytes(b) == expect
+    assert b.diff_keys_bytes(a) == ob.diff(oa)
+
+
 def test_diff_empty_trees():
     a, b = MerkleTree(), MerkleTree()
     assert a.diff_keys(b) == []
