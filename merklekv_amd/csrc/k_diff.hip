@@ -3,7 +3,8 @@
 // The reference builds a BTreeSet over the union of both leaf maps and looks every key up in both
 // HashMaps. Both trees here already hold their leaves sorted by key (R3), so the same set is a
 // merge-join of two sorted (key, digest) arrays:
-//   pass 0  partition the merged sequence into 512-output wave tiles (one merge-path binary search each);
+//   pass 0  partition the merged sequence into 512-output wave tiles (exact merge-path searches at every
+//           64th tile, interpolation + galloping search in between);
 //   pass 1  one wave per tile, no LDS: near-identical tiles (every A key paired in lockstep with a B key
 //           of the same prefix) compare their digest pairs with coalesced loads and wave ballots; any
 //           other tile runs the general per-lane 8-output merge: an A key is divergent unless the B
@@ -50,6 +51,8 @@ __device__ __forceinline__ bool digest_eq(const uint8_t *a, const uint8_t *b) {
            x1.z == y1.z && x1.w == y1.w;
 }
 
+__device__ __forceinline__ bool u4eq(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
+
 // Key order between A[i] and B[j] for the merge. Equal 8-byte prefixes first try the leaf digests:
 // equal digests mean equal encoded leaves (u32 |k| || k || u32 |v| || v), hence equal keys, unless
 // SHA-256 collides — the same assumption the top-down walk and the reference's anti-entropy make when
@@ -77,13 +80,69 @@ __device__ uint64_t split_global(const DiffSide &A, const DiffSide &B, uint64_t 
     return lo;
 }
 
+// Two-level partition. Coarse: exact global searches at every PART_STRIDE-th tile (and the last).
+constexpr uint64_t PART_STRIDE = 64;
+
 __global__ void k_diff_partition(DiffSide A, DiffSide B, uint64_t ntiles, uint64_t *__restrict__ split) {
-    uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    uint64_t M = A.n + B.n;
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nc = (ntiles + PART_STRIDE - 1) / PART_STRIDE;
+    if (u > nc) return;
+    const uint64_t t = u < nc ? u * PART_STRIDE : ntiles;
+    const uint64_t M = A.n + B.n;
     uint64_t d = t * WTILE;
     if (d > M) d = M;
     split[t] = split_global(A, B, d);
+}
+
+// Fine: every other tile's split lies between its two coarse neighbours' splits (the split is monotone
+// in the diagonal, and so is the B count). Start at the linear interpolation of the two (exact for
+// near-identical replicas up to the few inserts/deletes in between) and gallop outwards, then binary
+// search the bracket; the probes stay within a few cache lines that neighbouring tiles share.
+__global__ void k_diff_partition_fine(DiffSide A, DiffSide B, uint64_t ntiles, uint64_t *__restrict__ split) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles || t % PART_STRIDE == 0) return;
+    const uint64_t M = A.n + B.n;
+    const uint64_t t0 = t - t % PART_STRIDE, t1 = t0 + PART_STRIDE < ntiles ? t0 + PART_STRIDE : ntiles;
+    const uint64_t d = t * WTILE, d0 = t0 * WTILE, d1 = t1 * WTILE < M ? t1 * WTILE : M;
+    const uint64_t a0 = split[t0], a1 = split[t1];
+    uint64_t lo = a1 > d1 - d ? a1 - (d1 - d) : 0, hi = a0 + (d - d0);
+    if (lo < a0) lo = a0;
+    if (hi > a1) hi = a1;
+    if (d > B.n && lo < d - B.n) lo = d - B.n;
+    if (hi > A.n) hi = A.n;
+    if (hi > d) hi = d;
+    // pred(a): A[a] precedes B[d-1-a] in the merge, i.e. the split is > a (valid for lo <= a < hi)
+    auto pred = [&](uint64_t a) {
+        const uint64_t jb = d - 1 - a;
+        return cmp_merge(A, a, A.pfx[a], B, jb, B.pfx[jb]) <= 0;
+    };
+    uint64_t g = a0 + (uint64_t)((double)(a1 - a0) * (double)(d - d0) / (double)(d1 - d0) + 0.5);
+    if (g < lo) g = lo;
+    if (g > hi) g = hi;
+    uint64_t L = lo, H = hi;  // answer in [L, H]
+    if (g < hi && pred(g)) {
+        L = g + 1;
+        for (uint64_t step = 1;; step <<= 1) {
+            const uint64_t p = g + step;
+            if (p >= hi) break;
+            if (!pred(p)) { H = p; break; }
+            L = p + 1;
+        }
+    } else {
+        H = g;
+        for (uint64_t step = 1;; step <<= 1) {
+            if (g < lo + step) break;
+            const uint64_t p = g - step;
+            if (pred(p)) { L = p + 1; break; }
+            H = p;
+        }
+    }
+    while (L < H) {
+        const uint64_t mid = (L + H) >> 1;
+        if (pred(mid)) L = mid + 1;
+        else H = mid;
+    }
+    split[t] = L;
 }
 
 struct TileCtx {
@@ -171,13 +230,95 @@ __device__ __forceinline__ uint32_t merge_lane(const DiffSide &A, const DiffSide
     return (isplit << 16) | (fromA << 8) | div;
 }
 
+// Prefix-only merge of one lane's 8 outputs over the wave's LDS prefix slices (pa(0) = A[a0-1],
+// pa(1+x) = A[a0+x], pb(x) = B[b0+x], B[b1] included), A first on equal prefixes. Cross-side pairs with
+// equal prefixes are taken as the same key and verified afterwards with one batch of independent digest
+// loads (full key compare only when the digests differ). The prefix-only merge is the true merge as long
+// as the last A key and the first B key of every equal-prefix run are the same key, and that pair is
+// always among the verified ones, so a failed verification (*bad) sends the wave to the exact merge.
+constexpr int VMAX = 5;  // tentative pairs per lane: a B at output 0 plus at most 4 A/B pairs
+__device__ __forceinline__ uint32_t merge_lane_pfx(const DiffSide &A, const DiffSide &B, const TileCtx &c,
+                                                   uint32_t lane, const uint64_t *pa, const uint64_t *pb,
+                                                   uint32_t *ndiv, bool *bad) {
+    const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
+    const uint64_t M = A.n + B.n;
+    const uint64_t dl = (uint64_t)lane * DI;
+    *ndiv = 0;
+    if (c.d0 + dl >= M || dl >= na + nb) return 0;
+    uint64_t lo = dl > nb ? dl - nb : 0, hi = dl < na ? dl : na;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (pa[1 + mid] <= pb[dl - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint32_t isplit = (uint32_t)lo;
+    uint64_t i = c.a0 + lo, j = c.b0 + (dl - lo);
+    uint32_t fromA = 0, div = 0;
+    uint64_t vi[VMAX], vj[VMAX];
+    uint32_t vs[VMAX];  // output bit of each tentative pair (A output: divergent if the digests differ)
+    int nv = 0;
+    bool prevA_tie = false;
+#pragma unroll
+    for (int s = 0; s < DI; ++s) {
+        if (dl + s >= na + nb) break;
+        const uint64_t li = i - c.a0, lj = j - c.b0;
+        bool takeA, tie = false;
+        if (i >= c.a1) takeA = false;
+        else if (j >= B.n) takeA = true;
+        else {
+            const uint64_t xa = pa[1 + li], xb = pb[lj];
+            tie = xa == xb;
+            takeA = (j >= c.b1) || xa <= xb;
+        }
+        if (takeA) {
+            if (tie) {
+                if (nv == VMAX) { *bad = true; return 0; }
+                vi[nv] = i, vj[nv] = j, vs[nv] = 1u << s, ++nv;
+            } else {
+                div |= 1u << s;  // no B key shares its prefix
+            }
+            prevA_tie = tie;
+            fromA |= 1u << s;
+            ++i;
+        } else {
+            bool tieB = prevA_tie && s > 0 && ((fromA >> (s - 1)) & 1u);  // pair recorded at that A step
+            if (!tieB && i > 0 && pa[li] == pb[lj]) {
+                if (nv == VMAX) { *bad = true; return 0; }
+                vi[nv] = i - 1, vj[nv] = j, vs[nv] = 0, ++nv;  // B output: matched by key, never by digest
+                tieB = true;
+            }
+            if (!tieB) div |= 1u << s;
+            prevA_tie = false;
+            ++j;
+        }
+    }
+    // verification: all digest pairs loaded at once
+    uint4 da[VMAX][2], db[VMAX][2];
+#pragma unroll
+    for (int v = 0; v < VMAX; ++v) {
+        const uint64_t x = v < nv ? vi[v] : 0, y = v < nv ? vj[v] : 0;
+        const uint4 *p = reinterpret_cast<const uint4 *>(A.dig + 32 * x);
+        const uint4 *q = reinterpret_cast<const uint4 *>(B.dig + 32 * y);
+        da[v][0] = p[0], da[v][1] = p[1], db[v][0] = q[0], db[v][1] = q[1];
+    }
+#pragma unroll
+    for (int v = 0; v < VMAX; ++v) {
+        if (v >= nv) break;
+        if (u4eq(da[v][0], db[v][0]) && u4eq(da[v][1], db[v][1])) continue;
+        const uint64_t p = A.pfx[vi[v]];
+        if (cmp_ab(A, vi[v], p, B, vj[v], p) != 0) *bad = true;  // equal prefixes, different keys
+        else div |= vs[v];                                        // same key, changed value: A divergent
+    }
+    *ndiv = (uint32_t)__popc(div);
+    return (isplit << 16) | (fromA << 8) | div;
+}
+
 __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src) {
     return ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32) | (uint32_t)__shfl((int)(uint32_t)v, src);
 }
 __device__ __forceinline__ uint4 shfl_u4(uint4 v, int src) {
     return make_uint4(__shfl(v.x, src), __shfl(v.y, src), __shfl(v.z, src), __shfl(v.w, src));
 }
-__device__ __forceinline__ bool u4eq(uint4 a, uint4 b) { return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w; }
 
 // Pass 1, one wave per 512-output tile, no LDS (high occupancy keeps enough loads in flight).
 // Aligned fast path (near-identical replicas): when every A key of the tile has a partner B key with the
@@ -191,6 +332,7 @@ __device__ __forceinline__ bool u4eq(uint4 a, uint4 b) { return a.x == b.x && a.
 __global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, uint32_t *__restrict__ packed,
                                                     uint32_t *__restrict__ tilecnt) {
+    __shared__ uint64_t lds[4 * (WTILE + 2)];  // per-wave prefix slices for the general merge
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= nt) return;  // wave-uniform
     const uint32_t lane = threadIdx.x & 63;
@@ -299,7 +441,26 @@ __global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, cons
         }
     }
     if (general) {
-        pk = merge_lane(A, B, c, lane, &nd);
+        // stage the tile's prefixes in the wave's LDS slice: pa = lp[0 .. na], pb = lp[na+1 .. na+1+nb]
+        uint64_t *lp = lds + (threadIdx.x >> 6) * (WTILE + 2);
+        const uint64_t tot = na + nb + 2;
+#pragma unroll
+        for (int r = 0; r < (WTILE + 2 + 63) / 64; ++r) {
+            const uint64_t x = lane + 64 * r;
+            if (x < tot) {
+                uint64_t v;
+                if (x == 0) v = c.a0 ? A.pfx[c.a0 - 1] : 0;
+                else if (x <= na) v = A.pfx[c.a0 + x - 1];
+                else v = c.b0 + (x - na - 1) < B.n ? B.pfx[c.b0 + (x - na - 1)] : ~0ull;
+                lp[x] = v;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        bool bad = false;
+        pk = merge_lane_pfx(A, B, c, lane, lp, lp + na + 1, &nd, &bad);
+        if (__ballot(bad) != 0) pk = merge_lane(A, B, c, lane, &nd);  // exact merge (shared prefixes)
         uint32_t s = nd;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
@@ -573,7 +734,8 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
     uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     void *sc = carve(scan_scratch_bytes(nt));
-    hipLaunchKernelGGL(k_diff_partition, grid1d(nt + 1), dim3(256), 0, st, A, B, nt, split);
+    hipLaunchKernelGGL(k_diff_partition, grid1d(ceil_div(nt, PART_STRIDE) + 1), dim3(256), 0, st, A, B, nt, split);
+    hipLaunchKernelGGL(k_diff_partition_fine, grid1d(nt), dim3(256), 0, st, A, B, nt, split);
     const dim3 wg((uint32_t)ceil_div(nt, 4));
     hipLaunchKernelGGL(k_diff_pass1, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt);
     MKV_LAUNCH_CHECK();
