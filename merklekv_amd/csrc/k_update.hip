@@ -84,8 +84,9 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
                                                       const uint32_t *__restrict__ bidx, uint64_t m,
                                                       const uint8_t *__restrict__ bdig, uint8_t *__restrict__ nodes0,
                                                       uint32_t *__restrict__ bm, uint32_t *__restrict__ list,
-                                                      uint32_t *__restrict__ count) {
+                                                      uint32_t *__restrict__ count, const uint32_t *__restrict__ missing) {
     __shared__ uint32_t sapp[17];
+    if (*missing) return;  // some batch key is not a leaf: the caller takes the merge path, tree untouched
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = false;
     uint32_t p = 0;
@@ -104,50 +105,112 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
     block_append<uint32_t>(act, p, list, count, sapp);
 }
 
+// One dirty entry x (local index at level l): clears its children's bits, and, when its parent is owned
+// and its left sibling is not dirty (the left one owns the pair), rehashes the parent (or promotes past
+// an odd level end, R5), marks it dirty and returns true with the parent's local index in *qloc.
+__device__ __forceinline__ bool dirty_step(const DirtyLevel &L, uint64_t x, uint8_t *nodes, uint32_t *bm,
+                                           uint32_t *qloc) {
+    const uint64_t xg = L.a + x;
+    // children of this entry at level l-1: their bits are no longer read by anyone
+    if (L.has_child) {
+        const uint64_t c0 = 2 * xg - L.a_child;
+        if (c0 < L.c_child) clear_bit(bm, L.off_child + c0);
+        if (c0 + 1 < L.c_child) clear_bit(bm, L.off_child + c0 + 1);
+    }
+    const uint64_t qg = xg >> 1;
+    const bool owned = L.has_parent && qg >= L.a_par && qg < L.a_par + L.c_par;
+    if (!owned) {
+        clear_bit(bm, L.off + x);  // top of the local climb (root, or a seam parent)
+        return false;
+    }
+    if ((xg & 1) && get_bit(bm, L.off + x - 1)) return false;
+    const uint64_t lg = 2 * qg;  // left child (global); owned because the parent is
+    const uint8_t *lp = nodes + 32 * (L.off + (lg - L.a));
+    uint32_t lw[8], ow[8];
+    load_digest(lp, lw);
+    if (lg + 1 < L.S) {
+        uint32_t rw[8];
+        load_digest(lp + 32, rw);
+        sha_node<true>(lw, rw, ow);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) ow[q] = lw[q];  // R5 promotion
+    }
+    *qloc = (uint32_t)(qg - L.a_par);
+    store_digest(nodes + 32 * (L.off_par + *qloc), ow);
+    set_bit(bm, L.off_par + *qloc);
+    return true;
+}
+
 __global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, uint8_t *__restrict__ nodes,
                                                      uint32_t *__restrict__ bm, const uint32_t *__restrict__ lin,
                                                      const uint32_t *__restrict__ nin, uint32_t *__restrict__ lout,
-                                                     uint32_t *__restrict__ nout) {
+                                                     uint32_t *__restrict__ nout, const uint32_t *__restrict__ missing) {
     __shared__ uint32_t sapp[17];
+    if (*missing) return;
     const uint32_t cnt = *nin;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if ((uint64_t)blockIdx.x * blockDim.x >= cnt) return;  // whole workgroup idle (wave-uniform exit)
     bool act = false;
     uint32_t qloc = 0;
-    uint32_t ow[8];
-    if (i < cnt) {
-        const uint64_t x = lin[i];  // local index at level l
-        const uint64_t xg = L.a + x;
-        // children of this entry at level l-1: their bits are no longer read by anyone
-        if (L.has_child) {
-            const uint64_t c0 = 2 * xg - L.a_child;
-            if (c0 < L.c_child) clear_bit(bm, L.off_child + c0);
-            if (c0 + 1 < L.c_child) clear_bit(bm, L.off_child + c0 + 1);
-        }
-        const uint64_t qg = xg >> 1;
-        const bool owned = L.has_parent && qg >= L.a_par && qg < L.a_par + L.c_par;
-        if (!owned) {
-            clear_bit(bm, L.off + x);  // top of the local climb (root, or a seam parent)
-        } else if (!((xg & 1) && get_bit(bm, L.off + x - 1))) {
-            const uint64_t lg = 2 * qg;  // left child (global); owned because the parent is
-            const uint8_t *lp = nodes + 32 * (L.off + (lg - L.a));
-            uint32_t lw[8];
-            load_digest(lp, lw);
-            if (lg + 1 < L.S) {
-                uint32_t rw[8];
-                load_digest(lp + 32, rw);
-                sha_node<true>(lw, rw, ow);
-            } else {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) ow[q] = lw[q];  // R5 promotion
-            }
-            qloc = (uint32_t)(qg - L.a_par);
-            store_digest(nodes + 32 * (L.off_par + qloc), ow);
-            set_bit(bm, L.off_par + qloc);
-            act = true;
-        }
-    }
+    if (i < cnt) act = dirty_step(L, lin[i], nodes, bm, &qloc);
     block_append<uint32_t>(act, qloc, lout, nout, sapp);
+}
+
+__device__ __forceinline__ DirtyLevel level_of(const LevelPlan &P, int l) {
+    DirtyLevel D{};
+    D.a = P.base[l];
+    D.c = P.cnt[l];
+    D.off = P.off[l];
+    D.S = P.S[l];
+    D.has_parent = l + 1 < P.L && P.cnt[l + 1] > 0;
+    if (D.has_parent) {
+        D.a_par = P.base[l + 1];
+        D.c_par = P.cnt[l + 1];
+        D.off_par = P.off[l + 1];
+    }
+    D.has_child = l > 0;
+    if (l > 0) {
+        D.a_child = P.base[l - 1];
+        D.c_child = P.cnt[l - 1];
+        D.off_child = P.off[l - 1];
+    }
+    return D;
+}
+
+// All levels from l0 up in one workgroup, once a level's dirty set fits DIRTY_TOP_CAP (it never grows
+// going up): the dirty lists live in LDS, levels are separated by a device-scope fence + barrier instead
+// of a kernel boundary. Replaces the ~13 latency-bound single-workgroup launches at the top of a 1e8-leaf
+// tree, and every launch above level 0 for batches of at most DIRTY_TOP_CAP keys.
+__global__ __launch_bounds__(DIRTY_TOP_THREADS) void k_dirty_top(LevelPlan P, int l0, uint8_t *__restrict__ nodes,
+                                                                uint32_t *__restrict__ bm,
+                                                                const uint32_t *__restrict__ lin,
+                                                                const uint32_t *__restrict__ nin,
+                                                                const uint32_t *__restrict__ missing) {
+    __shared__ uint32_t list[2][DIRTY_TOP_CAP];
+    __shared__ uint32_t ncnt[2];
+    if (*missing) return;
+    uint32_t n = *nin;
+    if (n > DIRTY_TOP_CAP) n = DIRTY_TOP_CAP;  // cannot happen: the host bounds the level's dirty count
+    for (uint32_t e = threadIdx.x; e < n; e += DIRTY_TOP_THREADS) list[0][e] = lin[e];
+    if (threadIdx.x == 0) ncnt[1] = 0;
+    __syncthreads();
+    int cur = 0;
+    for (int l = l0; l < P.L; ++l) {
+        const DirtyLevel D = level_of(P, l);
+        for (uint32_t e = threadIdx.x; e < n; e += DIRTY_TOP_THREADS) {
+            uint32_t q;
+            if (dirty_step(D, list[cur][e], nodes, bm, &q)) list[cur ^ 1][atomicAdd(&ncnt[cur ^ 1], 1u)] = q;
+        }
+        __threadfence();  // parents' digests and bits visible to every wave of the next level
+        __syncthreads();
+        if (!D.has_parent) break;
+        n = ncnt[cur ^ 1];
+        cur ^= 1;
+        __syncthreads();
+        if (threadIdx.x == 0) ncnt[cur ^ 1] = 0;
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -297,16 +360,25 @@ void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const Di
 }
 
 void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
-                         uint32_t *bm, uint32_t *list, uint32_t *count, hipStream_t st) {
+                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st) {
     if (!m) return;
-    hipLaunchKernelGGL(k_dirty_leaves, grid1d(m), dim3(256), 0, st, pos, bidx, m, bdig, nodes0, bm, list, count);
+    hipLaunchKernelGGL(k_dirty_leaves, grid1d(m), dim3(256), 0, st, pos, bidx, m, bdig, nodes0, bm, list, count,
+                       missing);
     MKV_LAUNCH_CHECK();
 }
 
 void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
-                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, hipStream_t st) {
+                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, const uint32_t *missing,
+                        hipStream_t st) {
     if (!max_entries) return;
-    hipLaunchKernelGGL(k_dirty_level, grid1d(max_entries), dim3(256), 0, st, L, nodes, bm, lin, nin, lout, nout);
+    hipLaunchKernelGGL(k_dirty_level, grid1d(max_entries), dim3(256), 0, st, L, nodes, bm, lin, nin, lout, nout,
+                       missing);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_dirty_top(const LevelPlan &P, int l0, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
+                      const uint32_t *nin, const uint32_t *missing, hipStream_t st) {
+    hipLaunchKernelGGL(k_dirty_top, dim3(1), dim3(DIRTY_TOP_THREADS), 0, st, P, l0, nodes, bm, lin, nin, missing);
     MKV_LAUNCH_CHECK();
 }
 

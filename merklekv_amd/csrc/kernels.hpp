@@ -168,7 +168,7 @@ void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const Di
                    uint32_t *idx, uint32_t *missing, hipStream_t st);
 // (pos, bidx) sorted by pos (stable): scatter the last write per position into level 0, mark dirty.
 void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
-                         uint32_t *bm, uint32_t *list, uint32_t *count, hipStream_t st);
+                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st);
 // Level l of the local plan: owned global range [a, a+c) stored at node offset off, global size S;
 // parent level (l+1) and child level (l-1) ranges for ownership tests and bit clearing.
 struct DirtyLevel {
@@ -178,7 +178,19 @@ struct DirtyLevel {
     int has_parent, has_child;
 };
 void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
-                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, hipStream_t st);
+                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, const uint32_t *missing,
+                        hipStream_t st);
+// Level plan of a tree handle for the fused top-level climb (k_dirty_top).
+constexpr int MKV_MAXLEV = 48;
+struct LevelPlan {
+    uint64_t base[MKV_MAXLEV], cnt[MKV_MAXLEV], off[MKV_MAXLEV], S[MKV_MAXLEV];
+    int L;
+};
+constexpr int DIRTY_TOP_THREADS = 1024;
+constexpr uint64_t DIRTY_TOP_CAP = 4096;  // dirty entries per level the fused climb holds in LDS
+// Levels l0 .. top in one workgroup; requires every level >= l0 to have at most DIRTY_TOP_CAP dirty entries.
+void launch_dirty_top(const LevelPlan &P, int l0, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
+                      const uint32_t *nin, const uint32_t *missing, hipStream_t st);
 
 // Batch merge (k_update.hip): A = the tree's sorted leaves (dig = leaf level, indexed by position),
 // B = sorted unique batch (perm = batch storage index, dig = batch digests in storage order, tomb =

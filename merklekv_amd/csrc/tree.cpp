@@ -970,6 +970,7 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
     const uint64_t nn = total_nodes(t);
     hipStream_t st = t->st;
     size_t ptot = prof_begin(t, "update");
+    const bool had_root = t->has_root, had_pending = t->combine_pending;
     // bitmap: one bit per stored node, zero between calls
     const uint64_t words = (nn + 63) / 32 + 2;
     uint32_t *bm = ens<uint32_t>(t->u_bm, words);
@@ -981,12 +982,11 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
     MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, st));
     uint64_t *pos = ens<uint64_t>(t->u_pos, m + 1), *pos2 = ens<uint64_t>(t->u_pos2, m + 1);
     uint32_t *idx = ens<uint32_t>(t->u_idx, m + 1), *idx2 = ens<uint32_t>(t->u_idx2, m + 1);
+    // Keys that are not leaves are counted in cnt[L+1]; every dirty kernel checks that count on the
+    // device and does nothing when it is non-zero, so the whole climb is enqueued without a host round
+    // trip and the host reads the count once at the end (then the caller takes the merge path).
+    const uint32_t *missing = cnt + L + 1;
     launch_locate(kb, koff, m, side_of(t), pos, idx, cnt + L + 1, st);
-    if (d2h_u32(t, cnt + L + 1, st) != 0) {
-        prof_end(t, ptot);
-        sync(t);
-        return false;
-    }
     uint8_t *bdig = ens<uint8_t>(t->u_dig, m * 32);
     launch_leaf_hash(kb, koff, vb, voff, m, bdig, st);
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
@@ -994,8 +994,13 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
     uint32_t *l0 = ens<uint32_t>(t->u_l0, m + 1), *l1 = ens<uint32_t>(t->u_l1, m + 1);
     t->bm_dirty = true;
     uint8_t *nodes = t->nodes.as<uint8_t>();
-    launch_dirty_leaves(sw ? pos2 : pos, sw ? idx2 : idx, m, bdig, nodes, bm, l0, cnt, st);
-    for (size_t l = 0; l < L; ++l) {
+    launch_dirty_leaves(sw ? pos2 : pos, sw ? idx2 : idx, m, bdig, nodes, bm, l0, cnt, missing, st);
+    // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest of
+    // the climb in one fused launch (the dirty count never exceeds min(m, level size))
+    size_t ltop = 0;
+    while (ltop < L && std::min<uint64_t>(m, t->lev_cnt[ltop]) > DIRTY_TOP_CAP) ++ltop;
+    if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
+    for (size_t l = 0; l < ltop; ++l) {
         DirtyLevel D{};
         D.a = t->lev_base[l];
         D.c = t->lev_cnt[l];
@@ -1013,10 +1018,23 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
             D.c_child = t->lev_cnt[l - 1];
             D.off_child = t->lev_off[l - 1];
         }
-        launch_dirty_level(D, std::min<uint64_t>(m, t->lev_cnt[l]), nodes, bm, l0, cnt + l, l1, cnt + l + 1, st);
+        launch_dirty_level(D, std::min<uint64_t>(m, t->lev_cnt[l]), nodes, bm, l0, cnt + l, l1, cnt + l + 1, missing,
+                           st);
         std::swap(l0, l1);
         if (!D.has_parent) break;  // every entry at this level cleared its own bit: bitmap is zero again
     }
+    if (ltop < L) {
+        LevelPlan P{};
+        P.L = (int)L;
+        for (size_t l = 0; l < L; ++l) {
+            P.base[l] = t->lev_base[l];
+            P.cnt[l] = t->lev_cnt[l];
+            P.off[l] = t->lev_off[l];
+            P.S[l] = t->lev_S[l];
+        }
+        launch_dirty_top(P, (int)ltop, nodes, bm, l0, cnt + ltop, missing, st);
+    }
+    MKV_HIP(hipMemcpyAsync(t->h_small, missing, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     if (!t->sharded) {
         MKV_HIP(hipMemcpyAsync(t->root, nodes + 32 * t->lev_off[L - 1], 32, hipMemcpyDeviceToHost, st));
         t->has_root = true;
@@ -1027,6 +1045,11 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
     prof_end(t, ptot);
     sync(t);
     t->bm_dirty = false;
+    if (reinterpret_cast<volatile uint32_t *>(t->h_small)[0] != 0) {  // tree untouched
+        t->has_root = had_root;
+        t->combine_pending = had_pending;
+        return false;
+    }
     return true;
 }
 
