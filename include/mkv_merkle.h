@@ -75,6 +75,13 @@ mkv_status mkv_tree_build_wire(mkv_tree *t, const uint8_t *scan, uint64_t scan_l
 mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values);
 /* Same with device pointers (batch already resident in HBM; same contract as mkv_tree_build_device). */
 mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
+/* k x mkv_tree_upsert_device(trees[i], keys[i], values[i]) — the anti-entropy round that applies one
+ * value batch to each of k replicas (sync.rs:62-90 calls insert per repaired key on each node; configs[4]
+ * applies a 125K-key batch to each of 7 replicas). Results are identical to k separate calls. Replicas
+ * with one level plan (same key set) share the dirty climb: one launch per tree level for all of them.
+ * Trees must be distinct. */
+mkv_status mkv_tree_upsert_device_many(mkv_tree *const *trees, const mkv_blob *keys, const mkv_blob *values,
+                                       uint32_t k);
 /* n x remove(k_i) — merkle.rs:59-62. Missing keys are ignored. */
 mkv_status mkv_tree_remove(mkv_tree *t, mkv_blob keys);
 /* Mixed batch: record i is remove(k_i) if is_remove[i] else insert(k_i, v_i), applied in order. values

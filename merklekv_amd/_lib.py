@@ -20,7 +20,7 @@ FRINGE_BYTES = FRINGE_ENTRY_BYTES * FRINGE_MAX_ENTRIES
 EXPORTS = [
     "mkv_tree_create", "mkv_tree_destroy", "mkv_tree_clone", "mkv_tree_build", "mkv_tree_build_device",
     "mkv_tree_build_wire",
-    "mkv_tree_upsert", "mkv_tree_upsert_device", "mkv_tree_remove", "mkv_tree_apply", "mkv_tree_root", "mkv_tree_len",
+    "mkv_tree_upsert", "mkv_tree_upsert_device", "mkv_tree_upsert_device_many", "mkv_tree_remove", "mkv_tree_apply", "mkv_tree_root", "mkv_tree_len",
     "mkv_tree_node_count", "mkv_tree_level_count", "mkv_tree_level", "mkv_tree_leaves", "mkv_tree_diff",
     "mkv_tree_diff_many", "mkv_tree_node_digests", "mkv_tree_compare_nodes", "mkv_tree_keys_at",
     "mkv_tree_prefix_root", "mkv_keylist_get", "mkv_keylist_free", "mkv_last_error", "mkv_shard_prepare",
@@ -61,6 +61,7 @@ def lib():
         "mkv_tree_build_wire": ([vp, vp, u64, vp, u64], i32),
         "mkv_tree_upsert": ([vp, Blob, Blob], i32),
         "mkv_tree_upsert_device": ([vp, Blob, Blob], i32),
+        "mkv_tree_upsert_device_many": ([P(vp), P(Blob), P(Blob), u32], i32),
         "mkv_tree_remove": ([vp, Blob], i32),
         "mkv_tree_apply": ([vp, Blob, Blob, vp], i32),
         "mkv_tree_root": ([vp, vp, P(i32)], i32),

@@ -142,19 +142,19 @@ __device__ __forceinline__ bool dirty_step(const DirtyLevel &L, uint64_t x, uint
     return true;
 }
 
-__global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, uint8_t *__restrict__ nodes,
-                                                     uint32_t *__restrict__ bm, const uint32_t *__restrict__ lin,
-                                                     const uint32_t *__restrict__ nin, uint32_t *__restrict__ lout,
-                                                     uint32_t *__restrict__ nout, const uint32_t *__restrict__ missing) {
+__global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, int l, DirtyTrees T) {
     __shared__ uint32_t sapp[17];
-    if (*missing) return;
-    const uint32_t cnt = *nin;
+    const DirtyTree &D = T.t[blockIdx.y];
+    if (*D.missing) return;
+    const uint32_t *lin = (l & 1) ? D.l1 : D.l0;
+    uint32_t *lout = (l & 1) ? D.l0 : D.l1;
+    const uint32_t cnt = D.cnt[l];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if ((uint64_t)blockIdx.x * blockDim.x >= cnt) return;  // whole workgroup idle (wave-uniform exit)
     bool act = false;
     uint32_t qloc = 0;
-    if (i < cnt) act = dirty_step(L, lin[i], nodes, bm, &qloc);
-    block_append<uint32_t>(act, qloc, lout, nout, sapp);
+    if (i < cnt) act = dirty_step(L, lin[i], D.nodes, D.bm, &qloc);
+    block_append<uint32_t>(act, qloc, lout, D.cnt + l + 1, sapp);
 }
 
 __device__ __forceinline__ DirtyLevel level_of(const LevelPlan &P, int l) {
@@ -182,11 +182,13 @@ __device__ __forceinline__ DirtyLevel level_of(const LevelPlan &P, int l) {
 // going up): the dirty lists live in LDS, levels are separated by a device-scope fence + barrier instead
 // of a kernel boundary. Replaces the ~13 latency-bound single-workgroup launches at the top of a 1e8-leaf
 // tree, and every launch above level 0 for batches of at most DIRTY_TOP_CAP keys.
-__global__ __launch_bounds__(DIRTY_TOP_THREADS) void k_dirty_top(LevelPlan P, int l0, uint8_t *__restrict__ nodes,
-                                                                uint32_t *__restrict__ bm,
-                                                                const uint32_t *__restrict__ lin,
-                                                                const uint32_t *__restrict__ nin,
-                                                                const uint32_t *__restrict__ missing) {
+__global__ __launch_bounds__(DIRTY_TOP_THREADS) void k_dirty_top(LevelPlan P, int l0, DirtyTrees T) {
+    const DirtyTree &Dt = T.t[blockIdx.x];  // one workgroup per tree
+    uint8_t *nodes = Dt.nodes;
+    uint32_t *bm = Dt.bm;
+    const uint32_t *lin = (l0 & 1) ? Dt.l1 : Dt.l0;
+    const uint32_t *nin = Dt.cnt + l0;
+    const uint32_t *missing = Dt.missing;
     __shared__ uint32_t list[2][DIRTY_TOP_CAP];
     __shared__ uint32_t ncnt[2];
     if (*missing) return;
@@ -367,18 +369,16 @@ void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, 
     MKV_LAUNCH_CHECK();
 }
 
-void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
-                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, const uint32_t *missing,
+void launch_dirty_level(const DirtyLevel &L, int l, uint64_t max_entries, const DirtyTrees &T, uint32_t k,
                         hipStream_t st) {
-    if (!max_entries) return;
-    hipLaunchKernelGGL(k_dirty_level, grid1d(max_entries), dim3(256), 0, st, L, nodes, bm, lin, nin, lout, nout,
-                       missing);
+    if (!max_entries || !k) return;
+    hipLaunchKernelGGL(k_dirty_level, dim3((uint32_t)ceil_div(max_entries, 256), k), dim3(256), 0, st, L, l, T);
     MKV_LAUNCH_CHECK();
 }
 
-void launch_dirty_top(const LevelPlan &P, int l0, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
-                      const uint32_t *nin, const uint32_t *missing, hipStream_t st) {
-    hipLaunchKernelGGL(k_dirty_top, dim3(1), dim3(DIRTY_TOP_THREADS), 0, st, P, l0, nodes, bm, lin, nin, missing);
+void launch_dirty_top(const LevelPlan &P, int l0, const DirtyTrees &T, uint32_t k, hipStream_t st) {
+    if (!k) return;
+    hipLaunchKernelGGL(k_dirty_top, dim3(k), dim3(DIRTY_TOP_THREADS), 0, st, P, l0, T);
     MKV_LAUNCH_CHECK();
 }
 

@@ -177,8 +177,21 @@ struct DirtyLevel {
     uint64_t a_child, c_child, off_child;
     int has_parent, has_child;
 };
-void launch_dirty_level(const DirtyLevel &L, uint64_t max_entries, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
-                        const uint32_t *nin, uint32_t *lout, uint32_t *nout, const uint32_t *missing,
+// One tree of a batched climb: its nodes, bitmap, the two dirty-list buffers (level l reads l0 when l is
+// even, l1 when odd), the per-level counts and the device missing-key count (non-zero: do nothing).
+struct DirtyTree {
+    uint8_t *nodes;
+    uint32_t *bm;
+    uint32_t *l0, *l1;
+    uint32_t *cnt;
+    const uint32_t *missing;
+};
+constexpr int DIRTY_MAX_TREES = 16;
+struct DirtyTrees {
+    DirtyTree t[DIRTY_MAX_TREES];
+};
+// Level l of k trees sharing the level plan (grid.y = tree).
+void launch_dirty_level(const DirtyLevel &L, int l, uint64_t max_entries, const DirtyTrees &T, uint32_t k,
                         hipStream_t st);
 // Level plan of a tree handle for the fused top-level climb (k_dirty_top).
 constexpr int MKV_MAXLEV = 48;
@@ -189,8 +202,7 @@ struct LevelPlan {
 constexpr int DIRTY_TOP_THREADS = 1024;
 constexpr uint64_t DIRTY_TOP_CAP = 4096;  // dirty entries per level the fused climb holds in LDS
 // Levels l0 .. top in one workgroup; requires every level >= l0 to have at most DIRTY_TOP_CAP dirty entries.
-void launch_dirty_top(const LevelPlan &P, int l0, uint8_t *nodes, uint32_t *bm, const uint32_t *lin,
-                      const uint32_t *nin, const uint32_t *missing, hipStream_t st);
+void launch_dirty_top(const LevelPlan &P, int l0, const DirtyTrees &T, uint32_t k, hipStream_t st);
 
 // Batch merge (k_update.hip): A = the tree's sorted leaves (dig = leaf level, indexed by position),
 // B = sorted unique batch (perm = batch storage index, dig = batch digests in storage order, tomb =

@@ -962,15 +962,23 @@ static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
 
 // Dirty-path update (k_update.hip) for a batch whose keys are all leaves already: same key order and
 // level plan, so only changed leaves and their ancestors are rehashed. Batch records are device
-// pointers. Returns false, having changed nothing, when some key is not a leaf.
-static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
-                         const uint64_t *voff, uint64_t m) {
-    if (t->n == 0 || t->prepared || m == 0) return m == 0 && t->n > 0;
+// pointers. A batch with a key that is not a leaf changes nothing and reports false.
+static bool same_plan(const mkv_tree *a, const mkv_tree *b);
+
+struct DirtyBatch {
+    const uint8_t *kb;
+    const uint64_t *koff;
+    const uint8_t *vb;
+    const uint64_t *voff;
+    uint64_t m;
+};
+
+// Phase 1 on the tree's own stream: locate the batch keys, hash the batch, sort by position, scatter the
+// last write per position into level 0 (level-0 dirty list in u_l0, counts in u_cnt).
+static DirtyTree dirty_prepare(mkv_tree *t, const DirtyBatch &b) {
     const size_t L = t->lev_S.size();
-    const uint64_t nn = total_nodes(t);
+    const uint64_t nn = total_nodes(t), m = b.m;
     hipStream_t st = t->st;
-    size_t ptot = prof_begin(t, "update");
-    const bool had_root = t->has_root, had_pending = t->combine_pending;
     // bitmap: one bit per stored node, zero between calls
     const uint64_t words = (nn + 63) / 32 + 2;
     uint32_t *bm = ens<uint32_t>(t->u_bm, words);
@@ -986,71 +994,140 @@ static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, c
     // device and does nothing when it is non-zero, so the whole climb is enqueued without a host round
     // trip and the host reads the count once at the end (then the caller takes the merge path).
     const uint32_t *missing = cnt + L + 1;
-    launch_locate(kb, koff, m, side_of(t), pos, idx, cnt + L + 1, st);
+    launch_locate(b.kb, b.koff, m, side_of(t), pos, idx, cnt + L + 1, st);
     uint8_t *bdig = ens<uint8_t>(t->u_dig, m * 32);
-    launch_leaf_hash(kb, koff, vb, voff, m, bdig, st);
+    launch_leaf_hash(b.kb, b.koff, b.vb, b.voff, m, bdig, st);
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
     const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, m, 0, std::max(8, bits_for(t->n)), radix, st);
     uint32_t *l0 = ens<uint32_t>(t->u_l0, m + 1), *l1 = ens<uint32_t>(t->u_l1, m + 1);
     t->bm_dirty = true;
     uint8_t *nodes = t->nodes.as<uint8_t>();
     launch_dirty_leaves(sw ? pos2 : pos, sw ? idx2 : idx, m, bdig, nodes, bm, l0, cnt, missing, st);
-    // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest of
-    // the climb in one fused launch (the dirty count never exceeds min(m, level size))
-    size_t ltop = 0;
-    while (ltop < L && std::min<uint64_t>(m, t->lev_cnt[ltop]) > DIRTY_TOP_CAP) ++ltop;
-    if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
-    for (size_t l = 0; l < ltop; ++l) {
-        DirtyLevel D{};
-        D.a = t->lev_base[l];
-        D.c = t->lev_cnt[l];
-        D.off = t->lev_off[l];
-        D.S = t->lev_S[l];
-        D.has_parent = l + 1 < L && t->lev_cnt[l + 1] > 0;
-        if (D.has_parent) {
-            D.a_par = t->lev_base[l + 1];
-            D.c_par = t->lev_cnt[l + 1];
-            D.off_par = t->lev_off[l + 1];
+    return DirtyTree{nodes, bm, l0, l1, cnt, missing};
+}
+
+// k dirty-path updates at once (mkv_tree_upsert_device_many; k = 1 is mkv_tree_upsert_device): phase 1
+// runs per tree on its own stream, then trees sharing one level plan climb together — one launch per
+// level for all of them (grid.y = tree) and one fused top launch — instead of k interleaved chains of
+// small launches. ok[i] = false: tree i had a key that is not a leaf and is unchanged.
+static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_t k, bool *ok) {
+    std::vector<uint32_t> act;
+    for (uint32_t i = 0; i < k; ++i) {
+        mkv_tree *t = ts[i];
+        ok[i] = bs[i].m == 0 && t->n > 0;
+        if (t->n > 0 && !t->prepared && bs[i].m > 0) act.push_back(i);
+    }
+    if (act.empty()) return;
+    // group by level plan (replicas of one key set share it); each group climbs together
+    std::vector<std::vector<uint32_t>> groups;
+    for (uint32_t i : act) {
+        bool placed = false;
+        for (auto &g : groups)
+            if (g.size() < (size_t)DIRTY_MAX_TREES && ts[g[0]]->dev == ts[i]->dev && same_plan(ts[g[0]], ts[i])) {
+                g.push_back(i);
+                placed = true;
+                break;
+            }
+        if (!placed) groups.push_back({i});
+    }
+    for (auto &g : groups) {
+        mkv_tree *t0 = ts[g[0]];
+        DevGuard dg(t0->dev);
+        hipStream_t st = t0->st;
+        const size_t L = t0->lev_S.size();
+        std::vector<size_t> prof(g.size());
+        std::vector<char> had_root(g.size()), had_pending(g.size());
+        for (size_t q = 0; q < g.size(); ++q) {
+            mkv_tree *t = ts[g[q]];
+            prof[q] = prof_begin(t, "update", st);
+            had_root[q] = t->has_root;
+            had_pending[q] = t->combine_pending;
         }
-        D.has_child = l > 0;
-        if (l > 0) {
-            D.a_child = t->lev_base[l - 1];
-            D.c_child = t->lev_cnt[l - 1];
-            D.off_child = t->lev_off[l - 1];
+        MKV_HIP(hipEventRecord(t0->ev_in, st));
+        DirtyTrees T{};
+        uint64_t mmax = 0;
+        for (size_t q = 0; q < g.size(); ++q) {
+            mkv_tree *t = ts[g[q]];
+            if (q) MKV_HIP(hipStreamWaitEvent(t->st, t0->ev_in, 0));
+            T.t[q] = dirty_prepare(t, bs[g[q]]);
+            mmax = std::max(mmax, bs[g[q]].m);
+            if (q) {
+                MKV_HIP(hipEventRecord(t->ev_join, t->st));
+                MKV_HIP(hipStreamWaitEvent(st, t->ev_join, 0));
+            }
         }
-        launch_dirty_level(D, std::min<uint64_t>(m, t->lev_cnt[l]), nodes, bm, l0, cnt + l, l1, cnt + l + 1, missing,
-                           st);
-        std::swap(l0, l1);
-        if (!D.has_parent) break;  // every entry at this level cleared its own bit: bitmap is zero again
-    }
-    if (ltop < L) {
-        LevelPlan P{};
-        P.L = (int)L;
-        for (size_t l = 0; l < L; ++l) {
-            P.base[l] = t->lev_base[l];
-            P.cnt[l] = t->lev_cnt[l];
-            P.off[l] = t->lev_off[l];
-            P.S[l] = t->lev_S[l];
+        const uint32_t k2 = (uint32_t)g.size();
+        // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest
+        // of the climb in one fused launch (the dirty count never exceeds min(m, level size))
+        size_t ltop = 0;
+        while (ltop < L && std::min<uint64_t>(mmax, t0->lev_cnt[ltop]) > DIRTY_TOP_CAP) ++ltop;
+        if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
+        for (size_t l = 0; l < ltop; ++l) {
+            DirtyLevel D{};
+            D.a = t0->lev_base[l];
+            D.c = t0->lev_cnt[l];
+            D.off = t0->lev_off[l];
+            D.S = t0->lev_S[l];
+            D.has_parent = l + 1 < L && t0->lev_cnt[l + 1] > 0;
+            if (D.has_parent) {
+                D.a_par = t0->lev_base[l + 1];
+                D.c_par = t0->lev_cnt[l + 1];
+                D.off_par = t0->lev_off[l + 1];
+            }
+            D.has_child = l > 0;
+            if (l > 0) {
+                D.a_child = t0->lev_base[l - 1];
+                D.c_child = t0->lev_cnt[l - 1];
+                D.off_child = t0->lev_off[l - 1];
+            }
+            launch_dirty_level(D, (int)l, std::min<uint64_t>(mmax, t0->lev_cnt[l]), T, k2, st);
+            if (!D.has_parent) break;  // every entry at this level cleared its own bit: bitmap is zero again
         }
-        launch_dirty_top(P, (int)ltop, nodes, bm, l0, cnt + ltop, missing, st);
+        if (ltop < L) {
+            LevelPlan P{};
+            P.L = (int)L;
+            for (size_t l = 0; l < L; ++l) {
+                P.base[l] = t0->lev_base[l];
+                P.cnt[l] = t0->lev_cnt[l];
+                P.off[l] = t0->lev_off[l];
+                P.S[l] = t0->lev_S[l];
+            }
+            launch_dirty_top(P, (int)ltop, T, k2, st);
+        }
+        for (size_t q = 0; q < g.size(); ++q) {
+            mkv_tree *t = ts[g[q]];
+            MKV_HIP(hipMemcpyAsync(t->h_small, T.t[q].missing, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            if (!t->sharded) {
+                MKV_HIP(hipMemcpyAsync(t->root, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32,
+                                       hipMemcpyDeviceToHost, st));
+                t->has_root = true;
+            } else {
+                t->has_root = false;
+                t->combine_pending = true;  // seam + global root: mkv_shard_fringe + all-gather + combine
+            }
+            prof_end(t, prof[q]);
+        }
+        MKV_HIP(hipEventRecord(t0->ev_join, st));
+        for (size_t q = 1; q < g.size(); ++q) MKV_HIP(hipStreamWaitEvent(ts[g[q]]->st, t0->ev_join, 0));
+        for (size_t q = 0; q < g.size(); ++q) {
+            mkv_tree *t = ts[g[q]];
+            sync(t);
+            t->bm_dirty = false;
+            ok[g[q]] = reinterpret_cast<volatile uint32_t *>(t->h_small)[0] == 0;
+            if (!ok[g[q]]) {  // tree untouched
+                t->has_root = had_root[q];
+                t->combine_pending = had_pending[q];
+            }
+        }
     }
-    MKV_HIP(hipMemcpyAsync(t->h_small, missing, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    if (!t->sharded) {
-        MKV_HIP(hipMemcpyAsync(t->root, nodes + 32 * t->lev_off[L - 1], 32, hipMemcpyDeviceToHost, st));
-        t->has_root = true;
-    } else {
-        t->has_root = false;
-        t->combine_pending = true;  // the seam and the global root: mkv_shard_fringe + all-gather + combine
-    }
-    prof_end(t, ptot);
-    sync(t);
-    t->bm_dirty = false;
-    if (reinterpret_cast<volatile uint32_t *>(t->h_small)[0] != 0) {  // tree untouched
-        t->has_root = had_root;
-        t->combine_pending = had_pending;
-        return false;
-    }
-    return true;
+}
+
+static bool dirty_update(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
+                         const uint64_t *voff, uint64_t m) {
+    const DirtyBatch b{kb, koff, vb, voff, m};
+    bool ok = false;
+    dirty_update_many(&t, &b, 1, &ok);
+    return ok;
 }
 
 // Stage a host batch on the device for dirty_update.
@@ -1170,6 +1247,26 @@ mkv_status mkv_tree_upsert(mkv_tree *t, mkv_blob keys, mkv_blob values) {
     });
 }
 
+// Key-set change of a device batch: bring it to the host and take the general (merge/re-sort) path.
+static void upsert_device_general(mkv_tree *t, const mkv_blob &keys, const mkv_blob &values) {
+    if (t->sharded) throw Error(ST_ESTATE, "upsert of new keys on a sharded tree: rebuild the shard");
+    std::vector<uint64_t> ko(keys.n + 1), vo(keys.n + 1);
+    MKV_HIP(hipMemcpy(ko.data(), keys.offsets, ko.size() * 8, hipMemcpyDeviceToHost));
+    MKV_HIP(hipMemcpy(vo.data(), values.offsets, vo.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<uint8_t> kbh(ko.back() - ko[0] + 1), vbh(vo.back() - vo[0] + 1);
+    if (ko.back() > ko[0])
+        MKV_HIP(hipMemcpy(kbh.data(), keys.bytes + ko[0], ko.back() - ko[0], hipMemcpyDeviceToHost));
+    if (vo.back() > vo[0])
+        MKV_HIP(hipMemcpy(vbh.data(), values.bytes + vo[0], vo.back() - vo[0], hipMemcpyDeviceToHost));
+    const uint64_t k0 = ko[0], v0 = vo[0];
+    for (auto &x : ko) x -= k0;
+    for (auto &x : vo) x -= v0;
+    mkv_blob hk{kbh.data(), ko.data(), keys.n}, hv{vbh.data(), vo.data(), values.n};
+    check_blob(hk, "keys");
+    check_blob(hv, "values");
+    apply_batch(t, hk, &hv, nullptr);
+}
+
 mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
     MKV_TRY({
         NEED(t, "tree is null");
@@ -1180,23 +1277,34 @@ mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         if (keys.n == 0) return MKV_OK;
         NEED(!t->prepared, "shard_reduce pending");
         if (dirty_update(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n)) return MKV_OK;
-        if (t->sharded) throw Error(ST_ESTATE, "upsert of new keys on a sharded tree: rebuild the shard");
-        // key-set change: bring the batch to the host and take the general (re-sort) path
-        std::vector<uint64_t> ko(keys.n + 1), vo(keys.n + 1);
-        MKV_HIP(hipMemcpy(ko.data(), keys.offsets, ko.size() * 8, hipMemcpyDeviceToHost));
-        MKV_HIP(hipMemcpy(vo.data(), values.offsets, vo.size() * 8, hipMemcpyDeviceToHost));
-        std::vector<uint8_t> kbh(ko.back() - ko[0] + 1), vbh(vo.back() - vo[0] + 1);
-        if (ko.back() > ko[0])
-            MKV_HIP(hipMemcpy(kbh.data(), keys.bytes + ko[0], ko.back() - ko[0], hipMemcpyDeviceToHost));
-        if (vo.back() > vo[0])
-            MKV_HIP(hipMemcpy(vbh.data(), values.bytes + vo[0], vo.back() - vo[0], hipMemcpyDeviceToHost));
-        const uint64_t k0 = ko[0], v0 = vo[0];
-        for (auto &x : ko) x -= k0;
-        for (auto &x : vo) x -= v0;
-        mkv_blob hk{kbh.data(), ko.data(), keys.n}, hv{vbh.data(), vo.data(), values.n};
-        check_blob(hk, "keys");
-        check_blob(hv, "values");
-        apply_batch(t, hk, &hv, nullptr);
+        upsert_device_general(t, keys, values);
+    });
+}
+
+mkv_status mkv_tree_upsert_device_many(mkv_tree *const *trees, const mkv_blob *keys, const mkv_blob *values,
+                                       uint32_t k) {
+    MKV_TRY({
+        NEED(trees || k == 0, "null trees");
+        NEED((keys && values) || k == 0, "null batches");
+        for (uint32_t i = 0; i < k; ++i) {
+            NEED(trees[i], "tree is null");
+            NEED(keys[i].n == values[i].n, "keys.n != values.n");
+            NEED(keys[i].n < 0xFFFFFFF0ull, "too many records");
+            NEED(keys[i].n == 0 || (keys[i].offsets && values[i].offsets), "null offsets");
+            NEED(keys[i].n == 0 || !trees[i]->prepared, "shard_reduce pending");
+            for (uint32_t j = 0; j < i; ++j) NEED(trees[j] != trees[i], "a tree appears twice");
+        }
+        if (k == 0) return MKV_OK;
+        std::vector<DirtyBatch> bs(k);
+        for (uint32_t i = 0; i < k; ++i)
+            bs[i] = DirtyBatch{keys[i].bytes, keys[i].offsets, values[i].bytes, values[i].offsets, keys[i].n};
+        std::unique_ptr<bool[]> ok(new bool[k]);
+        dirty_update_many(trees, bs.data(), k, ok.get());
+        for (uint32_t i = 0; i < k; ++i) {
+            if (ok[i] || keys[i].n == 0) continue;
+            DevGuard g(trees[i]->dev);
+            upsert_device_general(trees[i], keys[i], values[i]);
+        }
     });
 }
 

@@ -210,6 +210,25 @@ class MerkleTree:
         self._cache.clear()
         check(lib().mkv_tree_upsert_device(self._h, Blob(kb_ptr, koff_ptr, n), Blob(vb_ptr, voff_ptr, n)))
 
+    @staticmethod
+    def upsert_device_many(trees, batches) -> None:
+        """upsert_device() on k distinct trees at once: batches[i] = (kb_ptr, koff_ptr, vb_ptr, voff_ptr, n)
+        for trees[i]. Replicas sharing a key set share the dirty climb (mkv_tree_upsert_device_many)."""
+        trees = list(trees)
+        batches = list(batches)
+        if len(trees) != len(batches):
+            raise ValueError("one batch per tree")
+        k = len(trees)
+        if k == 0:
+            return
+        for t in trees:
+            t._flush()
+            t._cache.clear()
+        hs = (C.c_void_p * k)(*[t._h.value for t in trees])
+        kbs = (Blob * k)(*[Blob(b[0], b[1], b[4]) for b in batches])
+        vbs = (Blob * k)(*[Blob(b[2], b[3], b[4]) for b in batches])
+        check(lib().mkv_tree_upsert_device_many(hs, kbs, vbs, k))
+
     def apply(self, keys, values, is_remove) -> None:
         """Mixed ordered batch: record i is remove(k_i) if is_remove[i] else insert(k_i, v_i)."""
         self._flush()

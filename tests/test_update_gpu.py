@@ -110,6 +110,53 @@ def test_upsert_device_dirty_and_fallback():
     assert _levels(t) == _oracle_levels(o)
 
 
+@pytest.mark.parametrize("n,m", [(20000, 300), (70001, 9000)])
+def test_upsert_device_many_matches_separate_calls(n, m):
+    """Batched dirty climb of several replicas (shared level plan) + a replica of another size (own
+    group) + one batch with a new key (general path) == separate upserts == oracle."""
+    import torch
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    rng = np.random.default_rng(m)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    small_n = n // 3
+    kbs, kos, vbs, vos = coracle.gen_records(DEFAULT_SEED, 0, small_n)
+    small = MerkleTree()
+    small.build((kbs, kos), (vbs, vos))
+    osmall = coracle.OracleTree.build(kbs, kos, vbs, vos)
+    trees = [base.clone() for _ in range(4)] + [small]
+    refs = [base.clone() for _ in range(4)] + [small.clone()]
+    batches, keep, expect = [], [], []
+    for r in range(5):
+        pool = keys if r < 4 else split_blob(kbs, kos)
+        idx = list(rng.integers(0, len(pool), size=m)) + [len(pool) - 1, 0]
+        ks = [pool[int(i)] for i in idx]
+        if r == 3:
+            ks.append(b"zz-new-key-%d" % r)  # key-set change: this tree leaves the group
+        vs = [b"many-%d-%d-%d" % (r, j, int(i)) for j, i in enumerate(idx)] + [b"nv"] * (len(ks) - len(idx))
+        bk, bo = pack(ks)
+        bv, bvo = pack(vs)
+        d = [torch.from_numpy(bk.copy()).cuda(), torch.from_numpy(bo.astype(np.int64)).cuda(),
+             torch.from_numpy(bv.copy()).cuda(), torch.from_numpy(bvo.astype(np.int64)).cuda()]
+        keep.append(d)
+        batches.append((d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), len(ks)))
+        expect.append((o if r < 4 else osmall).upsert(bk, bo, bv, bvo))
+    torch.cuda.synchronize()
+    MerkleTree.upsert_device_many(trees, batches)
+    for t, b in zip(refs, batches):
+        t.upsert_device(*b)
+    for r in range(5):
+        assert trees[r].get_root_hash() == expect[r].root() == refs[r].get_root_hash(), r
+        assert _levels(trees[r]) == _oracle_levels(expect[r]), r
+    # a second batched round on the same handles (bitmaps must be clean again)
+    MerkleTree.upsert_device_many(trees[:3], batches[:3])
+    for r in range(3):
+        refs[r].upsert_device(*batches[r])
+        assert trees[r].get_root_hash() == refs[r].get_root_hash(), r
+
+
 def _shard_trees(kb, ko, vb, vo, cuts):
     """Sorted records split at cuts -> prepared+reduced+combined shard trees."""
     keys, vals = split_blob(kb, ko), split_blob(vb, vo)
