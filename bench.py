@@ -368,9 +368,21 @@ def wl_diff(ctx, args):
         out = base_line(ctx, args, "Merkle diff keys/s (union keys compared, 2 replicas, 0.1% divergence)",
                         v["keys_per_s"], "keys/s", v["ms"], wl)
         achieved = DIFF_BYTES_PER_KEY * res["mixed"]["union_keys"] / (res["mixed"]["device_ms"] * 1e-3) / 1e9
+        # HBM bytes per merge-join diff from the PMC passes (scripts/prof_summary.py), same per-rank size only
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_diff_merge.json")
+        if os.path.exists(pmc_path):
+            try:
+                pm = json.load(open(pmc_path))
+                if pm.get("union_keys") == res["mixed"]["union_keys"] // ctx.world:
+                    traffic = pm.get("hbm_bytes_per_diff")
+            except Exception:
+                traffic = None
         out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "merge-join diff (mixed)",
-                           "bytes_per_union_key": DIFF_BYTES_PER_KEY}
+                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "merge-join diff (mixed)",
+                           "bytes_per_union_key": DIFF_BYTES_PER_KEY,
+                           "note": "achieved = 80 B x union keys / device time of the whole diff call (partition, "
+                                   "both passes, key gather); traffic = PMC HBM bytes of its merge-join kernels"}
         out["diff"] = res
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

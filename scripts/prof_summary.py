@@ -3,7 +3,8 @@
   <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   <tag>_pmc.json           per-kernel averages of every PMC counter collected + derived metrics
   pmc_leaf_hash.json       HBM bytes per k_leaf_hash launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction)
-Usage: python scripts/prof_summary.py <tag> [n_records]
+  pmc_diff_merge.json      HBM bytes per merge-join diff (sum over its kernels), when k_diff_pass1 ran
+Usage: python scripts/prof_summary.py <tag> [n_records] [prof_dir under gpurun_out/]
 """
 import collections
 import csv
@@ -15,6 +16,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "gpurun_out", "prof")
+# the kernels of one merge-join diff (k_diff.hip launch_diff_merge); key gathers excluded (output side)
+MERGE_KERNELS = ("k_diff_partition", "k_diff_partition_fine", "k_diff_pass1", "k_widen_u32", "k_diff_pass2")
 OUT = os.path.join(ROOT, "profiles")
 
 
@@ -24,8 +27,11 @@ def kname(s):
 
 
 def main():
+    global PROF
     tag = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000_000
+    if len(sys.argv) > 3:
+        PROF = os.path.join(ROOT, "gpurun_out", sys.argv[3])
     os.makedirs(OUT, exist_ok=True)
     stats = os.path.join(PROF, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(OUT, f"{tag}_kernel_stats.csv"))
@@ -58,6 +64,13 @@ def main():
                    "algorithmic_bytes_per_launch": 172 * n,
                    "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes"},
                   open(os.path.join(OUT, "pmc_leaf_hash.json"), "w"), indent=1)
+    if all(k in summary and "hbm_bytes_corrected" in summary[k] for k in MERGE_KERNELS):
+        per = {k: summary[k]["hbm_bytes_corrected"] for k in MERGE_KERNELS}
+        json.dump({"union_keys": n, "hbm_bytes_per_diff": sum(per.values()), "per_kernel": per,
+                   "source": f"{tag}_pmc.json", "algorithmic_bytes_per_diff": 80 * n,
+                   "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes, summed over "
+                           "the merge-join kernels of one diff"},
+                  open(os.path.join(OUT, "pmc_diff_merge.json"), "w"), indent=1)
     for k in sorted(summary, key=lambda k: -summary[k].get("avg_duration_us", 0))[:8]:
         e = summary[k]
         print(f"{k:24s} {e['avg_duration_us']:9.1f} us  valu_busy={e.get('valu_busy_frac', 0):.2f} "
