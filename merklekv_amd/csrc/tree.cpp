@@ -117,6 +117,8 @@ struct mkv_tree {
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
+    DevBuf td_bm, td_bc;            // divergent-position bitmap (all-zero between calls) + block counts
+    uint64_t td_bm_words = 0;       // words of td_bm known to be zero
     DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
     DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
     DevBuf w_scan, w_gets, w_nl1, w_nl2, w_scr, w_ks, w_kl, w_vs, w_vl, w_found, w_rank;  // wire ingestion
@@ -172,6 +174,100 @@ __global__ void k_widen_positions(const uint32_t *__restrict__ f, uint64_t m, ui
         v[i] = (uint32_t)i;
     }
 }
+// Divergent leaf positions in ascending order without a sort (top-down diff): one bit per leaf in a
+// bitmap that is all-zero between calls; per-block popcounts over POS_BLOCK_WORDS words; each emitting
+// block finds its output base by summing the counts of the blocks before it (at most a few thousand
+// u32, L2-resident), scans its own words and writes the positions, clearing the words it read.
+constexpr uint32_t POS_BLOCK_WORDS = 1024;  // 256 threads x 4 words
+constexpr uint64_t POS_MAX_BLOCKS = 8192;   // beyond this the O(blocks^2) base sums lose to the sort
+
+__global__ void k_pos_setbits(const uint32_t *__restrict__ f, uint64_t m, uint32_t *__restrict__ bm) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) {
+        const uint32_t p = f[i];
+        atomicOr(bm + (p >> 5), 1u << (p & 31));
+    }
+}
+
+__device__ __forceinline__ uint4 pos_words(const uint32_t *bm, uint64_t w0, uint64_t words) {
+    if (w0 + 3 < words) return *reinterpret_cast<const uint4 *>(bm + w0);
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (w0 < words) x.x = bm[w0];
+    if (w0 + 1 < words) x.y = bm[w0 + 1];
+    if (w0 + 2 < words) x.z = bm[w0 + 2];
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    return v;
+}
+
+__global__ __launch_bounds__(256) void k_pos_count(const uint32_t *__restrict__ bm, uint64_t words,
+                                                   uint32_t *__restrict__ bc) {
+    __shared__ uint32_t red[4];
+    const uint64_t w0 = (uint64_t)blockIdx.x * POS_BLOCK_WORDS + 4 * threadIdx.x;
+    const uint4 x = pos_words(bm, w0, words);
+    const uint32_t c = wave_sum(__popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void k_pos_emit(uint32_t *__restrict__ bm, uint64_t words,
+                                                  const uint32_t *__restrict__ bc, uint64_t *__restrict__ out) {
+    __shared__ uint32_t base_w[4], tot_w[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) s += bc[i];
+    s = wave_sum(s);
+    const uint64_t w0 = (uint64_t)blockIdx.x * POS_BLOCK_WORDS + 4 * threadIdx.x;
+    const uint4 x = pos_words(bm, w0, words);
+    const uint32_t c = __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    uint32_t v = c;  // inclusive scan over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d);
+        if (lane >= (uint32_t)d) v += y;
+    }
+    if (lane == 0) base_w[wave] = s;
+    if (lane == 63) tot_w[wave] = v;
+    __syncthreads();
+    uint64_t o = (uint64_t)base_w[0] + base_w[1] + base_w[2] + base_w[3] + (v - c);
+    for (uint32_t w = 0; w < wave; ++w) o += tot_w[w];
+    if (!c) return;
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t b = xs[q];
+        while (b) {
+            out[o++] = (w0 + q) * 32 + (uint32_t)(__ffs(b) - 1);
+            b &= b - 1;
+        }
+    }
+    if (w0 + 3 < words) {
+        *reinterpret_cast<uint4 *>(bm + w0) = make_uint4(0, 0, 0, 0);
+    } else {
+        for (int q = 0; q < 4; ++q)
+            if (w0 + q < words) bm[w0 + q] = 0;
+    }
+}
+
+// m unique positions < n (u32 frontier) -> ascending u64 in `out`. bm: ceil(n/32) zero words
+// (left zero); bc: one u32 per block. False when n is too large for this path (caller sorts).
+bool positions_sorted_bitmap(const uint32_t *f, uint64_t m, uint64_t n, uint32_t *bm, uint32_t *bc, uint64_t *out,
+                             hipStream_t st) {
+    const uint64_t words = (n + 31) / 32, nb = ceil_div(words, POS_BLOCK_WORDS);
+    if (nb > POS_MAX_BLOCKS) return false;
+    if (!m) return true;
+    hipLaunchKernelGGL(k_pos_setbits, dim3((uint32_t)ceil_div(m, 256)), dim3(256), 0, st, f, m, bm);
+    hipLaunchKernelGGL(k_pos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
+    hipLaunchKernelGGL(k_pos_emit, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc, out);
+    MKV_LAUNCH_CHECK();
+    return true;
+}
+
 __global__ void k_narrow_u64(const uint64_t *__restrict__ k, uint64_t m, uint32_t *__restrict__ f) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) f[i] = (uint32_t)k[i];
@@ -267,6 +363,16 @@ uint32_t d2h_u32(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
     MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     wait_stream(t, s);
     return reinterpret_cast<uint32_t *>(t->h_small)[0];
+}
+
+// `words` u32 starting at dptr in one round trip (h_small holds 64); the walk reads its level counters
+// and the key-set screen together this way instead of one wake-up per scalar.
+const uint32_t *d2h_u32s(mkv_tree *t, const void *dptr, uint32_t words, hipStream_t s = nullptr) {
+    if (!s) s = t->st;
+    if (words > 64) throw std::runtime_error("d2h_u32s: more than 64 words");
+    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, 4ull * words, hipMemcpyDeviceToHost, s));
+    wait_stream(t, s);
+    return reinterpret_cast<const uint32_t *>(t->h_small);
 }
 
 int bits_for(uint64_t m) {
@@ -1477,8 +1583,9 @@ static std::vector<size_t> jump_targets(size_t L) {
 // roots (the root, or a shard's fringe roots). Returns false (caller falls back to the merge-join)
 // when a divergent leaf position holds different keys, i.e. the key sets differ there.
 static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, const DiffSide &A, const DiffSide &B,
-                         uint64_t *refs, uint64_t *m_out) {
+                         uint64_t *refs, uint64_t *m_out, const uint32_t **nbad_out) {
     *m_out = 0;
+    *nbad_out = nullptr;
     const bool roots_valid = !a->combine_pending && !b->combine_pending && a->has_root && b->has_root;
     if (roots_valid && std::memcmp(a->root, b->root, 32) == 0) return true;  // equal roots: identical leaves
     const size_t L = a->lev_S.size();
@@ -1487,8 +1594,10 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 2);
     uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2);  // cnt[l]: frontier size at level l; cnt[L] = 0 (seed)
     MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
+    // Key-set screen: cnt[L + 1] counts sampled positions whose prefixes differ. It is read together
+    // with the first frontier count the walk reads back (level 4, or the leaf count of a small tree),
+    // so a clean screen costs no round trip of its own; a failed one aborts the walk there.
     launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
-    if (d2h_u32(t, cnt + L + 1) != 0) return false;  // key sets differ: straight to the merge-join
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
     if (!a->sharded && !b->sharded && L > 1 && jumps_enabled()) {
@@ -1505,8 +1614,8 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
                                 cnt + lt, std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
             std::swap(fin, fout);
             if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
-                const uint64_t c = d2h_u32(t, cnt + lt);
-                if (2 * c > a->lev_cnt[lt]) return false;
+                const uint32_t *h = d2h_u32s(t, cnt, (uint32_t)L + 2);
+                if (h[L + 1] != 0 || 2 * (uint64_t)h[lt] > a->lev_cnt[lt]) return false;
             }
         }
     } else
@@ -1522,22 +1631,38 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
         // ~1.6 % of them) stops such a walk before the expensive bottom levels; the merge-join is exact
         // for any key sets.
         if (l - 1 == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
-            const uint64_t c = d2h_u32(t, cnt + (l - 1));
-            if (2 * c > a->lev_cnt[l - 1]) return false;
+            const uint32_t *h = d2h_u32s(t, cnt, (uint32_t)L + 2);
+            if (h[L + 1] != 0 || 2 * (uint64_t)h[l - 1] > a->lev_cnt[l - 1]) return false;
         }
     }
-    const uint64_t m = d2h_u32(t, cnt);
+    const uint32_t *h = d2h_u32s(t, cnt, (uint32_t)L + 2);
+    if (h[L + 1] != 0) return false;  // key sets differ (screen): the merge-join is exact
+    const uint64_t m = h[0];
+    *nbad_out = cnt + L + 1;  // zero here; k_topdown_leaves counts key mismatches into it
     if (m) {
         // divergent leaf positions -> sorted u64 (they are appended in no particular order)
-        uint64_t *k1 = ens<uint64_t>(t->td_k1, m + 1), *k2 = ens<uint64_t>(t->td_k2, m + 1);
-        uint32_t *v1 = ens<uint32_t>(t->td_v1, m + 1), *v2 = ens<uint32_t>(t->td_v2, m + 1);
-        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
-        launch_widen_positions(fin, m, k1, v1, t->st);
-        const bool sw = radix_sort_pairs(k1, v1, k2, v2, m, 0, std::max(8, bits_for(n)), radix, t->st);
-        const uint64_t *pos = sw ? k2 : k1;
-        uint32_t *nbad = cnt + L + 1;
-        launch_topdown_leaves(pos, m, A, B, refs, nbad, t->st);
-        if (d2h_u32(t, nbad) != 0) return false;
+        uint64_t *k1 = ens<uint64_t>(t->td_k1, m + 1);
+        const uint64_t *pos = k1;
+        const uint64_t words = (n + 31) / 32;
+        uint32_t *bm = ens<uint32_t>(t->td_bm, words + 4);
+        uint32_t *bc = ens<uint32_t>(t->td_bc, ceil_div(words, 1024) + 1);
+        if (t->td_bm_words < words) {
+            MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
+            t->td_bm_words = words;
+        }
+        t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
+        if (positions_sorted_bitmap(fin, m, n, bm, bc, k1, t->st)) {
+            t->td_bm_words = words;
+        } else {
+            uint64_t *k2 = ens<uint64_t>(t->td_k2, m + 1);
+            uint32_t *v1 = ens<uint32_t>(t->td_v1, m + 1), *v2 = ens<uint32_t>(t->td_v2, m + 1);
+            void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
+            launch_widen_positions(fin, m, k1, v1, t->st);
+            const bool sw = radix_sort_pairs(k1, v1, k2, v2, m, 0, std::max(8, bits_for(n)), radix, t->st);
+            pos = sw ? k2 : k1;
+        }
+        // mismatching keys (nbad != 0) are read back with the key list's byte count (keylist_from_refs)
+        launch_topdown_leaves(pos, m, A, B, refs, cnt + L + 1, t->st);
     }
     *m_out = m;
     return true;
@@ -1554,9 +1679,10 @@ static DiffSide side_of(const mkv_tree *t) {
     return s;
 }
 
-// Key list of the refs (bit 63 = side B) gathered on the device and copied to the host.
+// Key list of the refs (bit 63 = side B) gathered on the device and copied to the host. `reject`
+// (optional device u32) is read back together with the byte count: nonzero -> nullptr, nothing copied.
 static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A,
-                                      const DiffSide &B) {
+                                      const DiffSide &B, const uint32_t *reject = nullptr) {
     auto *l = new mkv_keylist();
     try {
         if (m) {
@@ -1567,7 +1693,15 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
             launch_diff_keylens(refs, m, A, B, lens, t->st);
             exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
             prof_end(t, pk);
-            const uint64_t bytes = d2h_u64(t, off + m);
+            MKV_HIP(hipMemcpyAsync(t->h_small, off + m, 8, hipMemcpyDeviceToHost, t->st));
+            if (reject) MKV_HIP(hipMemcpyAsync(t->h_small + 1, reject, 4, hipMemcpyDeviceToHost, t->st));
+            wait_stream(t, t->st);
+            const uint64_t bytes = t->h_small[0];
+            if (reject && reinterpret_cast<const uint32_t *>(t->h_small + 1)[0] != 0) {
+                sync(t);
+                delete l;
+                return nullptr;
+            }
             uint8_t *ob = ens<uint8_t>(t->d_out, bytes + 16);
             launch_diff_keys(refs, m, A, B, off, ob, t->st);
             keylist_fill(t, l, off, ob, m, bytes);
@@ -1592,8 +1726,16 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     if (A.n > 0 && same_plan(a, b) && topdown_enabled()) {
         // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
         size_t pd = prof_begin(t, "diff");
-        done = topdown_diff(t, a, b, A, B, refs, &m);
+        const uint32_t *nbad = nullptr;
+        done = topdown_diff(t, a, b, A, B, refs, &m, &nbad);
         prof_end(t, pd);
+        if (done) {
+            // the leaf-key check (nbad) comes back with the key list's byte count
+            mkv_keylist *l = keylist_from_refs(t, refs, m, A, B, nbad);
+            if (l) return l;
+            m = 0;  // a divergent position holds different keys: the key sets differ
+            done = false;
+        }
     }
     if (!done) {
         size_t pd = prof_begin(t, "diff");

@@ -58,7 +58,8 @@ def main():
         summary[k] = e
     json.dump(summary, open(os.path.join(OUT, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
     lh = summary.get("k_leaf_persist") or summary.get("k_leaf_hash")
-    if lh and "hbm_bytes_corrected" in lh:
+    diff_run = "k_diff_pass1" in summary  # the diff workload also builds trees: keep the build's leaf figure
+    if lh and "hbm_bytes_corrected" in lh and not diff_run:
         json.dump({"n": n, "hbm_bytes_per_launch": lh["hbm_bytes_corrected"], "source": f"{tag}_pmc.json",
                    "kernel": "k_leaf_persist" if "k_leaf_persist" in summary else "k_leaf_hash",
                    "algorithmic_bytes_per_launch": 172 * n,

@@ -367,6 +367,30 @@ def test_topdown_value_only_vs_oracle(oracle_lib, n, stride):
     assert b.diff_keys_bytes(a) == want
 
 
+def test_topdown_positions_across_bitmap_blocks(oracle_lib):
+    """Divergent leaves at chosen sorted positions: word / uint4 / 32768-leaf block edges, a dense run
+    and the last leaf (the sorted-position compaction of the walk); repeated diffs on one handle, then a
+    larger tree diffed by the same handle (the position bitmap must come back zero every time)."""
+    a = MerkleTree()
+    for n, seed in ((70_001, 21), (70_001, 22), (140_003, 23)):
+        kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED + seed, 0, n)
+        order = np.lexsort(kb.reshape(n, 32).T[::-1])  # input index of each sorted position
+        pos = {0, 1, 31, 32, 127, 128, 129, 32767, 32768, 32769, 65535, n - 2, n - 1} | set(range(40_000, 40_200))
+        vb2 = vb.copy().reshape(n, 100)
+        vb2[order[sorted(pos)], 7] ^= 1
+        vb2 = vb2.reshape(-1)
+        b = MerkleTree()
+        a.build((kb, ko), (vb, vo))
+        b.build((kb, ko), (vb2, vo))
+        oa = oracle_lib.OracleTree.build(kb, ko, vb, vo)
+        ob = oracle_lib.OracleTree.build(kb, ko, vb2, vo)
+        want = oa.diff(ob)
+        assert len(want) == len(pos)
+        for _ in range(2):
+            assert a.diff_keys_bytes(b) == want
+        assert b.diff_keys_bytes(a) == want
+
+
 def test_topdown_equal_count_key_swap_falls_back(oracle_lib):
     """Same leaf count but different key sets: divergent positions hold different keys -> merge-join."""
     n = 10_000
