@@ -328,13 +328,18 @@ void prof_collect(mkv_tree *t) {
 
 // Low-latency wait: poll an event recorded on the stream instead of the runtime's blocking sync
 // (tens of microseconds of wake-up latency per scalar readback otherwise).
-void wait_stream(mkv_tree *t, hipStream_t s) {
-    MKV_HIP(hipEventRecord(t->ev_wait, s));
+// Spin on hipStreamQuery: no marker command is queued, so an already idle stream returns at once
+// (measured end to end it matches the earlier record-an-event-and-poll wait; kept for its simplicity).
+void wait_idle(hipStream_t s) {
     for (;;) {
-        hipError_t e = hipEventQuery(t->ev_wait);
+        hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) return;
         if (e != hipErrorNotReady) MKV_HIP(e);
     }
+}
+void wait_stream(mkv_tree *t, hipStream_t s) {
+    (void)t;
+    wait_idle(s);
 }
 
 // Full completion point of an API call: both streams drained, profiling pairs collected.
@@ -1717,7 +1722,7 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
 static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     mkv_tree *t = const_cast<mkv_tree *>(a);
     // b's last work must be complete before a's stream reads it
-    MKV_HIP(hipStreamSynchronize(b->st));
+    wait_idle(b->st);
     DiffSide A = side_of(a), B = side_of(b);
     const uint64_t M = A.n + B.n;
     uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
@@ -1873,7 +1878,7 @@ mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, 
         DevGuard g(t->dev);
         std::vector<mkv_keylist *> res(k, nullptr);
         try {
-            for (uint32_t i = 0; i < k; ++i) MKV_HIP(hipStreamSynchronize(others[i]->st));
+            for (uint32_t i = 0; i < k; ++i) wait_idle(others[i]->st);
             // candidates for the shared walk: same level plan and a clean key-set screen
             std::vector<uint32_t> cand;
             if (a->n > 0 && topdown_enabled()) {

@@ -9,3 +9,5 @@ timeout -k 10 400 python bench.py --workload diff --steps 10 --warmup 2 > gpurun
 cat gpurun_out/bench_diff.json
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
+timeout -k 10 400 python bench.py --workload incremental --steps 10 --warmup 3 > gpurun_out/bench_inc.json 2> gpurun_out/bench_inc.err || { tail -20 gpurun_out/bench_inc.err; exit 1; }
+cat gpurun_out/bench_inc.json
