@@ -43,6 +43,31 @@ __device__ __forceinline__ int cmp_ab(const DiffSide &A, uint64_t i, uint64_t pa
     return key_cmp(ka, la, pa, kb, lb, pb);
 }
 
+// Equal keys at sorted position i of both trees (the top-down leaf check). Prefixes and permutation
+// entries of both sides load together, then both offset pairs, then every key word beyond the prefix
+// at once (aligned keys up to 64 B), so a check is three dependent memory round trips; cmp_ab's
+// chunk loop pays one per 8 bytes. Equal 8-byte prefixes + equal lengths = equal first 8 bytes.
+__device__ __forceinline__ bool key_eq_at(const DiffSide &A, const DiffSide &B, uint64_t i) {
+    const uint64_t pa = A.pfx[i], pb = B.pfx[i];
+    const uint32_t oa = A.perm[i], ob = B.perm[i];
+    const uint64_t a0 = A.koff[oa], a1 = A.koff[oa + 1], b0 = B.koff[ob], b1 = B.koff[ob + 1];
+    const uint64_t len = a1 - a0;
+    if (pa != pb || len != b1 - b0) return false;
+    if (len <= 8) return true;
+    const uint8_t *ka = A.kb + a0, *kb = B.kb + b0;
+    if (((a0 | b0) & 3) == 0 && len <= 64) {
+        const uint32_t *wa = reinterpret_cast<const uint32_t *>(ka), *wb = reinterpret_cast<const uint32_t *>(kb);
+        const uint32_t nw = (uint32_t)(len >> 2);
+        bool eq = true;
+#pragma unroll
+        for (uint32_t q = 2; q < 16; ++q)
+            if (q < nw) eq &= wa[q] == wb[q];
+        for (uint64_t x = (uint64_t)nw * 4; x < len; ++x) eq &= ka[x] == kb[x];
+        return eq;
+    }
+    return key_cmp(ka, len, pa, kb, len, pb) == 0;
+}
+
 __device__ __forceinline__ bool digest_eq(const uint8_t *a, const uint8_t *b) {
     const uint4 *x = reinterpret_cast<const uint4 *>(a);
     const uint4 *y = reinterpret_cast<const uint4 *>(b);
@@ -680,7 +705,7 @@ __global__ void k_topdown_leaves_batch(const uint64_t *__restrict__ ent, uint64_
     const DiffSide B = Bs[v];
     refs[k] = i;
     if (k == 0 || (uint32_t)(ent[k - 1] >> pb) != v) count[v] = (uint32_t)k;  // segment start of variant v
-    if (cmp_ab(A, i, A.pfx[i], B, i, B.pfx[i]) != 0) atomicAdd(&nbad[v], 1u);
+    if (!key_eq_at(A, B, i)) atomicAdd(&nbad[v], 1u);
 }
 
 // Divergent leaf positions (sorted): refs of keys equal on both sides; counts positions whose keys
@@ -690,7 +715,7 @@ __global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, D
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
     const uint64_t i = pos[k];
-    const bool same = cmp_ab(A, i, A.pfx[i], B, i, B.pfx[i]) == 0;
+    const bool same = key_eq_at(A, B, i);
     refs[k] = i;
     if (!same) atomicAdd(nbad, 1u);
 }

@@ -410,6 +410,29 @@ def test_topdown_equal_count_key_swap_falls_back(oracle_lib):
     assert b.diff_keys_bytes(a) == ob.diff(oa)
 
 
+@pytest.mark.parametrize("klen", [12, 37, 60, 64, 90])
+def test_topdown_key_tail_change_falls_back(klen):
+    """Equal counts and 8-byte prefixes; one key differs only in its last byte (aligned and unaligned
+    key storage, keys up to and beyond the 64-byte batched compare): the leaf check must see it."""
+    rng = random.Random(klen)
+    n = 3000
+    keys = [bytes(rng.choice(b"abcdefgh") for _ in range(klen)) for _ in range(n)]
+    keys = sorted(set(keys))
+    vals = [b"v%d" % i for i in range(len(keys))]
+    keys2 = list(keys)
+    j = len(keys) // 2
+    keys2[j] = keys2[j][:-1] + (b"z" if keys2[j][-1:] != b"z" else b"y")
+    assert keys2[j] not in set(keys)
+    vals2 = list(vals)
+    vals2[7] = b"changed"
+    a, b = MerkleTree(), MerkleTree()
+    a.build(keys, vals)
+    b.build(keys2, vals2)
+    want = sorted({keys[7], keys[j], keys2[j]})
+    assert a.diff_keys_bytes(b) == want
+    assert b.diff_keys_bytes(a) == want
+
+
 def test_topdown_identical_trees_empty():
     kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 5000)
     a, b = MerkleTree(), MerkleTree()
