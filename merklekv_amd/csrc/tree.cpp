@@ -69,9 +69,23 @@ struct PinnedBlock {
     PinnedBlock(const PinnedBlock &) = delete;
     PinnedBlock &operator=(const PinnedBlock &) = delete;
     ~PinnedBlock() {
+        // A full pool keeps its largest blocks: small ones left by earlier calls (level views, short
+        // key lists) must not force every large diff result through hipHostMalloc/hipHostFree, whose
+        // page (un)pinning costs milliseconds.
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (g_pool.size() < 8) g_pool.emplace_back(p, cap);
-        else (void)hipHostFree(p);
+        if (g_pool.size() < 16) {
+            g_pool.emplace_back(p, cap);
+            return;
+        }
+        size_t small = 0;
+        for (size_t i = 1; i < g_pool.size(); ++i)
+            if (g_pool[i].second < g_pool[small].second) small = i;
+        uint8_t *victim = p;
+        if (g_pool[small].second < cap) {
+            victim = g_pool[small].first;
+            g_pool[small] = {p, cap};
+        }
+        (void)hipHostFree(victim);
     }
 };
 }  // namespace
