@@ -267,19 +267,32 @@ template <class T> void scan_impl(const T *in, T *out, uint64_t n, T *total, voi
 }
 
 // ---- ties / refinement ----
+// tie[i] = prefix of i equals prefix of i-1 (count[0] += ties). Run heads (positions starting a tie
+// run) are appended to heads[] (wave-aggregated, count[1] = number of heads), so the refinement visits
+// only the runs instead of scanning all n flags.
 __global__ void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, int shift, uint8_t *__restrict__ tie,
-                            uint32_t *__restrict__ count) {
+                            uint32_t *__restrict__ count, uint32_t *__restrict__ heads) {
     sort_prio();
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool t = false;
+    bool t = false, h = false;
     if (i < n) {
-        t = i > 0 && (pfx[i] >> shift) == (pfx[i - 1] >> shift);
+        const uint64_t p = pfx[i] >> shift;
+        t = i > 0 && p == (pfx[i - 1] >> shift);
+        h = !t && i + 1 < n && (pfx[i + 1] >> shift) == p;
         tie[i] = t;
     } else if (i == n) {
         tie[n] = 0;
     }
-    uint64_t m = __ballot(t);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (uint32_t)__popcll(m));
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t m = __ballot(t);
+    if (lane == 0 && m) atomicAdd(&count[0], (uint32_t)__popcll(m));
+    const uint64_t hm = __ballot(h);
+    if (hm) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&count[1], (uint32_t)__popcll(hm));
+        base = __shfl(base, 0);
+        if (h) heads[base + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    }
 }
 
 __global__ void k_active_flags(const uint8_t *__restrict__ tie, uint64_t n, uint32_t *__restrict__ flags) {
@@ -355,9 +368,12 @@ constexpr uint32_t RS_SMALL_RUN = 16;
 __global__ __launch_bounds__(256) void k_refine_small(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                      uint64_t n, uint32_t *__restrict__ perm,
                                                      uint64_t *__restrict__ pfx, uint8_t *__restrict__ tie,
-                                                     uint32_t *__restrict__ count) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || tie[i] || !tie[i + 1]) return;  // run heads only
+                                                     uint32_t *__restrict__ count,
+                                                     const uint32_t *__restrict__ heads,
+                                                     const uint32_t *__restrict__ nheads) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *nheads) return;
+    const uint64_t i = heads[t];  // a run head: tie[i] == 0, tie[i + 1] == 1
     uint64_t j = i + 1;
     while (j < n && tie[j] && j - i <= RS_SMALL_RUN) ++j;
     if (j - i > RS_SMALL_RUN) {
@@ -613,14 +629,17 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
     scan_impl<uint64_t>(in, out, n, total, scratch, st);
 }
 
-void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st, int shift) {
-    hipLaunchKernelGGL(k_mark_ties, grid1d(n + 1), dim3(256), 0, st, pfx, n, shift, tie, count);
+void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, uint32_t *heads,
+                      hipStream_t st, int shift) {
+    hipLaunchKernelGGL(k_mark_ties, grid1d(n + 1), dim3(256), 0, st, pfx, n, shift, tie, count, heads);
     MKV_LAUNCH_CHECK();
 }
 void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint64_t *pfx,
-                         uint8_t *tie, uint32_t *count, hipStream_t st) {
-    if (!n) return;
-    hipLaunchKernelGGL(k_refine_small, grid1d(n), dim3(256), 0, st, kb, koff, n, perm, pfx, tie, count);
+                         uint8_t *tie, uint32_t *count, const uint32_t *heads, const uint32_t *nheads,
+                         uint64_t max_heads, hipStream_t st) {
+    if (!n || !max_heads) return;
+    hipLaunchKernelGGL(k_refine_small, grid1d(max_heads), dim3(256), 0, st, kb, koff, n, perm, pfx, tie, count, heads,
+                       nheads);
     MKV_LAUNCH_CHECK();
 }
 void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *kb, const uint64_t *koff,

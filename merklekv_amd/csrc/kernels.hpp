@@ -26,10 +26,11 @@ void exclusive_scan_u32(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t 
 void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t *total, void *scratch,
                         hipStream_t st);
 
-// tie[i] = (pfx[i] == pfx[i-1]) for i>0, tie[0] = 0; *count += number of ties. tie has n+1 entries
-// (tie[n] = 0 sentinel).
-void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, hipStream_t st,
-                      int shift = 0);
+// tie[i] = (pfx[i] == pfx[i-1]) for i>0, tie[0] = 0; count[0] += number of ties. tie has n+1 entries
+// (tie[n] = 0 sentinel). Tie-run heads (tie[i] == 0, tie[i+1] == 1) go to heads[] (capacity n / 2 + 1,
+// any order), count[1] += their number.
+void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, uint32_t *heads,
+                      hipStream_t st, int shift = 0);
 // Adaptive prefix sort (tree builds): one histogram read gives all eight byte-digit histograms
 // (counts[p*256+d], p = 0 the least significant byte) in `scratch`; the host then picks the digits
 // worth a pass (radix_prefix_passes: bit p of digit_mask = sort on byte p). Digits below the chosen
@@ -39,8 +40,10 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
                          void *scratch, hipStream_t st);
 // Orders every tie run of <= 16 positions on the full key in place (one thread per run); tie[] becomes
 // full-key equality there. count[0] += duplicate positions, count[1] += longer runs (left as they are).
+// Visits only the *nheads run heads of launch_mark_ties (max_heads: a host-side upper bound on *nheads).
 void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint64_t *pfx,
-                         uint8_t *tie, uint32_t *count, hipStream_t st);
+                         uint8_t *tie, uint32_t *count, const uint32_t *heads, const uint32_t *nheads,
+                         uint64_t max_heads, hipStream_t st);
 // pfx[pos[k]] = 8-byte prefix of sorted key pos[k] (after a refinement that re-ordered tie runs).
 void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *kb, const uint64_t *koff,
                     uint64_t *pfx, hipStream_t st);

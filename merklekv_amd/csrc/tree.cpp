@@ -554,7 +554,12 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
 // rare (~n/256 for independent bytes) and the tie refinement orders them on the full key. Constant
 // digits carry no order and are skipped. Returns the digit mask; *lo_bit = lowest sorted bit.
 uint32_t choose_prefix_digits(const uint32_t *counts, uint64_t n, int *lo_bit) {
-    const double need = std::log2((double)(n > 1 ? n : 2)) + 8.0;
+    // margin bits beyond log2(n): fewer radix passes vs more prefix ties for the refinement
+    static const double margin = [] {
+        const char *e = getenv("MKV_SORT_MARGIN");
+        return e ? atof(e) : 8.0;
+    }();
+    const double need = std::log2((double)(n > 1 ? n : 2)) + margin;
     double cum = 0;
     int p0 = 0;
     uint32_t mask = 0;
@@ -616,8 +621,10 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     DevBuf *pmbuf = sw ? &t->s_v2 : &t->s_v1, *pmalt = sw ? &t->s_v1 : &t->s_v2;
     uint64_t *pk = pkbuf->as<uint64_t>();
     uint32_t *perm = pmbuf->as<uint32_t>();
-    MKV_HIP(hipMemsetAsync(misc, 0, 4, st));
-    launch_mark_ties(pk, n_in, tie, misc, st, lo_bit);
+    // run heads into the dedup flag scratch (free until the dedup below), their count in misc[1]
+    uint32_t *heads = ens<uint32_t>(t->s_flags, n_in + 1);
+    MKV_HIP(hipMemsetAsync(misc, 0, 8, st));
+    launch_mark_ties(pk, n_in, tie, misc, heads, st, lo_bit);
     prof_end(t, ps);
     const uint32_t nties = n_in ? d2h_u32(t, misc, st) : 0;
     bool dedup = false;
@@ -626,7 +633,8 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         // short tie runs: one in-place pass; longer ones: the general chunk-by-chunk refinement, which
         // reorders perm (and, when chunk 0 was sorted only in part, pk) inside tie runs only
         MKV_HIP(hipMemsetAsync(misc + 4, 0, 8, st));
-        launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, st);
+        // every run head is followed by >= 1 tie, so heads <= nties
+        launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, heads, misc + 1, nties, st);
         MKV_HIP(hipMemcpyAsync(t->h_small, misc + 4, 8, hipMemcpyDeviceToHost, st));
         wait_stream(t, st);
         const uint32_t dups = reinterpret_cast<uint32_t *>(t->h_small)[0];

@@ -144,6 +144,25 @@ def test_long_common_prefixes_refinement(oracle_lib):
     _check_pairs(oracle_lib, pairs)
 
 
+def test_many_tie_runs_heads_list(oracle_lib):
+    """Thousands of 8-byte-prefix tie runs (sizes 2..40 around the 16-position short-run limit, first and
+    last sorted positions included, duplicates inside runs): the refinement visits runs through the
+    head list k_mark_ties appends in arbitrary order."""
+    rng = random.Random(23)
+    pairs = []
+    for g in range(2500):
+        size = rng.choice([1, 2, 3, 5, 15, 16, 17, 40])
+        head = b"g%07d" % g  # exactly 8 bytes: the whole sorted prefix is shared by the run
+        for _ in range(size):
+            suffix = rng.choice([b"", b"\x00", b"x", b"%d" % rng.randrange(30), b"\xff\xfe"])
+            pairs.append((head + suffix, b"v%d" % rng.randrange(10 ** 6)))
+    pairs.append((b"", b"first"))  # a run-free position 0
+    pairs.append((b"\xff" * 8 + b"a", b"z1"))  # a run at the last sorted positions
+    pairs.append((b"\xff" * 8 + b"b", b"z2"))
+    rng.shuffle(pairs)
+    _check_pairs(oracle_lib, pairs)
+
+
 def test_prefix_of_other_key_order(oracle_lib):
     """Rust str Ord: a proper prefix sorts first; zero bytes vs end of string (R3)."""
     ks = [b"ab", b"ab\x00", b"ab\x00\x00", b"ab\x01", b"a", b"", b"abcdefgh", b"abcdefgh\x00", b"abcdefg",
