@@ -59,6 +59,13 @@ mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values);
  * with offsets[n] inside the allocation — they are trusted, not validated. */
 mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values);
 
+/* A tree from shipped (key, leaf digest) pairs: digests = n x 32 bytes, digest i = SHA-256(R1 encoding
+ * of key i and its value) as the peer computed it (merkle.rs:45-49). Same result as mkv_tree_build over
+ * the original records (duplicates: last wins), without the values and without Kernel A. This is the
+ * anti-entropy fallback when key sets differ: SyncManager ships a peer's snapshot (sync.rs:122-143); a
+ * peer that serves its leaves() (merkle.rs:133-138) lets the requester diff on the device. */
+mkv_status mkv_tree_build_digests(mkv_tree *t, mkv_blob keys, const uint8_t *digests);
+
 /* SyncManager::build_remote_merkle_snapshot (sync.rs:122-143) straight from the wire bytes: scan = the
  * SCAN response ("KEYS <n>\r\n" + n key lines, server.rs:580-587), gets = the n GET responses in key order
  * concatenated ("VALUE <v>\r\n" or "NOT_FOUND\r\n", server.rs:551-552). Parsed on the device with the
@@ -126,6 +133,12 @@ mkv_status mkv_tree_keys_at(const mkv_tree *t, const uint64_t *pos, uint64_t m, 
 mkv_status mkv_tree_prefix_root(const mkv_tree *t, const uint8_t *prefix, uint64_t plen, uint8_t out32[32],
                                 int *has_root);
 
+/* HASH [pattern] with the server's pattern convention (server.rs:651-656): pattern NULL / empty / "*"
+ * selects every key (scan("")), anything else is a byte prefix (scan(p)). A key that itself starts with
+ * '*' is therefore only reachable through mkv_tree_prefix_root, exactly as in the reference. */
+mkv_status mkv_tree_hash_pattern(const mkv_tree *t, const uint8_t *pattern, uint64_t plen, uint8_t out32[32],
+                                 int *has_root);
+
 /* Key i of a list is bytes[offsets[i] .. offsets[i+1]) (offsets has n+1 entries; offsets[0] may be
  * nonzero). The memory stays valid until mkv_keylist_free. */
 mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets);
@@ -153,6 +166,14 @@ mkv_status mkv_shard_reduce(mkv_tree *t, uint64_t global_offset, uint64_t global
 mkv_status mkv_shard_fringe(const mkv_tree *t, uint8_t *out /* MKV_FRINGE_BYTES */);
 mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes /* world x MKV_FRINGE_BYTES */, uint32_t world,
                              uint64_t global_n, uint8_t out32[32], int *has_root);
+/* Device-resident forms for an RCCL all-gather (no host staging of the fringes): fringe_device writes
+ * MKV_FRINGE_BYTES into device memory on the tree's device and returns when it is complete;
+ * combine_device reads `world` gathered blocks at dfringes + r * stride_bytes (stride >= MKV_FRINGE_BYTES,
+ * multiple of 16; several trees' fringes can share one all-gather), orders them on the device and
+ * returns the global root. The caller must have completed the collective before the call. */
+mkv_status mkv_shard_fringe_device(const mkv_tree *t, uint8_t *dout);
+mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32_t world, uint64_t stride_bytes,
+                                    uint64_t global_n, uint8_t out32[32], int *has_root);
 
 /* ---------------- measurement / test utilities (not part of the reference API) ---------------- */
 /* Per-kernel-group device time accumulated with HIP events on the tree's stream when enabled.
@@ -167,6 +188,12 @@ mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, 
                                   uint64_t *koff, uint8_t *vb, uint64_t *voff);
 /* Leaf digests only (Kernel A) over host records; out = n*32 bytes. */
 mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint8_t *out);
+/* Pinned key-list pool (results of diff / leaves / keys_at live in pinned host blocks recycled through
+ * a bounded pool; MKV_POOL_MAX_MB caps it, default 1024). trim frees every pooled block now (it is also
+ * emptied when the last tree is destroyed). stats: out6 = {hipHostMalloc calls, hipHostFree calls,
+ * bytes pinned in total, host ns spent in both, blocks pooled now, bytes pooled now}. */
+mkv_status mkv_pool_trim(void);
+mkv_status mkv_pool_stats(uint64_t out6[6]);
 /* Library version string. */
 const char *mkv_version(void);
 

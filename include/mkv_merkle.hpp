@@ -9,6 +9,14 @@
 // Semantics note: insert()/remove() are queued and applied as one ordered device batch before the
 // next observation. The reference rebuilds after every insert (merkle.rs:52-56), and a rebuild is a
 // function of the final leaf map only, so every observable result is identical.
+//
+// Const contract: the observers keep the reference's receivers — get_root_hash(&self),
+// diff_keys(&self, &MerkleTree), leaves(&self), ... are const here — so call sites written against
+// immutable bindings (sync.rs:61-67, server.rs:661-675) compile unchanged. Applying the queued
+// operations from a const observer is interior mutability (the queue is `mutable`; the device tree is
+// behind the handle): the observable value is the same as the reference's eager rebuild. Like the
+// reference (Send, not shared across threads without a lock), one object must not be used from two
+// threads at once.
 #pragma once
 #include <array>
 #include <cstdint>
@@ -55,7 +63,7 @@ class MerkleTree {
         if (h_) mkv_tree_destroy(h_);
     }
     MerkleTree(const MerkleTree &o) : dev_(o.dev_) {  // #[derive(Clone)] — merkle.rs:27
-        const_cast<MerkleTree &>(o).flush();
+        o.flush();
         check(mkv_tree_create(dev_, &h_));
         check(mkv_tree_clone(o.h_, h_));
     }
@@ -79,7 +87,7 @@ class MerkleTree {
     }
 
     // get_root_hash() — merkle.rs:65-67
-    std::optional<Digest> get_root_hash() {
+    std::optional<Digest> get_root_hash() const {
         flush();
         Digest d{};
         int has = 0;
@@ -88,7 +96,7 @@ class MerkleTree {
         return d;
     }
 
-    size_t len() {
+    size_t len() const {
         flush();
         uint64_t n = 0;
         check(mkv_tree_len(h_, &n));
@@ -96,14 +104,14 @@ class MerkleTree {
     }
 
     // inorder_keys() — merkle.rs:126-130
-    std::vector<std::string> inorder_keys() {
+    std::vector<std::string> inorder_keys() const {
         std::vector<std::string> out;
         for (auto &kv : leaves()) out.push_back(kv.first);
         return out;
     }
 
     // leaves() — merkle.rs:133-138
-    std::vector<std::pair<std::string, Digest>> leaves() {
+    std::vector<std::pair<std::string, Digest>> leaves() const {
         flush();
         uint64_t n = 0;
         check(mkv_tree_len(h_, &n));
@@ -121,7 +129,7 @@ class MerkleTree {
     }
 
     // Level l of the implicit tree (0 = leaf digests in key order).
-    std::vector<Digest> level(uint32_t l) {
+    std::vector<Digest> level(uint32_t l) const {
         flush();
         uint64_t c = 0;
         check(mkv_tree_level(h_, l, &c, nullptr));
@@ -129,7 +137,7 @@ class MerkleTree {
         if (c) check(mkv_tree_level(h_, l, &c, out.data()->data()));
         return out;
     }
-    uint32_t level_count() {
+    uint32_t level_count() const {
         flush();
         uint32_t L = 0;
         check(mkv_tree_level_count(h_, &L));
@@ -137,7 +145,7 @@ class MerkleTree {
     }
 
     // preorder_hashes() — merkle.rs:142-153 (a promoted node is the same node as its child: visited once)
-    std::vector<Digest> preorder_hashes() {
+    std::vector<Digest> preorder_hashes() const {
         uint32_t L = level_count();
         std::vector<std::vector<Digest>> lv;
         for (uint32_t l = 0; l < L; ++l) lv.push_back(level(l));
@@ -165,7 +173,7 @@ class MerkleTree {
     }
 
     // node_count() — merkle.rs:156-163
-    size_t node_count() {
+    size_t node_count() const {
         flush();
         uint64_t c = 0;
         check(mkv_tree_node_count(h_, &c));
@@ -174,7 +182,7 @@ class MerkleTree {
 
     // Shape of the root's children (merkle.rs:343-358 tests): is child `right` (or left) a leaf?
     // A promoted node is the same node as its only child (R5), exactly as in the reference.
-    bool root_child_is_leaf(bool right) {
+    bool root_child_is_leaf(bool right) const {
         uint32_t L = level_count();
         if (L < 2) return false;
         std::vector<uint64_t> sizes;
@@ -193,7 +201,7 @@ class MerkleTree {
     }
 
     // diff_keys(&other) — merkle.rs:171-196
-    std::vector<std::string> diff_keys(MerkleTree &other) {
+    std::vector<std::string> diff_keys(const MerkleTree &other) const {
         flush();
         other.flush();
         mkv_keylist *kl = nullptr;
@@ -201,14 +209,14 @@ class MerkleTree {
         return take(kl);
     }
     // diff_first_key(&other) — merkle.rs:199-204
-    std::optional<std::string> diff_first_key(MerkleTree &other) {
+    std::optional<std::string> diff_first_key(const MerkleTree &other) const {
         auto d = diff_keys(other);
         if (d.empty()) return std::nullopt;
         return d.front();
     }
 
-    // HASH <prefix> — server.rs:647-685
-    std::optional<Digest> prefix_root(std::string_view prefix) {
+    // Root of a fresh tree over the keys starting with the byte prefix (range reduction; '*' is a byte).
+    std::optional<Digest> prefix_root(std::string_view prefix) const {
         flush();
         Digest d{};
         int has = 0;
@@ -216,8 +224,17 @@ class MerkleTree {
         if (!has) return std::nullopt;
         return d;
     }
+    // HASH [pattern] — server.rs:647-685 with its convention (:651-656): "" or "*" = every key.
+    std::optional<Digest> hash_pattern(std::string_view pattern) const {
+        flush();
+        Digest d{};
+        int has = 0;
+        check(mkv_tree_hash_pattern(h_, reinterpret_cast<const uint8_t *>(pattern.data()), pattern.size(), d.data(), &has));
+        if (!has) return std::nullopt;
+        return d;
+    }
 
-    mkv_tree *handle() {
+    mkv_tree *handle() const {
         flush();
         return h_;
     }
@@ -229,7 +246,7 @@ class MerkleTree {
     };
     int dev_;
     mkv_tree *h_ = nullptr;
-    std::vector<Op> pending_;
+    mutable std::vector<Op> pending_;  // interior mutability: applied by the first observer
 
     static std::vector<std::string> take(mkv_keylist *kl) {
         uint64_t n = 0;
@@ -244,7 +261,7 @@ class MerkleTree {
         return out;
     }
 
-    void flush() {
+    void flush() const {
         if (pending_.empty()) return;
         PackedBlob k, v;
         std::vector<uint8_t> rm;

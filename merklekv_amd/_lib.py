@@ -26,6 +26,8 @@ EXPORTS = [
     "mkv_tree_prefix_root", "mkv_keylist_get", "mkv_keylist_free", "mkv_last_error", "mkv_shard_prepare",
     "mkv_shard_reduce", "mkv_shard_fringe", "mkv_shard_combine", "mkv_prof_enable", "mkv_prof_reset",
     "mkv_prof_read", "mkv_gen_records_device", "mkv_leaf_digests", "mkv_version",
+    "mkv_tree_build_digests", "mkv_tree_hash_pattern", "mkv_shard_fringe_device", "mkv_shard_combine_device",
+    "mkv_pool_trim", "mkv_pool_stats",
 ]
 
 
@@ -89,6 +91,12 @@ def lib():
         "mkv_gen_records_device": ([i32, u64, u64, u64, u32, u32, u32, u32, u32, vp, vp, vp, vp], i32),
         "mkv_leaf_digests": ([i32, Blob, Blob, vp], i32),
         "mkv_version": ([], C.c_char_p),
+        "mkv_tree_build_digests": ([vp, Blob, vp], i32),
+        "mkv_tree_hash_pattern": ([vp, vp, u64, vp, P(i32)], i32),
+        "mkv_shard_fringe_device": ([vp, vp], i32),
+        "mkv_shard_combine_device": ([vp, vp, u32, u64, u64, vp, P(i32)], i32),
+        "mkv_pool_trim": ([], i32),
+        "mkv_pool_stats": ([vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

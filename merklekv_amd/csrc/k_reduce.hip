@@ -102,13 +102,54 @@ struct SeamEntry {
 static_assert(sizeof(SeamEntry) == 48, "seam entry layout");
 
 constexpr int SEAM_MAX = 64;
+
+// Device-side fringe ordering (mkv_shard_combine_device): `world` all-gathered fringe blocks (block r at
+// blocks + r * stride; up to max_e entries, valid ones first, each rank's sorted by (level, index), at
+// most two per level) -> one array sorted by (level, index) plus its length. Ranks hold contiguous key
+// ranges ordered by rank, so inside a level rank order is index order: the position of an entry is
+// (entries of lower levels) + (entries of lower ranks at its level) + (0 or 1 within its rank).
+constexpr uint32_t SEAM_PREP_THREADS = 256;
+constexpr uint32_t SEAM_MAX_RANKS = 64;
+__global__ __launch_bounds__(SEAM_PREP_THREADS) void k_seam_prep(const uint8_t *__restrict__ blocks, uint32_t world,
+                                                                 uint64_t stride, uint32_t max_e,
+                                                                 SeamEntry *__restrict__ out, uint32_t *__restrict__ count) {
+    __shared__ uint32_t cnt[64 * SEAM_MAX_RANKS];  // [level][rank]
+    const uint32_t tid = threadIdx.x, groups = 64 * world, tot = world * max_e;
+    for (uint32_t i = tid; i < groups; i += SEAM_PREP_THREADS) cnt[i] = 0;
+    __syncthreads();
+    for (uint32_t s = tid; s < tot; s += SEAM_PREP_THREADS) {
+        const uint32_t r = s / max_e, e = s - r * max_e;
+        const SeamEntry *E = reinterpret_cast<const SeamEntry *>(blocks + r * stride) + e;
+        if (E->valid && E->level < 64) atomicAdd(&cnt[E->level * world + r], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {  // <= 64 x world groups, LDS only
+        uint32_t run = 0;
+        for (uint32_t i = 0; i < groups; ++i) {
+            const uint32_t c = cnt[i];
+            cnt[i] = run;
+            run += c;
+        }
+        *count = run;
+    }
+    __syncthreads();
+    for (uint32_t s = tid; s < tot; s += SEAM_PREP_THREADS) {
+        const uint32_t r = s / max_e, e = s - r * max_e;
+        const SeamEntry *E = reinterpret_cast<const SeamEntry *>(blocks + r * stride) + e;
+        if (!E->valid || E->level >= 64) continue;
+        const uint32_t within = (e > 0 && E[-1].valid && E[-1].level == E->level) ? 1u : 0u;
+        out[cnt[E->level * world + r] + within] = *E;
+    }
+}
 constexpr uint32_t SEAM_STAGE = 1024;  // fringe entries staged in LDS (8 ranks x <= 130 fit)
 
 // One wave. Loose nodes of level l (fringes handed over by the shards + seam nodes computed from
 // level l-1) are kept sorted by index in LDS; each lane hashes at most one parent per level.
 __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict__ ent, uint32_t nent,
+                                                    const uint32_t *__restrict__ nent_dev,
                                                     const uint64_t *__restrict__ S, uint32_t L,
                                                     uint8_t *__restrict__ root) {
+    if (nent_dev) nent = *nent_dev;  // entries prepared on the device (k_seam_prep)
     __shared__ uint64_t cidx[SEAM_MAX];
     __shared__ uint32_t ch[SEAM_MAX][8];
     __shared__ uint64_t nidx[SEAM_MAX];
@@ -268,7 +309,17 @@ void launch_seam_combine(const uint8_t *entries, uint32_t nent, const uint64_t *
                          uint8_t *scratch, uint8_t *root_out, hipStream_t st) {
     (void)scratch;
     hipLaunchKernelGGL(k_seam_combine, dim3(1), dim3(64), 0, st, reinterpret_cast<const SeamEntry *>(entries), nent,
-                       level_sizes, nlevels, root_out);
+                       static_cast<const uint32_t *>(nullptr), level_sizes, nlevels, root_out);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_seam_prep_combine(const uint8_t *blocks, uint32_t world, uint64_t stride, uint32_t max_entries,
+                              const uint64_t *level_sizes, uint32_t nlevels, uint8_t *scratch, uint32_t *count,
+                              uint8_t *root_out, hipStream_t st) {
+    SeamEntry *sorted = reinterpret_cast<SeamEntry *>(scratch);
+    hipLaunchKernelGGL(k_seam_prep, dim3(1), dim3(SEAM_PREP_THREADS), 0, st, blocks, world, stride, max_entries, sorted,
+                       count);
+    hipLaunchKernelGGL(k_seam_combine, dim3(1), dim3(64), 0, st, sorted, 0u, count, level_sizes, nlevels, root_out);
     MKV_LAUNCH_CHECK();
 }
 

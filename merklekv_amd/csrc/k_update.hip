@@ -54,15 +54,33 @@ __global__ __launch_bounds__(256) void k_locate(const uint8_t *__restrict__ kb, 
             else hi = mid;
         }
         uint64_t found = UINT64_MAX;
-        for (uint64_t j = lo; j < T.n && T.pfx[j] == c0; ++j) {
-            uint64_t tl;
-            const uint8_t *tk = tree_key(T, j, &tl);
-            const int c = key_cmp(k, len, c0, tk, tl, c0);
-            if (c == 0) {
-                found = j;
-                break;
+        if (lo < T.n && T.pfx[lo] == c0) {
+            // Equal-prefix run [lo, e): keys sharing >= 8 leading bytes ("tenant/0001/obj/...") can make
+            // it the whole tree, so it is binary-searched on the full key (lower_bound with key_cmp),
+            // never walked: O(log n) full-key compares per batch key.
+            uint64_t e = lo + 1;
+            if (e < T.n && T.pfx[e] == c0) {
+                uint64_t a = e, b = T.n;  // first position with pfx > c0
+                while (a < b) {
+                    const uint64_t mid = (a + b) >> 1;
+                    if (T.pfx[mid] <= c0) a = mid + 1;
+                    else b = mid;
+                }
+                e = a;
             }
-            if (c < 0) break;
+            uint64_t a = lo, b = e;
+            while (a < b) {
+                const uint64_t mid = (a + b) >> 1;
+                uint64_t tl;
+                const uint8_t *tk = tree_key(T, mid, &tl);
+                if (key_cmp(tk, tl, c0, k, len, c0) < 0) a = mid + 1;
+                else b = mid;
+            }
+            if (a < e) {
+                uint64_t tl;
+                const uint8_t *tk = tree_key(T, a, &tl);
+                if (key_cmp(k, len, c0, tk, tl, c0) == 0) found = a;
+            }
         }
         miss = found == UINT64_MAX;
         pos[i] = found;

@@ -102,6 +102,12 @@ void launch_reduce_fused(const FusePlan &p, hipStream_t st);
 // (level, index); see tree.cpp. Writes the root.
 void launch_seam_combine(const uint8_t *entries, uint32_t nent, const uint64_t *level_sizes, uint32_t nlevels,
                          uint8_t *scratch, uint8_t *root_out, hipStream_t st);
+// Same from `world` raw fringe blocks in device memory (block r at blocks + r * stride, max_entries
+// slots each): ordered on the device (scratch >= world * max_entries * 48 B, *count = entries), then
+// combined. No host round trip.
+void launch_seam_prep_combine(const uint8_t *blocks, uint32_t world, uint64_t stride, uint32_t max_entries,
+                              const uint64_t *level_sizes, uint32_t nlevels, uint8_t *scratch, uint32_t *count,
+                              uint8_t *root_out, hipStream_t st);
 
 // ---- Kernel D: diff (k_diff.hip) ----
 struct DiffSide {

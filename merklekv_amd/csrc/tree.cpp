@@ -4,6 +4,8 @@
 #include "mkv_merkle.h"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -11,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -41,10 +44,41 @@ struct EvPair {
 
 // Key lists live in pinned host blocks that the device writes directly (no pageable staging, no extra
 // host copy); a batched diff's per-variant lists are views sharing one block. Blocks are recycled
-// through a small pool because pinning tens of MB costs milliseconds.
+// through a small pool because pinning tens of MB costs milliseconds. The pool is bounded: at most
+// POOL_MAX_BLOCKS blocks and MKV_POOL_MAX_MB (default 1024) MiB are kept, a request never takes a
+// pooled block more than 4x its size (a one-key diff must not hold a multi-GB block), and the pool is
+// emptied when the last tree handle is destroyed or on mkv_pool_trim(). Allocation counters
+// (mkv_pool_stats) let a caller see whether a slow call paid for page pinning.
 namespace {
 std::mutex g_pool_mu;
-std::vector<std::pair<uint8_t *, size_t>> g_pool;  // free pinned blocks (never released at exit)
+std::vector<std::pair<uint8_t *, size_t>> g_pool;  // free pinned blocks
+size_t g_pool_bytes = 0;
+std::atomic<uint64_t> g_pin_allocs{0}, g_pin_frees{0}, g_pin_alloc_bytes{0};
+std::atomic<uint64_t> g_pin_ns{0};  // host time spent in hipHostMalloc / hipHostFree
+std::atomic<int64_t> g_live_trees{0};
+constexpr size_t POOL_MAX_BLOCKS = 16;
+
+size_t pool_max_bytes() {
+    static const size_t v = [] {
+        const char *e = getenv("MKV_POOL_MAX_MB");
+        const double mb = e ? atof(e) : 1024.0;
+        return (size_t)(mb > 0 ? mb : 0) << 20;
+    }();
+    return v;
+}
+
+void pin_free(uint8_t *p) {
+    const auto t0 = std::chrono::steady_clock::now();
+    (void)hipHostFree(p);
+    g_pin_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    ++g_pin_frees;
+}
+
+void pool_trim_locked() {
+    for (auto &b : g_pool) pin_free(b.first);
+    g_pool.clear();
+    g_pool_bytes = 0;
+}
 
 struct PinnedBlock {
     uint8_t *p = nullptr;
@@ -52,40 +86,53 @@ struct PinnedBlock {
     explicit PinnedBlock(size_t bytes) {
         {
             std::lock_guard<std::mutex> lk(g_pool_mu);
+            const size_t limit = std::max<size_t>(4 * bytes, 1 << 20);
             size_t best = SIZE_MAX;
             for (size_t i = 0; i < g_pool.size(); ++i)
-                if (g_pool[i].second >= bytes && (best == SIZE_MAX || g_pool[i].second < g_pool[best].second))
+                if (g_pool[i].second >= bytes && g_pool[i].second <= limit &&
+                    (best == SIZE_MAX || g_pool[i].second < g_pool[best].second))
                     best = i;
             if (best != SIZE_MAX) {
                 p = g_pool[best].first;
                 cap = g_pool[best].second;
+                g_pool_bytes -= cap;
                 g_pool.erase(g_pool.begin() + (long)best);
                 return;
             }
         }
         cap = std::max<size_t>(bytes + bytes / 4, 4096);
+        const auto t0 = std::chrono::steady_clock::now();
         MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), cap, hipHostMallocDefault));
+        g_pin_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        ++g_pin_allocs;
+        g_pin_alloc_bytes += cap;
     }
     PinnedBlock(const PinnedBlock &) = delete;
     PinnedBlock &operator=(const PinnedBlock &) = delete;
     ~PinnedBlock() {
-        // A full pool keeps its largest blocks: small ones left by earlier calls (level views, short
-        // key lists) must not force every large diff result through hipHostMalloc/hipHostFree, whose
-        // page (un)pinning costs milliseconds.
+        // A full pool keeps its largest blocks (within the byte cap): small ones left by earlier calls
+        // (level views, short key lists) must not force every large diff result through
+        // hipHostMalloc/hipHostFree, whose page (un)pinning costs milliseconds.
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (g_pool.size() < 16) {
-            g_pool.emplace_back(p, cap);
+        const size_t maxb = pool_max_bytes();
+        if (cap > maxb || g_live_trees.load() <= 0) {
+            pin_free(p);
             return;
         }
-        size_t small = 0;
-        for (size_t i = 1; i < g_pool.size(); ++i)
-            if (g_pool[i].second < g_pool[small].second) small = i;
-        uint8_t *victim = p;
-        if (g_pool[small].second < cap) {
-            victim = g_pool[small].first;
-            g_pool[small] = {p, cap};
+        while (!g_pool.empty() && (g_pool.size() >= POOL_MAX_BLOCKS || g_pool_bytes + cap > maxb)) {
+            size_t small = 0;
+            for (size_t i = 1; i < g_pool.size(); ++i)
+                if (g_pool[i].second < g_pool[small].second) small = i;
+            if (g_pool[small].second >= cap) {  // every pooled block is at least as large: drop this one
+                pin_free(p);
+                return;
+            }
+            g_pool_bytes -= g_pool[small].second;
+            pin_free(g_pool[small].first);
+            g_pool.erase(g_pool.begin() + (long)small);
         }
-        (void)hipHostFree(victim);
+        g_pool.emplace_back(p, cap);
+        g_pool_bytes += cap;
     }
 };
 }  // namespace
@@ -159,6 +206,7 @@ struct mkv_tree {
     const uint64_t *in_koff = nullptr;
     uint64_t in_n = 0;
     const uint8_t *in_tomb = nullptr;
+    bool counted = false;  // counted in g_live_trees
 };
 
 namespace {
@@ -179,6 +227,19 @@ __global__ void k_clear_tomb(const uint8_t *__restrict__ tomb, const uint32_t *_
                              uint32_t *__restrict__ flags) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n && tomb[perm[i]]) flags[i] = 0;
+}
+// Fringe entry i (48 B: level, valid, idx, digest) gets the digest of node nodes[idx[i]] at byte 16.
+__global__ void k_fringe_digests(const uint8_t *__restrict__ nodes, const uint32_t *__restrict__ idx, uint32_t k,
+                                 uint8_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 2 * k) {  // two 16-B halves per entry
+        const uint4 *src = reinterpret_cast<const uint4 *>(nodes + 32ull * idx[i >> 1]) + (i & 1);
+        *reinterpret_cast<uint4 *>(out + 48ull * (i >> 1) + 16 + 16 * (i & 1)) = *src;
+    }
+}
+void launch_fringe_digests(const uint8_t *nodes, const uint32_t *idx, uint32_t k, uint8_t *out, hipStream_t st) {
+    hipLaunchKernelGGL(k_fringe_digests, dim3((2 * k + 255) / 256), dim3(256), 0, st, nodes, idx, k, out);
+    MKV_LAUNCH_CHECK();
 }
 __global__ void k_widen_positions(const uint32_t *__restrict__ f, uint64_t m, uint64_t *__restrict__ k,
                                   uint32_t *__restrict__ v) {
@@ -340,15 +401,45 @@ void prof_collect(mkv_tree *t) {
     t->evdone.clear();
 }
 
-// Low-latency wait: poll an event recorded on the stream instead of the runtime's blocking sync
-// (tens of microseconds of wake-up latency per scalar readback otherwise).
-// Spin on hipStreamQuery: no marker command is queued, so an already idle stream returns at once
-// (measured end to end it matches the earlier record-an-event-and-poll wait; kept for its simplicity).
+// Low-latency wait: poll the stream instead of the runtime's blocking sync (tens of microseconds of
+// wake-up latency per scalar readback otherwise). hipStreamQuery queues no marker, so an idle stream
+// returns at once. The spin is bounded: after MKV_SPIN_US (default 200 µs) the thread yields, after
+// 20 ms it sleeps in 50-µs steps (a long kernel does not pin a host core, nor a tokio blocking-pool
+// thread), and after MKV_WAIT_TIMEOUT_S (default 120 s) the call fails with MKV_EHIP instead of
+// waiting forever on a hung device.
+static double wait_timeout_s() {
+    static const double v = [] {
+        const char *e = getenv("MKV_WAIT_TIMEOUT_S");
+        const double x = e ? atof(e) : 120.0;
+        return x > 0 ? x : 120.0;
+    }();
+    return v;
+}
+static double spin_us() {
+    static const double v = [] {
+        const char *e = getenv("MKV_SPIN_US");
+        return e ? atof(e) : 200.0;
+    }();
+    return v;
+}
 void wait_idle(hipStream_t s) {
-    for (;;) {
-        hipError_t e = hipStreamQuery(s);
+    hipError_t e = hipStreamQuery(s);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) MKV_HIP(e);
+    const auto t0 = std::chrono::steady_clock::now();
+    const double spin = spin_us(), limit = wait_timeout_s() * 1e6;
+    for (uint64_t it = 0;; ++it) {
+        e = hipStreamQuery(s);
         if (e == hipSuccess) return;
         if (e != hipErrorNotReady) MKV_HIP(e);
+        if ((it & 15) != 15) continue;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        if (us < spin) continue;
+        if (us > limit)
+            throw Error(ST_EHIP, "device wait timed out after " + std::to_string((int)(us / 1e6)) +
+                                     " s (hung kernel?); raise MKV_WAIT_TIMEOUT_S for longer work");
+        if (us < spin + 20000) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 void wait_stream(mkv_tree *t, hipStream_t s) {
@@ -865,6 +956,8 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             mkv_tree_destroy(t);
             throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
         }
+        ++g_live_trees;
+        t->counted = true;
         *out = t;
     });
 }
@@ -886,8 +979,33 @@ void mkv_tree_destroy(mkv_tree *t) {
     if (t->h_counts) (void)hipHostFree(t->h_counts);
     if (t->h_seam) (void)hipHostFree(t->h_seam);
     if (t->st) (void)hipStreamDestroy(t->st);
+    const bool counted = t->counted;
     delete t;
     (void)hipGetLastError();
+    if (counted && --g_live_trees <= 0) {  // last handle gone: unpin the pooled key-list blocks
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        pool_trim_locked();
+    }
+}
+
+mkv_status mkv_pool_trim(void) {
+    MKV_TRY({
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        pool_trim_locked();
+    });
+}
+
+mkv_status mkv_pool_stats(uint64_t *out6) {
+    MKV_TRY({
+        NEED(out6, "null argument");
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        out6[0] = g_pin_allocs.load();
+        out6[1] = g_pin_frees.load();
+        out6[2] = g_pin_alloc_bytes.load();
+        out6[3] = g_pin_ns.load();
+        out6[4] = g_pool.size();
+        out6[5] = g_pool_bytes;
+    });
 }
 
 mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
@@ -962,6 +1080,29 @@ mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         upload_blob(t, values, t->s_vb, t->s_voff);
         build_from_staged(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), t->s_vb.as<uint8_t>(),
                           t->s_voff.as<uint64_t>(), n, true, kbn);
+    });
+}
+
+mkv_status mkv_tree_build_digests(mkv_tree *t, mkv_blob keys, const uint8_t *digests) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(digests || keys.n == 0, "null digests");
+        check_blob(keys, "keys");
+        DevGuard g(t->dev);
+        const uint64_t n = keys.n;
+        const uint64_t kbn = n ? keys.offsets[n] - keys.offsets[0] : 0;
+        ens<uint8_t>(t->s_kb, kbn + 16);
+        ens<uint64_t>(t->s_koff, n + 1);
+        uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+        if (n) MKV_HIP(hipMemcpyAsync(dig, digests, 32 * n, hipMemcpyHostToDevice, t->st));
+        upload_blob(t, keys, t->s_kb, t->s_koff);  // synchronises t->st: the digests have landed too
+        // Kernel A is skipped: the leaf digests arrive ready-made (a peer's (key, leaf digest) pairs)
+        size_t ptot = prof_begin(t, "total_build");
+        fork_streams(t);
+        sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), n, nullptr, true, kbn, true);
+        finish_unsharded(t);
+        prof_end(t, ptot);
+        sync(t);
     });
 }
 
@@ -2003,8 +2144,7 @@ mkv_status mkv_tree_compare_nodes(const mkv_tree *tc, uint32_t level, const uint
 mkv_status mkv_tree_keys_at(const mkv_tree *tc, const uint64_t *pos, uint64_t m, mkv_keylist **out) {
     MKV_TRY({
         NEED(tc && out && (m == 0 || pos), "null argument");
-        NEED(!tc->prepared, "shard_reduce pending");
-        *out = nullptr;
+        *out = nullptr;  // valid right after mkv_shard_prepare too (sorted keys exist; shard range checks)
         mkv_tree *t = const_cast<mkv_tree *>(tc);
         for (uint64_t i = 0; i < m; ++i) NEED(pos[i] < t->n, "leaf position out of range");
         DevGuard g(t->dev);
@@ -2053,6 +2193,13 @@ mkv_status mkv_tree_prefix_root(const mkv_tree *tc, const uint8_t *prefix, uint6
         tmp.st = nullptr;
         *has_root = 1;
     });
+}
+
+mkv_status mkv_tree_hash_pattern(const mkv_tree *t, const uint8_t *pattern, uint64_t plen, uint8_t out32[32],
+                                 int *has_root) {
+    // server.rs:651-656: None, "" and "*" all mean scan("") (every key); anything else is a prefix
+    if (plen == 0 || (plen == 1 && pattern && pattern[0] == '*')) return mkv_tree_prefix_root(t, nullptr, 0, out32, has_root);
+    return mkv_tree_prefix_root(t, pattern, plen, out32, has_root);
 }
 
 mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets) {
@@ -2160,6 +2307,34 @@ struct FringeEntry {
 static_assert(sizeof(FringeEntry) == MKV_FRINGE_ENTRY_BYTES, "fringe layout");
 }  // namespace
 
+// The fringe of a shard: owned nodes whose parent is not owned (<= 2 per level), as entries with their
+// node-array index (digests filled by the caller).
+static void fringe_entries(const mkv_tree *t, std::vector<FringeEntry> &fe, std::vector<uint32_t> &nodeidx) {
+    const size_t L = t->lev_S.size();
+    for (size_t l = 0; l < L; ++l) {
+        const uint64_t a = t->lev_base[l], c = t->lev_cnt[l];
+        if (!c) continue;
+        uint64_t cand[2] = {a, a + c - 1};
+        for (int q = 0; q < 2; ++q) {
+            if (q == 1 && cand[1] == cand[0]) break;
+            const uint64_t x = cand[q];
+            bool parent_owned = false;
+            if (l + 1 < L) {
+                const uint64_t p = x / 2, a2 = t->lev_base[l + 1], c2 = t->lev_cnt[l + 1];
+                parent_owned = p >= a2 && p < a2 + c2;
+            }
+            if (parent_owned) continue;
+            FringeEntry e{};
+            e.level = (uint32_t)l;
+            e.valid = 1;
+            e.idx = x;
+            fe.push_back(e);
+            nodeidx.push_back((uint32_t)(t->lev_off[l] + (x - a)));
+        }
+    }
+    NEED(fe.size() <= MKV_FRINGE_MAX_ENTRIES, "fringe overflow");
+}
+
 mkv_status mkv_shard_fringe(const mkv_tree *tc, uint8_t *out) {
     MKV_TRY({
         NEED(tc && out, "null argument");
@@ -2169,29 +2344,7 @@ mkv_status mkv_shard_fringe(const mkv_tree *tc, uint8_t *out) {
         std::memset(out, 0, MKV_FRINGE_BYTES);
         std::vector<FringeEntry> fe;
         std::vector<uint32_t> nodeidx;
-        const size_t L = t->lev_S.size();
-        for (size_t l = 0; l < L; ++l) {
-            const uint64_t a = t->lev_base[l], c = t->lev_cnt[l];
-            if (!c) continue;
-            uint64_t cand[2] = {a, a + c - 1};
-            for (int q = 0; q < 2; ++q) {
-                if (q == 1 && cand[1] == cand[0]) break;
-                const uint64_t x = cand[q];
-                bool parent_owned = false;
-                if (l + 1 < L) {
-                    const uint64_t p = x / 2, a2 = t->lev_base[l + 1], c2 = t->lev_cnt[l + 1];
-                    parent_owned = p >= a2 && p < a2 + c2;
-                }
-                if (parent_owned) continue;
-                FringeEntry e{};
-                e.level = (uint32_t)l;
-                e.valid = 1;
-                e.idx = x;
-                fe.push_back(e);
-                nodeidx.push_back((uint32_t)(t->lev_off[l] + (x - a)));
-            }
-        }
-        NEED(fe.size() <= MKV_FRINGE_MAX_ENTRIES, "fringe overflow");
+        fringe_entries(t, fe, nodeidx);
         if (!fe.empty()) {
             uint32_t *didx = ens<uint32_t>(t->d_fr, fe.size() + 64);
             uint8_t *dh = ens<uint8_t>(t->d_seam, fe.size() * 32 + 64);
@@ -2203,6 +2356,41 @@ mkv_status mkv_shard_fringe(const mkv_tree *tc, uint8_t *out) {
             for (size_t i = 0; i < fe.size(); ++i) std::memcpy(fe[i].h, hh.data() + 32 * i, 32);
         }
         std::memcpy(out, fe.data(), fe.size() * sizeof(FringeEntry));
+    });
+}
+
+// Pinned staging of at least `bytes` (seam inputs / fringe headers).
+static uint8_t *seam_staging(mkv_tree *t, size_t bytes) {
+    if (!t->h_seam || t->h_seam_cap < bytes) {
+        if (t->h_seam) MKV_HIP(hipHostFree(t->h_seam));
+        t->h_seam = nullptr;
+        t->h_seam_cap = bytes + 4096;
+        MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&t->h_seam), t->h_seam_cap, hipHostMallocDefault));
+    }
+    return t->h_seam;
+}
+
+mkv_status mkv_shard_fringe_device(const mkv_tree *tc, uint8_t *dout) {
+    MKV_TRY({
+        NEED(tc && dout, "null argument");
+        NEED(!tc->prepared, "mkv_shard_reduce first");
+        mkv_tree *t = const_cast<mkv_tree *>(tc);
+        DevGuard g(t->dev);
+        std::vector<FringeEntry> fe;
+        std::vector<uint32_t> nodeidx;
+        fringe_entries(t, fe, nodeidx);
+        // headers (and zeroed slots) from pinned staging, digests gathered on the device in place
+        uint8_t *h = seam_staging(t, MKV_FRINGE_BYTES + 4 * (nodeidx.size() + 1));
+        std::memset(h, 0, MKV_FRINGE_BYTES);
+        if (!fe.empty()) std::memcpy(h, fe.data(), fe.size() * sizeof(FringeEntry));
+        if (!nodeidx.empty()) std::memcpy(h + MKV_FRINGE_BYTES, nodeidx.data(), 4 * nodeidx.size());
+        uint32_t *didx = ens<uint32_t>(t->d_fr, nodeidx.size() + 64);
+        MKV_HIP(hipMemcpyAsync(dout, h, MKV_FRINGE_BYTES, hipMemcpyHostToDevice, t->st));
+        if (!nodeidx.empty()) {
+            MKV_HIP(hipMemcpyAsync(didx, h + MKV_FRINGE_BYTES, 4 * nodeidx.size(), hipMemcpyHostToDevice, t->st));
+            launch_fringe_digests(t->nodes.as<uint8_t>(), didx, (uint32_t)nodeidx.size(), dout, t->st);
+        }
+        wait_stream(t, t->st);  // dout is complete before the caller's collective reads it
     });
 }
 
@@ -2229,12 +2417,7 @@ mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes, uint32_t world
         }
         // one pinned staging block: [S (64 x u64) | entries]; the root comes back through h_small
         const size_t sbytes = 64 * 8, ebytes = all.size() * sizeof(FringeEntry);
-        if (!t->h_seam || t->h_seam_cap < sbytes + ebytes) {
-            if (t->h_seam) MKV_HIP(hipHostFree(t->h_seam));
-            t->h_seam = nullptr;
-            t->h_seam_cap = sbytes + ebytes + 4096;
-            MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&t->h_seam), t->h_seam_cap, hipHostMallocDefault));
-        }
+        seam_staging(t, sbytes + ebytes);
         NEED(S.size() <= 64, "too many levels");
         std::memcpy(t->h_seam, S.data(), S.size() * 8);
         if (ebytes) std::memcpy(t->h_seam + sbytes, all.data(), ebytes);
@@ -2244,6 +2427,42 @@ mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes, uint32_t world
         MKV_HIP(hipMemsetAsync(droot, 0, 32, t->st));
         launch_seam_combine(dst + sbytes, (uint32_t)all.size(), reinterpret_cast<const uint64_t *>(dst),
                             (uint32_t)S.size(), nullptr, droot, t->st);
+        MKV_HIP(hipMemcpyAsync(t->h_small, droot, 32, hipMemcpyDeviceToHost, t->st));
+        wait_stream(t, t->st);
+        std::memcpy(out32, t->h_small, 32);
+        *has_root = 1;
+        std::memcpy(t->root, out32, 32);
+        t->has_root = true;
+        t->combine_pending = false;
+    });
+}
+
+mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32_t world, uint64_t stride_bytes,
+                                   uint64_t global_n, uint8_t out32[32], int *has_root) {
+    MKV_TRY({
+        NEED(t && dfringes && out32 && has_root, "null argument");
+        NEED(world >= 1 && world <= 64, "world must be 1..64");
+        NEED(stride_bytes >= MKV_FRINGE_BYTES && stride_bytes % 16 == 0, "bad fringe stride");
+        DevGuard g(t->dev);
+        *has_root = 0;
+        std::memset(out32, 0, 32);
+        if (global_n == 0) return MKV_OK;
+        std::vector<uint64_t> S;
+        for (uint64_t s = global_n;; s = (s + 1) / 2) {
+            S.push_back(s);
+            if (s == 1) break;
+        }
+        NEED(S.size() <= 64, "too many levels");
+        uint8_t *h = seam_staging(t, 64 * 8);
+        std::memcpy(h, S.data(), S.size() * 8);
+        const size_t sbytes = 64 * 8, ebytes = (size_t)world * MKV_FRINGE_MAX_ENTRIES * sizeof(FringeEntry);
+        uint8_t *dst = ens<uint8_t>(t->d_seam, sbytes + ebytes + 64);
+        uint8_t *droot = ens<uint8_t>(t->d_fr, 64);
+        MKV_HIP(hipMemcpyAsync(dst, h, sbytes, hipMemcpyHostToDevice, t->st));
+        MKV_HIP(hipMemsetAsync(droot, 0, 32, t->st));
+        launch_seam_prep_combine(dfringes, world, stride_bytes, MKV_FRINGE_MAX_ENTRIES,
+                                 reinterpret_cast<const uint64_t *>(dst), (uint32_t)S.size(), dst + sbytes,
+                                 reinterpret_cast<uint32_t *>(droot + 32), droot, t->st);
         MKV_HIP(hipMemcpyAsync(t->h_small, droot, 32, hipMemcpyDeviceToHost, t->st));
         wait_stream(t, t->st);
         std::memcpy(out32, t->h_small, 32);

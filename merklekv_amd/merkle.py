@@ -186,6 +186,27 @@ class MerkleTree:
             raise ValueError("keys and values differ in length")
         check(lib().mkv_tree_build(self._h, pk.blob(), pv.blob()))
 
+    def build_digests(self, keys, digests) -> None:
+        """Tree from shipped (key, leaf digest) pairs (mkv_tree_build_digests): same as build() over the
+        original records, without their values (a peer's leaves(), merkle.rs:133-138). digests: bytes
+        or uint8 array of 32 x len(keys), or a sequence of 32-byte digests."""
+        self._pending.clear()
+        self._cache.clear()
+        pk = pack_blob(keys)
+        if not isinstance(digests, (bytes, bytearray, memoryview, np.ndarray)):
+            digests = b"".join(digests)
+        d = np.ascontiguousarray(np.frombuffer(bytes(digests), np.uint8) if not isinstance(digests, np.ndarray)
+                                 else digests.reshape(-1).astype(np.uint8, copy=False))
+        if d.size != 32 * pk.n:
+            raise ValueError("need 32 digest bytes per key")
+        check(lib().mkv_tree_build_digests(self._h, pk.blob(), d.ctypes.data if d.size else None))
+
+    @classmethod
+    def from_digests(cls, keys, digests, device: int = 0) -> "MerkleTree":
+        t = cls(device)
+        t.build_digests(keys, digests)
+        return t
+
     def build_wire(self, scan_response: bytes, get_responses: bytes) -> None:
         """build_remote_merkle_snapshot (sync.rs:122-143) from the raw SCAN response and the concatenated
         GET responses; parsed on the device (mkv_tree_build_wire)."""
@@ -326,6 +347,20 @@ class MerkleTree:
             finally:
                 lib().mkv_keylist_free(kl)
         return self._cache["keys"]
+
+    def leaves_packed(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """leaves() as arrays: (key bytes, offsets[n+1], digests n x 32) — what a peer ships when key
+        sets differ (mkv_tree_leaves)."""
+        self._flush()
+        n = len(self)
+        dig = np.zeros((max(n, 1), 32), np.uint8)
+        kl = C.c_void_p()
+        check(lib().mkv_tree_leaves(self._h, C.byref(kl), dig.ctypes.data))
+        try:
+            raw, offs = _keylist_packed(kl)
+        finally:
+            lib().mkv_keylist_free(kl)
+        return raw, offs, dig[:n]
 
     def inorder_keys(self) -> list[str]:
         """inorder_keys() — merkle.rs:126-130."""
@@ -475,7 +510,9 @@ class MerkleTree:
         return d[0] if d else None
 
     def prefix_root(self, prefix) -> bytes | None:
-        """Root of a fresh tree over the keys starting with prefix (HASH <prefix>, server.rs:647-685)."""
+        """Root of a fresh tree over the keys starting with the byte prefix (mkv_tree_prefix_root). This is
+        the raw range reduction: "*" is a literal byte here; hash_pattern() has the HASH command's
+        wildcard convention."""
         self._flush()
         p = _b(prefix)
         buf = (C.c_uint8 * max(len(p), 1)).from_buffer_copy(p or b"\0")
@@ -483,6 +520,24 @@ class MerkleTree:
         has = C.c_int()
         check(lib().mkv_tree_prefix_root(self._h, buf, len(p), out, C.byref(has)))
         return bytes(out) if has.value else None
+
+    def hash_pattern(self, pattern=None) -> bytes | None:
+        """HASH [pattern] (server.rs:647-685): None, "" and "*" mean every key (server.rs:651-656),
+        anything else is a prefix; None result = the empty set (the server prints 64 zeros)."""
+        self._flush()
+        p = b"" if pattern is None else _b(pattern)
+        buf = (C.c_uint8 * max(len(p), 1)).from_buffer_copy(p or b"\0")
+        out = (C.c_uint8 * 32)()
+        has = C.c_int()
+        check(lib().mkv_tree_hash_pattern(self._h, buf, len(p), out, C.byref(has)))
+        return bytes(out) if has.value else None
+
+    def hash_command(self, pattern=None) -> str:
+        """The server's HASH response line (server.rs:672-682), root or 64 zeros."""
+        r = self.hash_pattern(pattern)
+        hx = r.hex() if r is not None else "0" * 64
+        pat = "" if pattern is None else (pattern if isinstance(pattern, str) else _s(pattern))
+        return f"HASH {hx}\r\n" if not pat else f"HASH {pat} {hx}\r\n"
 
     def clone(self) -> "MerkleTree":
         """#[derive(Clone)] — merkle.rs:27."""
@@ -534,6 +589,17 @@ class MerkleTree:
         check(lib().mkv_shard_combine(self._h, src, world, global_n, out, C.byref(has)))
         return bytes(out) if has.value else None
 
+    def shard_fringe_device(self, dptr: int) -> None:
+        """Write this shard's fringe (MKV_FRINGE_BYTES) into device memory at dptr (complete on return)."""
+        check(lib().mkv_shard_fringe_device(self._h, dptr))
+
+    def shard_combine_device(self, dptr: int, world: int, stride: int, global_n: int) -> bytes | None:
+        """Global root from `world` all-gathered fringe blocks in device memory (block r at dptr + r * stride)."""
+        out = (C.c_uint8 * 32)()
+        has = C.c_int()
+        check(lib().mkv_shard_combine_device(self._h, dptr, world, stride, global_n, out, C.byref(has)))
+        return bytes(out) if has.value else None
+
     def build_device(self, kb_ptr: int, koff_ptr: int, vb_ptr: int, voff_ptr: int, n: int) -> None:
         """Build from records already resident in HBM (device pointers)."""
         self._pending.clear()
@@ -554,6 +620,18 @@ def gen_records_device(device: int, seed: int, idx0: int, n: int, klen: int, vle
                        vb: int, voff: int, shard: int = 0, nshards: int = 1, vfield: int = 1) -> None:
     check(lib().mkv_gen_records_device(device, seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb,
                                        voff))
+
+
+def pool_stats() -> dict:
+    """Pinned key-list pool counters (mkv_pool_stats)."""
+    a = (C.c_uint64 * 6)()
+    check(lib().mkv_pool_stats(a))
+    return {"host_mallocs": a[0], "host_frees": a[1], "bytes_pinned": a[2], "pin_ms": a[3] / 1e6,
+            "pooled_blocks": a[4], "pooled_bytes": a[5]}
+
+
+def pool_trim() -> None:
+    check(lib().mkv_pool_trim())
 
 
 def version() -> str:

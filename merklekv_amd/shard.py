@@ -7,20 +7,49 @@ all-gather fringes, and hash the seam nodes on the device (mkv_shard_combine). E
 same global root, bit-exact with the single-tree root. Collectives go through torch.distributed: on
 ROCm the "nccl" backend is RCCL over xGMI; "gloo" is used by the CPU tests.
 
+Device path (collective device = a GPU): fringes are written straight into a device buffer
+(mkv_shard_fringe_device), all-gathered by RCCL into another device buffer and combined from there
+(mkv_shard_combine_device) — no host staging of the payload. Several trees (replicas) share ONE
+all-gather per step (shard_recombine_many). Host path (gloo / CPU): byte payloads, as the CPU tests use.
+
+Range check: the seam protocol is exact only if rank r holds a contiguous key range below rank r+1's
+(the reference keeps one leaf per key, last write wins). `sharded_root(..., validate=True)` all-gathers
+each shard's first and last sorted key and raises unless last(r) < first(next non-empty rank).
+
 `tree` is anything with the shard_* methods of merklekv_amd.MerkleTree.
 """
 from __future__ import annotations
 
 import numpy as np
 
+from ._lib import FRINGE_BYTES
+
+_bufs: dict = {}
+
+
+def _is_gpu(device) -> bool:
+    import torch
+    return device is not None and torch.device(device).type == "cuda"
+
+
+def _buf(device, tag: str, nbytes: int):
+    """Cached device byte buffer (stable across steps: no allocator churn inside the timed loop)."""
+    import torch
+    key = (str(device), tag)
+    b = _bufs.get(key)
+    if b is None or b.numel() < nbytes:
+        b = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=device)
+        _bufs[key] = b
+    return b
+
 
 def _all_gather_bytes(dist, payload: bytes, device, group=None) -> list[bytes]:
-    """All-gather of equal-size byte payloads: one collective into one buffer, one copy back."""
+    """All-gather of equal-size host byte payloads (host path: gloo / CPU tests, one-off metadata)."""
     import torch
     world = dist.get_world_size(group)
     t = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
     out = torch.empty(world * t.numel(), dtype=torch.uint8, device=device)
-    if hasattr(dist, "all_gather_into_tensor") and (device is None or torch.device(device).type != "cpu"):
+    if hasattr(dist, "all_gather_into_tensor") and _is_gpu(device):
         dist.all_gather_into_tensor(out, t, group=group)
     else:  # gloo has no all_gather_into_tensor on some versions
         dist.all_gather(list(out.chunk(world)), t, group=group)
@@ -30,26 +59,92 @@ def _all_gather_bytes(dist, payload: bytes, device, group=None) -> list[bytes]:
 
 
 def shard_counts(dist, n_local: int, device, group=None) -> list[int]:
+    """All-gather of the 8-byte leaf counts; the host needs them (offsets plan the levels)."""
+    import torch
+    if _is_gpu(device):
+        world = dist.get_world_size(group)
+        src = torch.full((1,), int(n_local), dtype=torch.int64, device=device)
+        out = torch.empty(world, dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(out, src, group=group)
+        return [int(x) for x in out.tolist()]
     raw = _all_gather_bytes(dist, np.array([n_local], dtype=np.uint64).tobytes(), device, group)
     return [int(np.frombuffer(r, dtype=np.uint64)[0]) for r in raw]
 
 
-def sharded_root(tree, keys, values, dist, device="cpu", group=None, on_device: bool = False):
+def check_ranges(tree, counts: list[int], dist, device, group=None) -> None:
+    """Raise ValueError unless the shards hold disjoint contiguous key ranges ordered by rank (every
+    non-empty shard's last key < the next non-empty shard's first key; Rust str order = bytes order)."""
+    rank = dist.get_rank(group)
+    n = counts[rank]
+    ends = tree.keys_at([0, n - 1]) if n else [b"", b""]
+    lens = _all_gather_bytes(dist, np.array([len(ends[0]), len(ends[1])], dtype=np.uint64).tobytes(), device, group)
+    width = max(int(x) for r in lens for x in np.frombuffer(r, dtype=np.uint64)) or 1
+    pay = ends[0].ljust(width, b"\0") + ends[1].ljust(width, b"\0")
+    got = _all_gather_bytes(dist, pay, device, group)
+    prev_last, prev_rank = None, None
+    for r, (lr, raw) in enumerate(zip(lens, got)):
+        if counts[r] == 0:
+            continue
+        l0, l1 = (int(x) for x in np.frombuffer(lr, dtype=np.uint64))
+        first, last = raw[:l0], raw[width:width + l1]
+        if prev_last is not None and not prev_last < first:
+            raise ValueError(f"shard key ranges overlap or are out of rank order: rank {prev_rank} ends at "
+                             f"{prev_last!r}, rank {r} starts at {first!r} (the seam protocol needs contiguous "
+                             f"key ranges ordered by rank)")
+        prev_last, prev_rank = last, r
+
+
+def sharded_root(tree, keys, values, dist, device="cpu", group=None, on_device: bool = False,
+                 validate: bool = True):
     """Build this rank's shard of the global tree and return (global root or None, counts)."""
     rank = dist.get_rank(group)
-    world = dist.get_world_size(group)
     n_local = tree.shard_prepare(keys, values, on_device=on_device)
     counts = shard_counts(dist, n_local, device, group)
+    if validate:
+        check_ranges(tree, counts, dist, device, group)
     offset, total = sum(counts[:rank]), sum(counts)
     tree.shard_reduce(offset, total)
-    fringes = _all_gather_bytes(dist, tree.shard_fringe(), device, group)
-    root = tree.shard_combine(b"".join(fringes), world, total)
-    return root, counts
+    return shard_recombine_many([tree], dist, total, device, group)[0], counts
+
+
+def shard_recombine_many(trees, dist, total: int, device="cpu", group=None) -> list:
+    """Fringe all-gather + seam combine for k trees (replicas of one key range) in ONE collective:
+    after in-place updates (MerkleTree.upsert / upsert_device of keys in the rank's range: the dirty
+    path) or after shard_reduce. Returns the k global roots."""
+    trees = list(trees)
+    k = len(trees)
+    if k == 0:
+        return []
+    world = dist.get_world_size(group)
+    if _is_gpu(device) and all(hasattr(t, "shard_fringe_device") for t in trees):
+        import torch
+        src = _buf(device, "fr_in", k * FRINGE_BYTES)
+        dst = _buf(device, "fr_out", world * k * FRINGE_BYTES)
+        base = src.data_ptr()
+        for i, t in enumerate(trees):
+            t.shard_fringe_device(base + i * FRINGE_BYTES)  # complete on return
+        dist.all_gather_into_tensor(dst[:world * k * FRINGE_BYTES], src[:k * FRINGE_BYTES], group=group)
+        torch.cuda.current_stream(device).synchronize()  # the library runs on its own streams
+        out = dst.data_ptr()
+        return [t.shard_combine_device(out + i * FRINGE_BYTES, world, k * FRINGE_BYTES, total)
+                for i, t in enumerate(trees)]
+    blocks = _all_gather_bytes(dist, b"".join(t.shard_fringe() for t in trees), device, group)
+    return [t.shard_combine(b"".join(b[i * FRINGE_BYTES:(i + 1) * FRINGE_BYTES] for b in blocks), world, total)
+            for i, t in enumerate(trees)]
 
 
 def shard_recombine(tree, dist, total: int, device="cpu", group=None):
-    """After an in-place update of this rank's shard (MerkleTree.upsert / upsert_device of keys in its
-    range: the dirty path), all-gather the new fringes and recompute the seam nodes and global root."""
-    world = dist.get_world_size(group)
-    fringes = _all_gather_bytes(dist, tree.shard_fringe(), device, group)
-    return tree.shard_combine(b"".join(fringes), world, total)
+    """shard_recombine_many for one tree."""
+    return shard_recombine_many([tree], dist, total, device, group)[0]
+
+
+def sharded_diff(a, b, dist, device="cpu", group=None):
+    """diff_keys (merkle.rs:171-196) of two sharded trees with the same key-range partition: each rank
+    diffs its own range on the device (top-down when the shard plans match, merge-join when the key sets
+    differ), then the divergence counts are all-gathered (8 B/rank) so every rank knows where its keys
+    sit in the global sorted list (ranges are ordered by rank, so the concatenation is sorted).
+    Returns (this rank's packed keys (bytes array, offsets), global offset, global count)."""
+    rank = dist.get_rank(group)
+    raw, offs = a.diff_keys_packed(b)
+    counts = shard_counts(dist, len(offs) - 1, device, group)
+    return (raw, offs), sum(counts[:rank]), sum(counts)

@@ -133,6 +133,16 @@ def main():
     t = tree_of(zip(split_blob(kb, ko), split_blob(vb, vo)))
     fx["prefix_roots"] = {p: hx(t.prefix_root(p.encode())) for p in ["", "A", "Zz", "a", "-", "_", "zzzz", "q9"]}
 
+    # HASH [pattern] (server.rs:651-656): None / "" / "*" select every key, anything else is a prefix;
+    # a key that starts with '*' is reachable only through a real prefix such as "*a"
+    hk = [b"*", b"*a", b"*b", b"a*", b"ab", b"b", b"", b"**"]
+    hv = [b"v%d" % i for i in range(len(hk))]
+    th = tree_of(zip(hk, hv))
+    def hash_cmd(pat):
+        return th.prefix_root(b"" if pat in ("", "*") else pat.encode())
+    fx["hash_patterns"] = {"keys": [k.decode() for k in hk], "values": [v.decode() for v in hv],
+                           "roots": {p: hx(hash_cmd(p)) for p in ["", "*", "*a", "**", "a", "b", "c"]}}
+
     out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures.json")
     with open(out, "w") as f:
         json.dump(fx, f, indent=1, sort_keys=True)

@@ -6,7 +6,9 @@ from __future__ import annotations
 
 import struct
 
-from oracle.merkle_oracle import PyMerkleTree, node_hash
+import numpy as np
+
+from oracle.merkle_oracle import PyMerkleTree, node_hash, pack
 
 ENTRY = struct.Struct("<IIQ32s")  # level, valid, idx, digest  (MKV_FRINGE_ENTRY_BYTES = 48)
 MAX_ENTRIES = 130
@@ -34,6 +36,16 @@ class ModelShardTree:
         self.leaves = [h for _, h in t.leaves()]
         self.keys = [k for k, _ in t.leaves()]
         return len(self.leaves)
+
+    def keys_at(self, pos):
+        return [self.keys[int(p)] for p in pos]
+
+    def diff_keys_packed(self, other):
+        """merkle.rs:171-196 over this shard's leaves (the device path runs per rank the same way)."""
+        a, b = PyMerkleTree(), PyMerkleTree()
+        a.leaf_map.update(zip(self.keys, self.leaves))
+        b.leaf_map.update(zip(other.keys, other.leaves))
+        return pack(a.diff_keys(b))
 
     def upsert(self, keys, values):
         """Value-only batch on keys already in this shard (the dirty path's contract): leaves change in

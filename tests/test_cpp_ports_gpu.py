@@ -20,3 +20,14 @@ def test_cpp_reference_ports():
     print(r.stdout[-4000:])
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
     assert "56 tests, 0 failed" in r.stdout
+
+
+def test_cpp_boundary_const_call_sites():
+    """sync.rs:61-67 / server.rs:661-675 shapes: get_root_hash / diff_keys on const MerkleTree&."""
+    b = os.path.join(ROOT, "tests", "cpp", "test_boundary")
+    if not os.path.exists(b):
+        import __graft_entry__
+        __graft_entry__.build_cpp_tests()
+    r = subprocess.run([b], capture_output=True, text=True, timeout=300)
+    print(r.stdout[-4000:])
+    assert r.returncode == 0 and "boundary: ok" in r.stdout, r.stdout[-4000:] + r.stderr[-2000:]

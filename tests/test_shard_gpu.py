@@ -122,3 +122,115 @@ def test_sharded_two_processes_gloo_same_gpu():
     t = MerkleTree()
     t.build(allk, allv)
     assert [r for _, r in res] == [t.get_root_hash()] * world
+
+
+def test_fringe_device_combine_matches_host():
+    """mkv_shard_fringe_device / mkv_shard_combine_device (the RCCL path's device-resident buffers):
+    the same root as the host fringe path, also when two replicas' fringes share one gathered buffer
+    (stride = 2 x MKV_FRINGE_BYTES, what shard_recombine_many hands to the combine)."""
+    import torch
+
+    from merklekv_amd._lib import FRINGE_BYTES
+    n = 100_003
+    kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, n)
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    want = t.get_root_hash()
+    for world in (1, 3, 8):
+        step = n // world
+        shards = _shards(keys, vals, [step * i + 17 * i for i in range(1, world)])
+        trees = [MerkleTree() for _ in shards]
+        counts = [tr.shard_prepare(k, v) for tr, (k, v) in zip(trees, shards)]
+        N = sum(counts)
+        for r, tr in enumerate(trees):
+            tr.shard_reduce(sum(counts[:r]), N)
+        buf = torch.zeros(world * 2 * FRINGE_BYTES, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        for r, tr in enumerate(trees):  # rank r's block holds [replica 0 | replica 1] (same tree twice)
+            tr.shard_fringe_device(buf.data_ptr() + (2 * r) * FRINGE_BYTES)
+            tr.shard_fringe_device(buf.data_ptr() + (2 * r + 1) * FRINGE_BYTES)
+        host = b"".join(tr.shard_fringe() for tr in trees)
+        got = buf.view(world, 2, FRINGE_BYTES)[:, 0].cpu().numpy().tobytes()
+        assert got == host, world
+        for r, tr in enumerate(trees):
+            assert tr.shard_combine_device(buf.data_ptr(), world, 2 * FRINGE_BYTES, N) == want, (world, r)
+            assert tr.shard_combine_device(buf.data_ptr() + FRINGE_BYTES, world, 2 * FRINGE_BYTES, N) == want
+            assert tr.get_root_hash() == want
+
+
+def _worker_mixed(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.shard import sharded_diff, sharded_root
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ka, va, kb_, vb_ = _mixed_shard(rank, world)
+        A, B = MerkleTree(0), MerkleTree(0)
+        sharded_root(A, ka, va, dist, device="cpu")
+        sharded_root(B, kb_, vb_, dist, device="cpu")
+        (raw, offs), off, tot = sharded_diff(A, B, dist, device="cpu")
+        b = raw.tobytes()
+        q.put((rank, [b[int(offs[i]):int(offs[i + 1])] for i in range(len(offs) - 1)], off, tot))
+    finally:
+        dist.destroy_process_group()
+
+
+def _mixed_shard(rank, world, n=40_000):
+    """Replica A's and B's records of shard `rank` (key char 0 in the rank's range): B has value
+    changes, deletions and insertions inside the range, so the shard leaf counts differ."""
+    kb, ko, vb, vo = gen_records(DEFAULT_SEED, rank * n, n, shard=rank, nshards=world)
+    ka, va = split_blob(kb, ko), split_blob(vb, vo)
+    kb_, vb_ = [], []
+    for i, (k, v) in enumerate(zip(ka, va)):
+        if i % 211 == 5:
+            continue                        # deleted on B
+        kb_.append(k)
+        vb_.append(b"changed" + v[7:] if i % 97 == 3 else v)
+    nk, nko, nv, nvo = gen_records(DEFAULT_SEED, 10**9 + rank * 1000, 150, shard=rank, nshards=world)
+    kb_ += split_blob(nk, nko)              # inserted on B (same key range)
+    vb_ += split_blob(nv, nvo)
+    return ka, va, kb_, vb_
+
+
+def test_sharded_mixed_diff_two_processes_gloo_same_gpu():
+    """Sharded diff with key-set changes per shard on the HIP path (each rank merge-joins its range),
+    collectives on gloo: the rank-ordered concatenation equals the unsharded device diff and the oracle."""
+    import torch.multiprocessing as mp
+
+    from oracle import coracle
+    from oracle.merkle_oracle import pack
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_mixed, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    allA, allB = [[], []], [[], []]
+    for r in range(world):
+        ka, va, kb_, vb_ = _mixed_shard(r, world)
+        allA[0] += ka
+        allA[1] += va
+        allB[0] += kb_
+        allB[1] += vb_
+    A, B = MerkleTree(), MerkleTree()
+    A.build(*allA)
+    B.build(*allB)
+    want = A.diff_keys_bytes(B)
+    oa = coracle.OracleTree.build(*pack(allA[0]), *pack(allA[1]))
+    ob = coracle.OracleTree.build(*pack(allB[0]), *pack(allB[1]))
+    assert want == oa.diff(ob)
+    got = []
+    for _, keys, off, tot in res:
+        assert off == len(got) and tot == len(want)
+        got += keys
+    assert got == want
