@@ -4,10 +4,14 @@
 Default workload (`--workload build`, what the driver runs): a step = one full tree build (leaf hashing
 + key ordering + dedup + gathers + level reduction + root readback) over n synthetic records (32-B
 keys, 100-B values, generated on the device, already resident in HBM when the timed region starts).
-With N>1 ranks (torch.distributed.run, one process per GPU) each rank owns a contiguous key range of n
-records (weak scaling); the step adds the RCCL all-gathers of shard leaf counts and seam fringes and
-the on-device seam combine that yields the global root on every rank. `--records 125000000` at N=8 is
-configs[3] (1B keys over 8 GPUs); at N=1 it is one shard of it.
+N=1: n = 10M (configs[1]). N>1 ranks (torch.distributed.run, one process per GPU): each rank owns a
+contiguous key range of 125M records by default, so N=8 is configs[3] (1B keys over 8 GPUs; weak
+scaling); the step adds the RCCL all-gathers of shard leaf counts and seam fringes (device-resident
+buffers) and the on-device seam combine that yields the global root on every rank. The N=1 line also
+carries `anchor_125m` (the same build at 125M keys on one GPU: the per-GPU anchor of that curve),
+`diff_100m` (configs[2], both divergence modes, exactness vs construction), `configs0` (the 100K CPU
+config on the GPU) and the CPU baselines (cpu_ref: the reference's data structures, single thread;
+cpu_mt: all host cores).
 
 Other BASELINE configs (run explicitly; their JSON lines are committed under profiles/):
   --workload diff         configs[2]: two 100M-key replicas, (a) 0.1 % value-only divergence (top-down
@@ -105,14 +109,15 @@ class Ctx:
         torch.cuda.synchronize()
         return kb, ko, vb, vo
 
-    def build(self, tree, kb, ko, vb, vo, n):
-        """Full build of this rank's records; returns the global root (all ranks agree)."""
+    def build(self, tree, kb, ko, vb, vo, n, validate=False):
+        """Full build of this rank's records; returns the global root (all ranks agree). validate: also
+        check once that the shards hold contiguous key ranges ordered by rank (outside timed loops)."""
         if self.world == 1:
             tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
             return tree.get_root_hash(), n
         from merklekv_amd.shard import sharded_root
         root, counts = sharded_root(tree, (kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), None,
-                                    self.dist, device=self.coll, on_device=True)
+                                    self.dist, device=self.coll, on_device=True, validate=validate)
         return root, sum(counts)
 
     def check_roots_agree(self, root: bytes):
@@ -156,6 +161,216 @@ def random_values(torch, m, dev, gen):
 
 
 # ============================================================================================ build
+def leaf_roofline(n, leaf_avg_ms, launches):
+    """roofline of the dominant kernel (k_leaf_persist). achieved = 172 B/leaf x n / live launch time (HIP
+    events on the tree's stream, sort co-running); traffic and the VALU fractions come from the PMC file
+    of the same tree (profiles/pmc_leaf_hash.json, written by scripts/prof_summary.py)."""
+    achieved = LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_leaf_persist",
+           "bytes_per_leaf": LEAF_BYTES, "avg_launch_ms": leaf_avg_ms, "launches": launches,
+           "gb_per_s_hashed": (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9,
+           "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): the HBM frac ceiling is ~0.39; "
+                   "avg_launch_ms is measured live while the ordering kernels co-run on the aux stream"}
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_leaf_hash.json")
+    try:
+        pm = json.load(open(pmc_path))
+    except (OSError, ValueError):
+        pm = None
+    if pm and pm.get("n") == n:
+        out["traffic"] = pm.get("hbm_bytes_per_launch")
+        out["traffic_source"] = pm.get("source")
+        vi, gui, dur = pm.get("SQ_INSTS_VALU"), pm.get("GRBM_GUI_ACTIVE"), pm.get("avg_duration_us")
+        if vi and gui and dur:
+            # SQ_INSTS_VALU = wave64 VALU instructions per launch; capacity = 256 CU x 128 lanes per clock;
+            # clock from GRBM_GUI_ACTIVE (summed over the 8 XCDs) over the PMC launch's duration
+            f_clk = gui / 8 / (dur * 1e-6)
+            lane_ops = vi * 64
+            out["valu"] = {
+                "SQ_INSTS_VALU": vi, "GRBM_GUI_ACTIVE": gui, "pmc_avg_duration_us": dur,
+                "f_clk_ghz": f_clk / 1e9, "lane_ops_per_compression": lane_ops / (3 * n),
+                "frac": lane_ops / (256 * 128 * gui / 8),
+                "frac_live": lane_ops / (256 * 128 * f_clk * leaf_avg_ms * 1e-3),
+                "frac_live_nominal_clk": lane_ops / (256 * 128 * 2.4e9 * leaf_avg_ms * 1e-3),
+                "SQ_INSTS_SALU": pm.get("SQ_INSTS_SALU"), "source": pm.get("source"),
+                "note": "frac = SQ_INSTS_VALU x 64 / (256 CU x 128 lanes x GRBM_GUI_ACTIVE/8) over the PMC "
+                        "(serialised, standalone) launch; frac_live = the same instructions over the live "
+                        "co-run launch time at the PMC clock"}
+    return out
+
+
+def diff_secondary(ctx, tree, kb, ko, vb, vo, n, reps=5):
+    """10M value-only diff on the build's tree: per-rep host ms, device ms (HIP events) and pinned-pool
+    activity (hipHostMalloc/Free counts and host ms) — a slow rep names its cause in the line."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.merkle import pool_stats
+    vb2 = vb.clone()
+    v2 = vb2[: n * VLEN].view(n, VLEN)
+    idx = torch.arange(0, n, 1000, device=ctx.dev)
+    v2[idx, 0] = v2[idx, 0] ^ 1
+    torch.cuda.synchronize()
+    treeB = MerkleTree(ctx.local)
+    treeB.build_device(kb.data_ptr(), ko.data_ptr(), vb2.data_ptr(), vo.data_ptr(), n)
+    tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+    d = tree.diff_keys_view(treeB)  # warm
+    del d
+    torch.cuda.synchronize()
+    rep_ms, dev_ms, pool = [], [], []
+    tree.prof_enable(True)
+    for _ in range(reps):
+        tree.prof_reset()
+        p0 = pool_stats()
+        t0 = time.perf_counter()
+        d = tree.diff_keys_view(treeB)
+        rep_ms.append((time.perf_counter() - t0) * 1e3)
+        p1 = pool_stats()
+        dev_ms.append(tree.prof_read("diff")[0])
+        pool.append({"mallocs": p1["host_mallocs"] - p0["host_mallocs"], "frees": p1["host_frees"] - p0["host_frees"],
+                     "pin_ms": round(p1["pin_ms"] - p0["pin_ms"], 4)})
+        ndiv = len(d)
+        del d  # the result's pinned block goes back to the pool before the next rep
+    tree.prof_enable(False)
+    dt = sum(rep_ms) / reps / 1e3
+    del treeB, vb2
+    return {"union_keys": n, "divergent": ndiv, "expected_divergent": int(idx.numel()),
+            "ms": dt * 1e3, "ms_per_rep": [round(x, 4) for x in rep_ms],
+            "device_ms_per_rep": [round(x, 4) for x in dev_ms], "pool_per_rep": pool,
+            "ms_median": sorted(rep_ms)[reps // 2], "keys_per_s": n / dt,
+            "mode": "top-down (equal key sets), value-only 0.1%, incl. key-list D2H"}
+
+
+def incremental_secondary(ctx, tree, kb, ko, vb, vo, n, reps=5):
+    torch = ctx.torch
+    import numpy as np
+    m = max(1, n // 1000)
+    g = torch.Generator(device=ctx.dev)
+    g.manual_seed(7)
+    sel = torch.randint(0, n, (m,), device=ctx.dev, generator=g)
+    ukb = kb[: n * KLEN].view(n, KLEN)[sel].contiguous().view(-1)
+    uvb = random_values(torch, m, ctx.dev, g).contiguous().view(-1)
+    uko = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * KLEN
+    uvo = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * VLEN
+    torch.cuda.synchronize()
+    tree.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)  # warm
+    tree.prof_enable(True)
+    tree.prof_reset()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        tree.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
+    dt = (time.perf_counter() - t0) / reps
+    tree.prof_enable(False)
+    ums, ucnt = tree.prof_read("update")
+    upd = {"tree_keys": n, "batch": m, "ms": dt * 1e3, "device_ms": ums / max(ucnt, 1),
+           "update_keys_per_s": m / dt, "mode": "dirty-path rehash (value-only batch)"}
+    # key-set change: 0.1 % mixed batch (80 % value updates, 10 % removes, 10 % new keys) through the host
+    # API (mkv_tree_apply: batch sort + merge into the sorted leaves + reduction)
+    kv_h = kb[: n * KLEN].view(n, KLEN)[sel].cpu().numpy()
+    nnew = m // 10
+    nk, _, _, _ = ctx.records(nnew, idx0=10**12)
+    keys_h = np.concatenate([kv_h[: m - nnew], nk[: nnew * KLEN].view(nnew, KLEN).cpu().numpy()])
+    rm_h = np.zeros(m, np.uint8)
+    rm_h[int(m * 0.8): m - nnew] = 1
+    vals_h = np.frombuffer(bytes(ALPHA * 2)[:VLEN] * m, np.uint8).reshape(m, VLEN)
+    koff_h = np.arange(0, m + 1, dtype=np.uint64) * KLEN
+    voff_h = np.arange(0, m + 1, dtype=np.uint64) * VLEN
+    ks_times = []
+    for _ in range(3):
+        tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tree.apply((keys_h.reshape(-1), koff_h), (vals_h.reshape(-1), voff_h), rm_h)
+        ks_times.append(time.perf_counter() - t0)
+    dt = min(ks_times)
+    upd["keyset_batch"] = {"batch": m, "new": nnew, "removed": int(rm_h.sum()), "ms": dt * 1e3,
+                           "keys_per_s": m / dt, "leaves_after": len(tree),
+                           "mode": "batch sort + merge into sorted leaves + reduction (host blobs)"}
+    return upd
+
+
+def anchor_block(ctx, n, steps=5, warmup=2):
+    """The default build step at n keys on this one GPU (N=1 anchor of the 125M-per-rank SCALE curve)."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    kb, ko, vb, vo = ctx.records(n)
+    t = MerkleTree(ctx.local)
+    for _ in range(warmup):
+        t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+    t.prof_enable(True)
+    t.prof_reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+        root = t.get_root_hash()
+    el = time.perf_counter() - t0
+    lm, lc = t.prof_read("leaf_hash")
+    out = {"keys": n, "steps": steps, "ms_per_step": el / steps * 1e3, "leaves_per_s": n * steps / el,
+           "leaf_hash_ms": lm / max(lc, 1), "root": root.hex()}
+    del t, kb, vb
+    torch.cuda.empty_cache()
+    return out
+
+
+def configs0_block(ctx, reps=5):
+    """BASELINE configs[0] on the GPU: 100K-key tree A, replica B with 1 % 80/10/10 events, host blobs
+    (what a server snapshot hands over): build A, build B, diff."""
+    from merklekv_amd import MerkleTree
+    a_rec, b_rec = _configs0_records()
+    A, B = MerkleTree(ctx.local), MerkleTree(ctx.local)
+    tb, td = [], []
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        A.build((a_rec[0], a_rec[1]), (a_rec[2], a_rec[3]))
+        B.build((b_rec[0], b_rec[1]), (b_rec[2], b_rec[3]))
+        t1 = time.perf_counter()
+        d = A.diff_keys_packed(B)
+        t2 = time.perf_counter()
+        tb.append(t1 - t0)
+        td.append(t2 - t1)
+    tb, td = sorted(tb[1:]), sorted(td[1:])
+    return {"keys": len(a_rec[1]) - 1, "keys_b": len(b_rec[1]) - 1, "divergent": len(d[1]) - 1,
+            "build_two_trees_ms": tb[len(tb) // 2] * 1e3, "diff_ms": td[len(td) // 2] * 1e3,
+            "root_a": A.get_root_hash().hex(), "note": "host blobs incl. H2D; median of 5"}
+
+
+def _configs0_records():
+    """configs[0] records: 100K synthetic records and the 1 % 80/10/10 replica."""
+    import numpy as np
+    n, rate = 100_000, 10_000
+    from merklekv_amd.merkle import pack_blob
+    a = _gen_host(n)
+    keys = [a[0][int(a[1][i]):int(a[1][i + 1])].tobytes() for i in range(n)]
+    vals = [a[2][int(a[3][i]):int(a[3][i + 1])].tobytes() for i in range(n)]
+    # replica B: the oracle generator's plan, restated with numpy here (bench.py must not need tests/)
+    rng = np.random.default_rng(SEED & 0xFFFFFFFF)
+    cls = rng.integers(0, 1_000_000, size=n)
+    changed, deleted = cls < rate * 8 // 10, (cls >= rate * 8 // 10) & (cls < rate * 9 // 10)
+    bk = [k for k, dl in zip(keys, deleted) if not dl]
+    bv = [(b"#" + v[1:]) if ch else v for v, ch, dl in zip(vals, changed, deleted) if not dl]
+    n_ins = n * rate // 10_000_000
+    ins = _gen_host(n_ins, idx0=10**9)
+    bk += [ins[0][int(ins[1][i]):int(ins[1][i + 1])].tobytes() for i in range(n_ins)]
+    bv += [ins[2][int(ins[3][i]):int(ins[3][i + 1])].tobytes() for i in range(n_ins)]
+    pk, pv = pack_blob(bk), pack_blob(bv)
+    return a, (pk.bytes, pk.offsets, pv.bytes, pv.offsets)
+
+
+def _gen_host(n, idx0=0):
+    """Synthetic records generated on the device, copied to host numpy arrays (kb, koff, vb, voff)."""
+    import torch
+    from merklekv_amd.merkle import gen_records_device
+    kb = torch.empty(n * KLEN + 64, dtype=torch.uint8, device="cuda")
+    vb = torch.empty(n * VLEN + 64, dtype=torch.uint8, device="cuda")
+    ko = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    vo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    gen_records_device(torch.cuda.current_device(), SEED, idx0, n, KLEN, VLEN, kb.data_ptr(), ko.data_ptr(),
+                       vb.data_ptr(), vo.data_ptr())
+    torch.cuda.synchronize()
+    return (kb[: n * KLEN].cpu().numpy(), ko.cpu().numpy().astype("uint64"), vb[: n * VLEN].cpu().numpy(),
+            vo.cpu().numpy().astype("uint64"))
+
+
 def wl_build(ctx, args):
     torch = ctx.torch
     from merklekv_amd import MerkleTree
@@ -163,14 +378,18 @@ def wl_build(ctx, args):
     kb, ko, vb, vo = ctx.records(n)
     tree = MerkleTree(ctx.local)
 
+    first = True
     for _ in range(args.warmup):
-        root, N = ctx.build(tree, kb, ko, vb, vo, n)
+        root, N = ctx.build(tree, kb, ko, vb, vo, n, validate=first)
+        first = False
+    if first:  # no warmup: validate the shard ranges outside the timed region anyway
+        ctx.build(tree, kb, ko, vb, vo, n, validate=True)
     tree.prof_enable(True)
     tree.prof_reset()
     ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        root, N = ctx.build(tree, kb, ko, vb, vo, n)
+        root, N = ctx.build(tree, kb, ko, vb, vo, n, validate=False)
     ctx.barrier()
     t1 = time.perf_counter()
     tree.prof_enable(False)
@@ -182,128 +401,56 @@ def wl_build(ctx, args):
     leaf_ms, leaf_cnt = tree.prof_read("leaf_hash")
     groups = {g: tree.prof_read(g) for g in ("leaf_hash", "sort", "keycopy", "gather", "reduce", "total_build")}
     leaf_avg_ms = leaf_ms / max(leaf_cnt, 1)
-    achieved = LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9
-    hashed_gbs = (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9
-    valu_frac = SHA_OPS_PER_LEAF * n / (leaf_avg_ms * 1e-3) / 1e12 / VALU_PEAK_TOPS
+    roofline = leaf_roofline(n, leaf_avg_ms, leaf_cnt)
 
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_leaf_hash.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("n") == n:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
-    # ---------------- secondary, 1 GPU only: diff and incremental update on the same tree -------------
-    diff_info = upd_info = None
+    # ---------------- secondary, 1 GPU only ----------------
+    diff_info = upd_info = d100 = anchor = c0 = None
     if not args.no_diff and ctx.world == 1:
-        # replica B: same keys, value byte 0 flipped in every 1000th record (0.1 % value-only divergence)
-        vb2 = vb.clone()
-        v2 = vb2[: n * VLEN].view(n, VLEN)
-        idx = torch.arange(0, n, 1000, device=ctx.dev)
-        v2[idx, 0] = v2[idx, 0] ^ 1
-        torch.cuda.synchronize()
-        treeB = MerkleTree(ctx.local)
-        treeB.build_device(kb.data_ptr(), ko.data_ptr(), vb2.data_ptr(), vo.data_ptr(), n)
-        tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
-        d = tree.diff_keys_view(treeB)  # warm
-        reps = 5
-        torch.cuda.synchronize()
-        rep_ms = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            d = tree.diff_keys_view(treeB)
-            rep_ms.append((time.perf_counter() - t0) * 1e3)
-        dt = sum(rep_ms) / reps / 1e3
-        diff_info = {"union_keys": n, "divergent": len(d), "expected_divergent": int(idx.numel()),
-                     "ms": dt * 1e3, "ms_per_rep": [round(x, 4) for x in rep_ms], "ms_median": sorted(rep_ms)[reps // 2], "keys_per_s": n / dt,
-                     "mode": "top-down (equal key sets), value-only 0.1%, incl. key-list D2H"}
-        # incremental: 0.1 % value-update batch of existing keys (dirty path), configs[4]'s ratio
-        m = max(1, n // 1000)
-        g = torch.Generator(device=ctx.dev)
-        g.manual_seed(7)
-        sel = torch.randint(0, n, (m,), device=ctx.dev, generator=g)
-        ukb = kb[: n * KLEN].view(n, KLEN)[sel].contiguous().view(-1)
-        uvb = random_values(torch, m, ctx.dev, g).contiguous().view(-1)
-        uko = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * KLEN
-        uvo = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * VLEN
-        torch.cuda.synchronize()
-        tree.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)  # warm
-        tree.prof_enable(True)
-        tree.prof_reset()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            tree.upsert_device(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m)
-        dt = (time.perf_counter() - t0) / reps
-        tree.prof_enable(False)
-        ums, ucnt = tree.prof_read("update")
-        upd_info = {"tree_keys": n, "batch": m, "ms": dt * 1e3, "device_ms": ums / max(ucnt, 1),
-                    "update_keys_per_s": m / dt, "mode": "dirty-path rehash (value-only batch)"}
-        # key-set change: 0.1 % mixed batch (80 % value updates, 10 % removes, 10 % new keys) through the
-        # host API (mkv_tree_apply: batch sort + merge into the sorted leaves + reduction)
-        import numpy as np
-        sel_h = sel.cpu().numpy()
-        kv_h = kb[: n * KLEN].view(n, KLEN)[sel].cpu().numpy()
-        nnew = m // 10
-        nk, _, _, _ = ctx.records(nnew, idx0=10**12)
-        keys_h = np.concatenate([kv_h[: m - nnew], nk[: nnew * KLEN].view(nnew, KLEN).cpu().numpy()])
-        rm_h = np.zeros(m, np.uint8)
-        rm_h[int(m * 0.8): m - nnew] = 1
-        vals_h = np.frombuffer(bytes(ALPHA * 2)[:VLEN] * m, np.uint8).reshape(m, VLEN)
-        koff_h = np.arange(0, m + 1, dtype=np.uint64) * KLEN
-        voff_h = np.arange(0, m + 1, dtype=np.uint64) * VLEN
-        del sel_h
-        ks_times = []
-        for _ in range(3):
-            tree.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            tree.apply((keys_h.reshape(-1), koff_h), (vals_h.reshape(-1), voff_h), rm_h)
-            ks_times.append(time.perf_counter() - t0)
-        dt = min(ks_times)
-        upd_info["keyset_batch"] = {"batch": m, "new": nnew, "removed": int(rm_h.sum()), "ms": dt * 1e3,
-                                    "keys_per_s": m / dt, "leaves_after": len(tree),
-                                    "mode": "batch sort + merge into sorted leaves + reduction (host blobs)"}
-        del treeB, vb2
+        diff_info = diff_secondary(ctx, tree, kb, ko, vb, vo, n)
+        upd_info = incremental_secondary(ctx, tree, kb, ko, vb, vo, n)
+    del tree, kb, vb, ko, vo
+    torch.cuda.empty_cache()
+    if not args.no_diff and ctx.world == 1:
+        c0 = configs0_block(ctx)
+        d100 = diff_modes(ctx, args.diff_records, steps=5, warmup=2)
+        torch.cuda.empty_cache()
+        if args.anchor_records:
+            anchor = anchor_block(ctx, args.anchor_records)
 
     cpu = None
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_build(args.cpu_seconds)
 
     if ctx.rank == 0:
-        wl = ("configs[1]: 10M keys x 1 MI355X per rank, 32-B keys / 100-B values" if n == 10_000_000
-              else f"{n} keys per rank (configs[3] = 125M x 8 ranks), 32-B keys / 100-B values")
-        out = base_line(ctx, args, "Merkle build leaves/s (10M keys, full tree: hash+sort+reduce)", value,
+        wl = ("configs[1]: 10M keys x 1 MI355X, 32-B keys / 100-B values" if n == 10_000_000 and ctx.world == 1
+              else f"{n} keys per rank x {ctx.world} GPUs (configs[3] = 125M x 8 ranks = 1B keys), 32-B keys / 100-B values")
+        out = base_line(ctx, args, "Merkle build leaves/s (full tree: hash+sort+reduce)", value,
                         "leaves/s", ms_per_step, wl)
         out["root"] = root.hex() if root else None
-        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                           "kernel": "k_leaf_hash", "bytes_per_leaf": LEAF_BYTES,
-                           "avg_launch_ms": leaf_avg_ms, "launches": leaf_cnt,
-                           "gb_per_s_hashed": hashed_gbs,
-                           "valu_frac_model": valu_frac,
-                           "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): HBM frac ceiling ~0.39; "
-                                   "avg_launch_ms is measured while the sort co-runs on the aux stream"}
+        out["global_keys"] = N
+        out["roofline"] = roofline
         out["stage_ms_per_step"] = {g: (v[0] / max(v[1], 1) if g == "leaf_hash" else v[0] / args.steps)
                                     for g, v in groups.items()}
         out["diff"] = diff_info
         out["incremental"] = upd_info
+        out["diff_100m"] = d100
+        out["anchor_125m"] = anchor
+        out["configs0_gpu"] = c0
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
 
 
 # ============================================================================================= diff
-def wl_diff(ctx, args):
-    """configs[2]: two replicas with 0.1 % divergence; diff keys/s over the union of keys."""
+def diff_modes(ctx, n, steps, warmup):
+    """configs[2]: two n-key replicas per rank, 0.1 % divergence, (a) value-only -> top-down walk,
+    (b) mixed 80/10/10 change/delete/insert -> merge-join. Each output is checked against the constructed
+    divergent set (exact_vs_construction)."""
     torch = ctx.torch
     import numpy as np
     from merklekv_amd import MerkleTree
-    n = args.n
     kb, ko, vb, vo = ctx.records(n)
     A = MerkleTree(ctx.local)
-    ctx.build(A, kb, ko, vb, vo, n)
+    ctx.build(A, kb, ko, vb, vo, n, validate=True)
     ndiv = max(1, n // 1000)
     g = torch.Generator(device=ctx.dev)
     g.manual_seed(11 + ctx.rank)
@@ -335,15 +482,16 @@ def wl_diff(ctx, args):
         exp_sorted = exp_np[np.lexsort(exp_np.T[::-1])]
         del vb2, kB, vB, exp
         B = MerkleTree(ctx.local)
-        ctx.build(B, kBf, koB, vBf, voB, nB)
+        ctx.build(B, kBf, koB, vBf, voB, nB, validate=True)
         torch.cuda.synchronize()
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             d = A.diff_keys_view(B)
+            del d
         A.prof_enable(True)
         A.prof_reset()
         ctx.barrier()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             d = A.diff_keys_view(B)
         ctx.barrier()
         el = ctx.max_over_ranks(time.perf_counter() - t0)
@@ -352,43 +500,55 @@ def wl_diff(ctx, args):
         got = d.raw.reshape(-1, KLEN)
         exact = got.shape == exp_sorted.shape and bool((got == exp_sorted).all())
         union = ctx.sum_over_ranks(n + new)
-        res[mode] = {"union_keys": union, "divergent": ctx.sum_over_ranks(len(d)),
+        res[mode] = {"union_keys": union, "union_keys_per_rank": n + new, "divergent": ctx.sum_over_ranks(len(d)),
                      "expected_divergent": ctx.sum_over_ranks(int(exp_sorted.shape[0])),
-                     "exact_vs_construction": exact, "ms": el / args.steps * 1e3,
-                     "device_ms": dms / max(args.steps, 1),
-                     "keys_per_s": union * args.steps / el,
+                     "exact_vs_construction": exact, "ms": el / steps * 1e3,
+                     "device_ms": dms / max(steps, 1),
+                     "keys_per_s": union * steps / el,
                      "path": "top-down" if mode == "value_only" else "merge-join"}
-        del B, kBf, vBf
+        del d, B, kBf, vBf
         torch.cuda.empty_cache()
+    del A, kb, vb
+    torch.cuda.empty_cache()
+    return res
+
+
+def diff_roofline(res):
+    m = res["mixed"]
+    achieved = DIFF_BYTES_PER_KEY * m["union_keys_per_rank"] / (m["device_ms"] * 1e-3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_diff_merge.json")
+    try:
+        pm = json.load(open(pmc_path))
+        # the PMC file is per rank: it must describe this rank's diff (same union size)
+        if pm.get("union_keys") == m["union_keys_per_rank"]:
+            traffic = pm.get("hbm_bytes_per_diff")
+    except (OSError, ValueError):
+        pm = None
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "merge-join diff (mixed)",
+            "bytes_per_union_key": DIFF_BYTES_PER_KEY,
+            "note": "achieved = 80 B x union keys / device time of the whole diff call (partition, both passes, "
+                    "key gather); traffic = PMC HBM bytes of its merge-join kernels"}
+
+
+def wl_diff(ctx, args):
+    """configs[2]: two replicas with 0.1 % divergence; diff keys/s over the union of keys."""
+    res = diff_modes(ctx, args.n, args.steps, args.warmup)
     cpu = None
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_diff()
     if ctx.rank == 0:
         v = res["value_only"]
+        n = args.n
         wl = (f"configs[2]: {n // 1_000_000}M keys x 2 replicas per rank, 0.1% divergence; value = value-only "
               f"(top-down) union keys/s; 'mixed' = 80/10/10 change/delete/insert (merge-join)")
         out = base_line(ctx, args, "Merkle diff keys/s (union keys compared, 2 replicas, 0.1% divergence)",
                         v["keys_per_s"], "keys/s", v["ms"], wl)
-        achieved = DIFF_BYTES_PER_KEY * res["mixed"]["union_keys"] / (res["mixed"]["device_ms"] * 1e-3) / 1e9
-        # HBM bytes per merge-join diff from the PMC passes (scripts/prof_summary.py), same per-rank size only
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_diff_merge.json")
-        if os.path.exists(pmc_path):
-            try:
-                pm = json.load(open(pmc_path))
-                if pm.get("union_keys") == res["mixed"]["union_keys"] // ctx.world:
-                    traffic = pm.get("hbm_bytes_per_diff")
-            except Exception:
-                traffic = None
-        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "merge-join diff (mixed)",
-                           "bytes_per_union_key": DIFF_BYTES_PER_KEY,
-                           "note": "achieved = 80 B x union keys / device time of the whole diff call (partition, "
-                                   "both passes, key gather); traffic = PMC HBM bytes of its merge-join kernels"}
+        out["roofline"] = diff_roofline(res)
         out["diff"] = res
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
-    del A
 
 
 # ====================================================================================== incremental
@@ -397,13 +557,13 @@ def wl_incremental(ctx, args):
     each variant applies its own value-update batch (dirty path + seam recombine) + base diffed vs all 7."""
     torch = ctx.torch
     from merklekv_amd import MerkleTree
-    from merklekv_amd.shard import shard_recombine
+    from merklekv_amd.shard import shard_recombine_many
     n = args.n
     m = args.batch
     R = args.replicas
     kb, ko, vb, vo = ctx.records(n)
     base = MerkleTree(ctx.local)
-    root, N = ctx.build(base, kb, ko, vb, vo, n)
+    root, N = ctx.build(base, kb, ko, vb, vo, n, validate=True)
     del vb, vo
     torch.cuda.empty_cache()
     variants = [base.clone() for _ in range(R - 1)]
@@ -425,9 +585,8 @@ def wl_incremental(ctx, args):
 
     def step():
         MerkleTree.upsert_device_many(variants, ptrs)
-        if ctx.world > 1:
-            for t in variants:
-                shard_recombine(t, ctx.dist, N, device=ctx.coll)
+        if ctx.world > 1:  # all 7 variants' fringes in ONE all-gather, combined on the device
+            shard_recombine_many(variants, ctx.dist, N, device=ctx.coll)
         return base.diff_keys_many_view(variants)  # one shared top-down walk (mkv_tree_diff_many)
 
     for _ in range(args.warmup):
@@ -462,24 +621,76 @@ def wl_incremental(ctx, args):
 
 
 # ===================================================================================== CPU baselines
+def _host_threads() -> int:
+    """Host threads this process may use: OMP_NUM_THREADS when set (the GPU box sets 16: its CPU share),
+    else the affinity mask."""
+    try:
+        return max(1, int(os.environ.get("OMP_NUM_THREADS", "")))
+    except ValueError:
+        return max(1, len(os.sched_getaffinity(0)))
+
+
 def cpu_baseline_build(target_s: float):
-    """Oracle (C restatement of merkle.rs, single thread, SHA-NI like sha2 0.10.9) on a bounded sample."""
-    import ctypes
+    """CPU baselines on the GPU box's host (oracle/: test infrastructure, never inside a timed GPU region).
+    value = cpu_ref: the reference's own data structures (SipHash HashMap of heap Strings, node tree with
+    the per-level deep clones of merkle.rs:107-108), single thread, SHA-NI like sha2 0.10.9 — one bulk
+    build (= n x (compute_leaf_hash + map insert) + ONE rebuild). Beside it: the reference's real API
+    cost (n x insert, a rebuild per insert, O(n^2 log n)) timed at 1K/2K and extrapolated; cpu_mt (all
+    host threads); the lean single-thread port; and configs[0] (100K build + 1 % diff) per flavour."""
+    import math
 
     from oracle import coracle as co
     shani = co.set_backend(1)
     try:
-        buf = (ctypes.c_uint8 * 32)()
-        n0 = 100_000
-        kb, ko, vb, vo = co.gen_records(SEED, 0, n0)
-        secs = co.lib().orc_bench_build(kb.ctypes.data, ko.ctypes.data, vb.ctypes.data, vo.ctypes.data, n0, buf)
-        n = int(min(8_000_000, max(n0, n0 / secs * target_s)))
-        kb, ko, vb, vo = co.gen_records(SEED, 0, n)
-        secs = co.lib().orc_bench_build(kb.ctypes.data, ko.ctypes.data, vb.ctypes.data, vo.ctypes.data, n, buf)
-        return {"value": n / secs, "unit": "leaves/s", "cores": 1, "kind": "port",
-                "sample": f"one bulk build (= one merkle.rs rebuild) of {n} synthetic 32B/100B records, "
-                          f"{secs:.1f} s, sha={'SHA-NI' if shani else 'portable'}",
-                "cpu_model": _cpu_model()}
+        thr = _host_threads()
+        # ---- cpu_ref bulk build, sized to ~40 % of the budget
+        kb, ko, vb, vo = co.gen_records(SEED, 0, 50_000)
+        s0, _ = co.ref_bulk(kb, ko, vb, vo)
+        n_ref = int(min(4_000_000, max(50_000, 50_000 / s0 * target_s * 0.4)))
+        kb, ko, vb, vo = co.gen_records(SEED, 0, n_ref)
+        s_ref, root_ref = co.ref_bulk(kb, ko, vb, vo)
+        # ---- cpu_mt + the lean port on the same sample
+        s_mt, root_mt = co.mt_build(kb, ko, vb, vo, thr)
+        n_lean = min(n_ref, 2_000_000)
+        buf = (__import__("ctypes").c_uint8 * 32)()
+        s_lean = co.lib().orc_bench_build(kb.ctypes.data, ko.ctypes.data, vb.ctypes.data, vo.ctypes.data, n_lean, buf)
+        assert root_mt == root_ref, "cpu_mt and cpu_ref disagree"
+        del kb, vb
+        # ---- the reference API: n x insert, each rebuilding (sync.rs:110-115, server.rs:664-667)
+        loop = {}
+        for m in (1000, 2000):
+            a = co.gen_records(SEED, 0, m)
+            loop[m] = co.ref_insert_loop(*a)[0]
+        # sum_{i<=n} rebuild(i) ~ c * n^2 log2 n: fit c on 2K, extrapolate
+        c = loop[2000] / (2000 ** 2 * math.log2(2000))
+        est = {k: c * k * k * math.log2(k) for k in (100_000, 10_000_000)}
+        # ---- configs[0]: 100K build of A and B + diff, per flavour
+        (ak, ako, av, avo), (bk, bko, bv, bvo) = _configs0_records()
+        ra, _ = co.ref_bulk(ak, ako, av, avo)
+        rb, _ = co.ref_bulk(bk, bko, bv, bvo)
+        rd, rcnt = co.ref_diff((ak, ako, av, avo), (bk, bko, bv, bvo))
+        ma, _ = co.mt_build(ak, ako, av, avo, thr)
+        mb, _ = co.mt_build(bk, bko, bv, bvo, thr)
+        ta, tb = co.OracleTree.build(ak, ako, av, avo), co.OracleTree.build(bk, bko, bv, bvo)
+        md, mcnt = co.mt_diff(ta, tb, thr)
+        assert rcnt == mcnt == len(ta.diff(tb)), "configs[0] diff counts disagree"
+        model = _cpu_model()
+        return {"value": n_ref / s_ref, "unit": "leaves/s", "cores": 1, "kind": "port",
+                "sample": f"cpu_ref: one bulk build of {n_ref} synthetic 32B/100B records with the reference's data "
+                          f"structures (SipHash HashMap, per-level deep-cloned node tree), {s_ref:.1f} s, "
+                          f"sha={'SHA-NI' if shani else 'portable'}",
+                "cpu_model": model,
+                "flavours": {
+                    "cpu_ref": {"leaves_per_s": n_ref / s_ref, "cores": 1, "records": n_ref, "s": s_ref},
+                    "cpu_mt": {"leaves_per_s": n_ref / s_mt, "cores": thr, "records": n_ref, "s": s_mt},
+                    "lean_port_1t": {"leaves_per_s": n_lean / s_lean, "cores": 1, "records": n_lean, "s": s_lean,
+                                     "note": "round-1 baseline: qsort index + flat levels, no node clones"}},
+                "insert_loop": {"s_1k": loop[1000], "s_2k": loop[2000], "model": "c * n^2 log2 n fitted at 2K",
+                                "est_s_100k": est[100_000], "est_s_10m": est[10_000_000],
+                                "note": "the reference API as its callers use it (insert rebuilds every time)"},
+                "configs0": {"keys": len(ako) - 1, "keys_b": len(bko) - 1, "divergent": rcnt,
+                             "cpu_ref": {"build_two_trees_s": ra + rb, "diff_s": rd, "cores": 1},
+                             "cpu_mt": {"build_two_trees_s": ma + mb, "diff_s": md, "cores": thr}}}
     finally:
         co.set_backend(0)
 
@@ -553,10 +764,15 @@ def main():
     ap.add_argument("--replicas", type=int, default=8, help="incremental: base + variants")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
-    ap.add_argument("--no-diff", action="store_true")
+    ap.add_argument("--no-diff", action="store_true", help="build workload: skip the secondary blocks")
+    ap.add_argument("--diff-records", type=int, default=100_000_000, help="build workload: diff_100m keys")
+    ap.add_argument("--anchor-records", type=int, default=125_000_000,
+                    help="build workload at N=1: anchor build size (0 = skip)")
     args = ap.parse_args()
     if args.n is None:
-        args.n = {"build": 10_000_000, "diff": 100_000_000, "incremental": 125_000_000}[args.workload]
+        multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
+        args.n = {"build": 125_000_000 if multi else 10_000_000, "diff": 100_000_000,
+                  "incremental": 125_000_000}[args.workload]
     ctx = Ctx()
     {"build": wl_build, "diff": wl_diff, "incremental": wl_incremental}[args.workload](ctx, args)
     ctx.finish()

@@ -60,8 +60,50 @@ def lib():
         L.orc_bench_build.restype = C.c_double
         L.orc_bench_leaf_hash.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_void_p]
         L.orc_bench_leaf_hash.restype = C.c_double
+        for name in ("orc_ref_bulk", "orc_ref_insert_loop"):
+            getattr(L, name).argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_void_p]
+            getattr(L, name).restype = C.c_double
+        L.orc_ref_diff.argtypes = [C.c_void_p] * 4 + [C.c_uint64] + [C.c_void_p] * 4 + [C.c_uint64, u64p]
+        L.orc_ref_diff.restype = C.c_double
+        L.orc_mt_build.argtypes = [C.c_void_p] * 4 + [C.c_uint64, C.c_int, C.c_void_p]
+        L.orc_mt_build.restype = C.c_double
+        L.orc_mt_diff.argtypes = [C.c_void_p, C.c_void_p, C.c_int, u64p]
+        L.orc_mt_diff.restype = C.c_double
         _LIB = L
     return _LIB
+
+
+def ref_bulk(kb, ko, vb, vo):
+    """cpu_ref one bulk build (reference data structures, one rebuild): (seconds, root)."""
+    out = (C.c_uint8 * 32)()
+    s = lib().orc_ref_bulk(_p(kb), _p(ko), _p(vb), _p(vo), len(ko) - 1, out)
+    return s, bytes(out) if len(ko) > 1 else None
+
+
+def ref_insert_loop(kb, ko, vb, vo):
+    """cpu_ref new() + n x insert() (a rebuild per insert): (seconds, root)."""
+    out = (C.c_uint8 * 32)()
+    s = lib().orc_ref_insert_loop(_p(kb), _p(ko), _p(vb), _p(vo), len(ko) - 1, out)
+    return s, bytes(out) if len(ko) > 1 else None
+
+
+def ref_diff(a, b):
+    """cpu_ref diff_keys between two record sets a, b = (kb, ko, vb, vo): (seconds, count)."""
+    c = C.c_uint64()
+    s = lib().orc_ref_diff(*(_p(x) for x in a), len(a[1]) - 1, *(_p(x) for x in b), len(b[1]) - 1, C.byref(c))
+    return s, c.value
+
+
+def mt_build(kb, ko, vb, vo, threads):
+    out = (C.c_uint8 * 32)()
+    s = lib().orc_mt_build(_p(kb), _p(ko), _p(vb), _p(vo), len(ko) - 1, threads, out)
+    return s, bytes(out) if len(ko) > 1 else None
+
+
+def mt_diff(ta: "OracleTree", tb: "OracleTree", threads):
+    c = C.c_uint64()
+    s = lib().orc_mt_diff(ta.h, tb.h, threads, C.byref(c))
+    return s, c.value
 
 
 def _p(a: np.ndarray):

@@ -86,6 +86,21 @@ double orc_bench_build(const uint8_t *kb, const uint64_t *koff, const uint8_t *v
 double orc_bench_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff,
                            uint64_t n, uint8_t *digests_out);
 
+/* ---- timed CPU baselines (cpu_baselines.c; bench.py cpu_baseline leg) ----
+ * cpu_ref: the reference's data structures (SipHash HashMap of heap Strings / Vecs, deep-cloned node
+ * tree per level, merkle.rs:52-121, :171-196), single thread. cpu_mt: optimised, `threads` host threads.
+ * Each returns seconds of the timed part. */
+double orc_ref_bulk(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                    uint8_t root_out[32]);
+double orc_ref_insert_loop(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff,
+                           uint64_t n, uint8_t root_out[32]);
+double orc_ref_diff(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                    const uint8_t *kb2, const uint64_t *koff2, const uint8_t *vb2, const uint64_t *voff2, uint64_t n2,
+                    uint64_t *count);
+double orc_mt_build(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                    int threads, uint8_t root_out[32]);
+double orc_mt_diff(const orc_tree *a, const orc_tree *b, int threads, uint64_t *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,14 +45,17 @@ def main():
     summary = {}
     for k, d in agg.items():
         e = {c: sum(v for v, _ in vals) / len(vals) for c, vals in d.items()}
+        for c, vals in d.items():  # launch duration of the pass that collected c (passes differ)
+            e[c + "@dur_us"] = sum(t for _, t in vals) / len(vals) / 1e3
         e["avg_duration_us"] = sum(t for vals in d.values() for _, t in vals) / sum(len(v) for v in d.values()) / 1e3
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
             e["hbm_bytes_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
         if "GRBM_GUI_ACTIVE" in e:
-            e["eff_clock_ghz"] = e["GRBM_GUI_ACTIVE"] / 8 / (e["avg_duration_us"] * 1e-6) / 1e9
+            gdur = e["GRBM_GUI_ACTIVE@dur_us"]
+            e["eff_clock_ghz"] = e["GRBM_GUI_ACTIVE"] / 8 / (gdur * 1e-6) / 1e9
             if "SQ_INSTS_VALU" in e:
-                cycles = e["avg_duration_us"] * 1e-6 * e["eff_clock_ghz"] * 1e9
-                e["valu_busy_frac"] = e["SQ_INSTS_VALU"] * 2 / 1024 / cycles  # wave64 VALU = 2 cycles on SIMD32
+                # VALU issue capacity: 256 CUs x 4 SIMDs, one wave64 instruction per 2 cycles per SIMD
+                e["valu_busy_frac"] = e["SQ_INSTS_VALU"] * 2 / 1024 / (e["GRBM_GUI_ACTIVE"] / 8)
         if "SQ_WAIT_INST_ANY" in e and "SQ_WAVE_CYCLES" in e:
             e["issue_stall_frac"] = e["SQ_WAIT_INST_ANY"] / e["SQ_WAVE_CYCLES"]
         summary[k] = e
@@ -60,11 +63,17 @@ def main():
     lh = summary.get("k_leaf_persist") or summary.get("k_leaf_hash")
     diff_run = "k_diff_pass1" in summary  # the diff workload also builds trees: keep the build's leaf figure
     if lh and "hbm_bytes_corrected" in lh and not diff_run:
-        json.dump({"n": n, "hbm_bytes_per_launch": lh["hbm_bytes_corrected"], "source": f"{tag}_pmc.json",
-                   "kernel": "k_leaf_persist" if "k_leaf_persist" in summary else "k_leaf_hash",
-                   "algorithmic_bytes_per_launch": 172 * n,
-                   "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes"},
-                  open(os.path.join(OUT, "pmc_leaf_hash.json"), "w"), indent=1)
+        rec = {"n": n, "hbm_bytes_per_launch": lh["hbm_bytes_corrected"], "source": f"{tag}_pmc.json",
+               "kernel": "k_leaf_persist" if "k_leaf_persist" in summary else "k_leaf_hash",
+               "algorithmic_bytes_per_launch": 172 * n,
+               "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes; VALU counters per "
+                       "launch with the duration of the pass that collected GRBM_GUI_ACTIVE"}
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
+            if c in lh:
+                rec[c] = lh[c]
+        if "GRBM_GUI_ACTIVE" in lh:
+            rec["avg_duration_us"] = lh["GRBM_GUI_ACTIVE@dur_us"]
+        json.dump(rec, open(os.path.join(OUT, "pmc_leaf_hash.json"), "w"), indent=1)
     if all(k in summary and "hbm_bytes_corrected" in summary[k] for k in MERGE_KERNELS):
         per = {k: summary[k]["hbm_bytes_corrected"] for k in MERGE_KERNELS}
         json.dump({"union_keys": n, "hbm_bytes_per_diff": sum(per.values()), "per_kernel": per,

@@ -140,3 +140,37 @@ def test_upsert_remove_c_oracle(oracle_lib):
         py.remove(k)
     assert t3.root() == py.get_root_hash()
     assert len(t3) == 49
+
+
+def test_cpu_baselines_match_oracle(oracle_lib):
+    """The timed CPU baselines (oracle/cpu_baselines.c) compute the reference's results: cpu_ref's
+    bulk build and insert loop (reference data structures, deep-cloned node tree) and cpu_mt's
+    parallel build give the oracle root; both diffs give the oracle's divergent-key count."""
+    from oracle.merkle_oracle import pack, split_blob
+    from tests.golden.make_golden import replica_b
+    co = oracle_lib
+    for n in (1, 2, 3, 257, 5000):
+        kb, ko, vb, vo = co.gen_records(0x4D65726B6C654B56, 0, n)
+        want = co.OracleTree.build(kb, ko, vb, vo).root()
+        assert co.ref_bulk(kb, ko, vb, vo)[1] == want, n
+        assert co.mt_build(kb, ko, vb, vo, 4)[1] == want, n
+        assert co.mt_build(kb, ko, vb, vo, 1)[1] == want, n
+        if n <= 257:
+            assert co.ref_insert_loop(kb, ko, vb, vo)[1] == want, n
+    # duplicates: last write wins in every flavour
+    keys = [b"k2", b"k1", b"k2", b"k3", b"k1", b"k2"]
+    vals = [b"a", b"b", b"c", b"d", b"e", b"f"]
+    (kb, ko), (vb, vo) = pack(keys), pack(vals)
+    want = co.OracleTree.build(kb, ko, vb, vo).root()
+    assert co.ref_bulk(kb, ko, vb, vo)[1] == co.ref_insert_loop(kb, ko, vb, vo)[1] == want
+    assert co.mt_build(kb, ko, vb, vo, 3)[1] == want
+    # configs[0] shape at 20K: 1 % 80/10/10 replica
+    n = 20_000
+    kb, ko, vb, vo = co.gen_records(0x4D65726B6C654B56, 0, n)
+    bk, bv = replica_b(split_blob(kb, ko), split_blob(vb, vo), 0x4D65726B6C654B56, 10_000)
+    (kb2, ko2), (vb2, vo2) = pack(bk), pack(bv)
+    ta, tb = co.OracleTree.build(kb, ko, vb, vo), co.OracleTree.build(kb2, ko2, vb2, vo2)
+    want = len(ta.diff(tb))
+    assert co.ref_diff((kb, ko, vb, vo), (kb2, ko2, vb2, vo2))[1] == want
+    for th in (1, 3, 8):
+        assert co.mt_diff(ta, tb, th)[1] == want
