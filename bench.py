@@ -204,7 +204,7 @@ def diff_secondary(ctx, tree, kb, ko, vb, vo, n, reps=5):
     activity (hipHostMalloc/Free counts and host ms) — a slow rep names its cause in the line."""
     torch = ctx.torch
     from merklekv_amd import MerkleTree
-    from merklekv_amd.merkle import pool_stats
+    from merklekv_amd.merkle import debug_trace, pool_stats
     vb2 = vb.clone()
     v2 = vb2[: n * VLEN].view(n, VLEN)
     idx = torch.arange(0, n, 1000, device=ctx.dev)
@@ -216,18 +216,20 @@ def diff_secondary(ctx, tree, kb, ko, vb, vo, n, reps=5):
     d = tree.diff_keys_view(treeB)  # warm
     del d
     torch.cuda.synchronize()
-    rep_ms, dev_ms, pool = [], [], []
+    rep_ms, dev_ms, pool, traces, thr = [], [], [], [], []
     tree.prof_enable(True)
     for _ in range(reps):
         tree.prof_reset()
-        p0 = pool_stats()
+        p0, c0 = pool_stats(), _cgroup_cpu()
         t0 = time.perf_counter()
         d = tree.diff_keys_view(treeB)
         rep_ms.append((time.perf_counter() - t0) * 1e3)
-        p1 = pool_stats()
+        p1, c1 = pool_stats(), _cgroup_cpu()
+        traces.append(debug_trace())
         dev_ms.append(tree.prof_read("diff")[0])
         pool.append({"mallocs": p1["host_mallocs"] - p0["host_mallocs"], "frees": p1["host_frees"] - p0["host_frees"],
                      "pin_ms": round(p1["pin_ms"] - p0["pin_ms"], 4)})
+        thr.append({k: c1[k] - c0[k] for k in c0} if c0 and c1 else None)
         ndiv = len(d)
         del d  # the result's pinned block goes back to the pool before the next rep
     tree.prof_enable(False)
@@ -236,6 +238,7 @@ def diff_secondary(ctx, tree, kb, ko, vb, vo, n, reps=5):
     return {"union_keys": n, "divergent": ndiv, "expected_divergent": int(idx.numel()),
             "ms": dt * 1e3, "ms_per_rep": [round(x, 4) for x in rep_ms],
             "device_ms_per_rep": [round(x, 4) for x in dev_ms], "pool_per_rep": pool,
+            "host_trace_per_rep": traces, "cgroup_cpu_per_rep": thr,
             "ms_median": sorted(rep_ms)[reps // 2], "keys_per_s": n / dt,
             "mode": "top-down (equal key sets), value-only 0.1%, incl. key-list D2H"}
 
@@ -286,6 +289,19 @@ def incremental_secondary(ctx, tree, kb, ko, vb, vo, n, reps=5):
                            "keys_per_s": m / dt, "leaves_after": len(tree),
                            "mode": "batch sort + merge into sorted leaves + reduction (host blobs)"}
     return upd
+
+
+def _cgroup_cpu():
+    """cgroup v2 CPU accounting of this container (nr_throttled / throttled_usec / usage_usec), or None."""
+    try:
+        d = {}
+        for line in open("/sys/fs/cgroup/cpu.stat"):
+            k, v = line.split()
+            if k in ("usage_usec", "nr_throttled", "throttled_usec", "nr_periods"):
+                d[k] = int(v)
+        return d
+    except (OSError, ValueError):
+        return None
 
 
 def anchor_block(ctx, n, steps=5, warmup=2):

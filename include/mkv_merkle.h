@@ -194,6 +194,9 @@ mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint
  * bytes pinned in total, host ns spent in both, blocks pooled now, bytes pooled now}. */
 mkv_status mkv_pool_trim(void);
 mkv_status mkv_pool_stats(uint64_t out6[6]);
+/* Host phase trace of the last diff call on this thread: "label=µs;label=µs;..." (µs since the call
+ * started; labels at the blocking points: device waits, readbacks, copies). *len = full length. */
+mkv_status mkv_debug_trace(char *buf, uint64_t cap, uint64_t *len);
 /* Library version string. */
 const char *mkv_version(void);
 

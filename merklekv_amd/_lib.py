@@ -27,7 +27,7 @@ EXPORTS = [
     "mkv_shard_reduce", "mkv_shard_fringe", "mkv_shard_combine", "mkv_prof_enable", "mkv_prof_reset",
     "mkv_prof_read", "mkv_gen_records_device", "mkv_leaf_digests", "mkv_version",
     "mkv_tree_build_digests", "mkv_tree_hash_pattern", "mkv_shard_fringe_device", "mkv_shard_combine_device",
-    "mkv_pool_trim", "mkv_pool_stats",
+    "mkv_pool_trim", "mkv_pool_stats", "mkv_debug_trace",
 ]
 
 
@@ -97,6 +97,7 @@ def lib():
         "mkv_shard_combine_device": ([vp, vp, u32, u64, u64, vp, P(i32)], i32),
         "mkv_pool_trim": ([], i32),
         "mkv_pool_stats": ([vp], i32),
+        "mkv_debug_trace": ([vp, u64, P(u64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

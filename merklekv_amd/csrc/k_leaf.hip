@@ -148,6 +148,76 @@ __device__ __forceinline__ void hash_fast(const uint32_t *lds, uint32_t kword, u
     }
 }
 
+// Compile-time record shape (the configs' 32-B keys / 100-B values): every message word's source is
+// known while compiling — a constant (length fields, 0x80 terminator, zero padding, bit length) or one
+// LDS word at a fixed offset. The constant words are folded at compile time (sha256.hpp
+// sha_compress_known): K + W literals, schedule terms summed in advance, round 0 of the first block
+// computed by the compiler. Block 3 of a 140-B leaf carries 13 constant words. No runtime selection
+// chain, no scalar branches.
+template <uint32_t K0, uint32_t V0>
+struct LeafShape {
+    static constexpr uint32_t kw = K0 / 4, vw = V0 / 4;
+    static constexpr uint32_t vbeg = kw + 2, vend = kw + 2 + vw;  // value words [vbeg, vend); vend = L/4
+    static constexpr uint32_t L = 8 + K0 + V0;
+    static constexpr uint32_t NB = (L + 9 + 63) / 64;
+    static constexpr uint64_t bits = (uint64_t)L * 8;
+    // kind of message word g: 0 constant (value in *c), 1 key word g-1, 2 value word g-vbeg
+    static constexpr int kind(uint32_t g, uint32_t *c) {
+        if (g / 16 == NB - 1 && g % 16 == 14) return *c = (uint32_t)(bits >> 32), 0;
+        if (g / 16 == NB - 1 && g % 16 == 15) return *c = (uint32_t)bits, 0;
+        if (g == 0) return *c = K0, 0;
+        if (g <= kw) return 1;
+        if (g == kw + 1) return *c = V0, 0;
+        if (g < vend) return 2;
+        return *c = (g == vend ? 0x80000000u : 0u), 0;
+    }
+};
+template <uint32_t K0, uint32_t V0, uint32_t BLK>
+struct LeafBlockKnown {
+    static constexpr MsgKnown msg() {
+        MsgKnown m{};
+        for (uint32_t i = 0; i < 16; ++i) {
+            uint32_t c = 0;
+            if (LeafShape<K0, V0>::kind(BLK * 16 + i, &c) == 0) {
+                m.mask |= 1u << i;
+                m.val[i] = c;
+            }
+        }
+        return m;
+    }
+    static constexpr SchedKnown value = expand_known(msg());
+};
+
+template <bool SHORT, uint32_t K0, uint32_t V0, uint32_t BLK>
+__device__ __forceinline__ void hash_fixed_block(const uint32_t *lds, uint32_t kword, uint32_t vword, uint32_t out[8]) {
+    using Sh = LeafShape<K0, V0>;
+    uint32_t w[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        uint32_t c = 0;
+        const uint32_t g = BLK * 16 + i;
+        const int kd = Sh::kind(g, &c);
+        w[i] = kd == 1 ? bswap32(lds[kword + g - 1]) : kd == 2 ? bswap32(lds[vword + g - Sh::vbeg]) : c;
+    }
+    sha_compress_known<SHORT, LeafBlockKnown<K0, V0, BLK>, BLK == 0>(out, w);
+    if constexpr (BLK + 1 < Sh::NB) hash_fixed_block<SHORT, K0, V0, BLK + 1>(lds, kword, vword, out);
+}
+
+template <bool SHORT, uint32_t K0, uint32_t V0>
+__device__ __forceinline__ void hash_fixed(const uint32_t *lds, uint32_t kword, uint32_t vword, uint32_t out[8]) {
+    static_assert(K0 % 4 == 0 && V0 % 4 == 0, "fast-path shapes are word multiples");
+    sha_init(out);
+    hash_fixed_block<SHORT, K0, V0, 0>(lds, kword, vword, out);
+}
+
+// Wave-uniform dispatch of the fast path: specialised shapes first, the runtime-shape loop otherwise.
+template <bool SHORT>
+__device__ __forceinline__ void hash_fast_any(const uint32_t *lds, uint32_t kword, uint32_t vword, uint32_t K0,
+                                              uint32_t V0, uint32_t out[8]) {
+    if (K0 == 32 && V0 == 100) hash_fixed<SHORT, 32, 100>(lds, kword, vword, out);
+    else hash_fast<SHORT>(lds, kword, vword, K0, V0, out);
+}
+
 template <bool SHORT>
 __global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                   const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
@@ -312,8 +382,8 @@ __global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict_
                 const uint32_t K0 = __shfl(klen, 0), V0 = __shfl(vlen, 0);
                 const bool mine = klen == K0 && vlen == V0 && ((K0 | V0 | kbyte | vbyte) & 3) == 0;
                 if (__all(mine)) {
-                    hash_fast<SHORT>(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
-                                     __builtin_amdgcn_readfirstlane(V0), st);
+                    hash_fast_any<SHORT>(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
+                                         __builtin_amdgcn_readfirstlane(V0), st);
                 } else {
                     LdsSrc src{lds, kbyte, vbyte};
                     hash_generic<SHORT>(src, klen, vlen, st);

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace mkv {
 
 __host__ __device__ constexpr uint32_t k256(int t) {
@@ -124,6 +126,119 @@ __device__ __forceinline__ void sha_round(uint32_t &a, uint32_t &b, uint32_t &c,
     }
 }
 
+// Round whose message word is a compile-time constant: kw = K[t] + W[t] is one literal, so h + K + W is a
+// plain v_add (fast) instead of a v_add3 with a materialised zero or constant.
+template <bool SHORT>
+__device__ __forceinline__ void sha_round_kw(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                             uint32_t &f, uint32_t &g, uint32_t &h, uint32_t kw) {
+    if constexpr (SHORT) {
+        const uint32_t hkw = h + kw;
+        const uint32_t dhkw = add_asm(d, hkw);
+        const uint32_t s1 = bsig1(e), c1 = ch(e, f, g);
+        const uint32_t t1 = add3_asm(s1, c1, hkw);
+        d = add3_asm(s1, c1, dhkw);
+        h = add3_asm(t1, bsig0(a), maj(a, b, c));
+    } else {
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw;
+        d = d + t1;
+        h = t1 + bsig0(a) + maj(a, b, c);
+    }
+}
+
+// Plain-C round (no inline asm): the compiler folds it completely when the state and W are constants,
+// e.g. round 0 of a message's first block when the first word (a length field) is known.
+__host__ __device__ constexpr void sha_round_c(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, uint32_t &e,
+                                               uint32_t &f, uint32_t &g, uint32_t &h, uint32_t k, uint32_t w) {
+    const uint32_t t1 = h + (crotr(e, 6) ^ crotr(e, 11) ^ crotr(e, 25)) + ((e & f) ^ (~e & g)) + k + w;
+    const uint32_t t2 = (crotr(a, 2) ^ crotr(a, 13) ^ crotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+    d = d + t1;
+    h = t1 + t2;
+}
+
+__host__ __device__ constexpr uint32_t cssig0(uint32_t w) { return crotr(w, 7) ^ crotr(w, 18) ^ (w >> 3); }
+__host__ __device__ constexpr uint32_t cssig1(uint32_t w) { return crotr(w, 17) ^ crotr(w, 19) ^ (w >> 10); }
+
+// Compile-time knowledge of a message block: which of its 16 words are constants (length fields,
+// terminator, zero padding, bit length of a fixed-shape record) and their values, expanded through the
+// message schedule (W[t] is known iff its four inputs are).
+struct MsgKnown {
+    uint32_t mask;  // bit i: word i is known
+    uint32_t val[16];
+};
+struct SchedKnown {
+    bool known[64];
+    uint32_t val[64];
+};
+__host__ __device__ constexpr SchedKnown expand_known(const MsgKnown &m) {
+    SchedKnown s{};
+    for (int t = 0; t < 16; ++t) {
+        s.known[t] = (m.mask >> t) & 1u;
+        s.val[t] = s.known[t] ? m.val[t] : 0u;
+    }
+    for (int t = 16; t < 64; ++t) {
+        s.known[t] = s.known[t - 2] && s.known[t - 7] && s.known[t - 15] && s.known[t - 16];
+        s.val[t] = s.known[t] ? cssig1(s.val[t - 2]) + s.val[t - 7] + cssig0(s.val[t - 15]) + s.val[t - 16] : 0u;
+    }
+    return s;
+}
+
+// One round of a partly known block. Known schedule terms are summed at compile time (one literal);
+// a known W[t] folds into the round constant; unknown words come from the rolling ring w[16].
+template <bool SHORT, class KS, int T>
+__device__ __forceinline__ void sha_step_known(uint32_t v[8], uint32_t w[16]) {
+    constexpr SchedKnown S = KS::value;
+    constexpr int A = (64 - T) & 7;
+    if constexpr (S.known[T]) {
+        sha_round_kw<SHORT>(v[A], v[(A + 1) & 7], v[(A + 2) & 7], v[(A + 3) & 7], v[(A + 4) & 7], v[(A + 5) & 7],
+                            v[(A + 6) & 7], v[(A + 7) & 7], k256(T) + S.val[T]);
+    } else {
+        uint32_t wt;
+        if constexpr (T < 16) {
+            wt = w[T];
+        } else {
+            constexpr uint32_t cs = (S.known[T - 2] ? cssig1(S.val[T - 2]) : 0u) + (S.known[T - 7] ? S.val[T - 7] : 0u) +
+                                    (S.known[T - 15] ? cssig0(S.val[T - 15]) : 0u) + (S.known[T - 16] ? S.val[T - 16] : 0u);
+            uint32_t x = cs;
+            if constexpr (!S.known[T - 2]) x += ssig1(w[(T - 2) & 15]);
+            if constexpr (!S.known[T - 7]) x += w[(T - 7) & 15];
+            if constexpr (!S.known[T - 15]) x += ssig0(w[(T - 15) & 15]);
+            if constexpr (!S.known[T - 16]) x += w[T & 15];
+            wt = x;
+            w[T & 15] = wt;
+        }
+        sha_round<SHORT>(v[A], v[(A + 1) & 7], v[(A + 2) & 7], v[(A + 3) & 7], v[(A + 4) & 7], v[(A + 5) & 7],
+                         v[(A + 6) & 7], v[(A + 7) & 7], k256(T), wt);
+    }
+}
+
+template <bool SHORT, class KS, int... T>
+__device__ __forceinline__ void sha_steps_known(uint32_t v[8], uint32_t w[16], std::integer_sequence<int, T...>) {
+    (sha_step_known<SHORT, KS, T>(v, w), ...);
+}
+
+// Compression of a partly known block. FIRST: s holds the initial hash value H0 (a message's first
+// block) — with a known W[0], rounds 0 and 1 then run in plain C, which the compiler folds to constants
+// (round 0) and two adds (round 1).
+template <bool SHORT, class KS, bool FIRST>
+__device__ __forceinline__ void sha_compress_known(uint32_t s[8], uint32_t w[16]) {
+    constexpr SchedKnown S = KS::value;
+    uint32_t v[8] = {s[0], s[1], s[2], s[3], s[4], s[5], s[6], s[7]};
+    if constexpr (FIRST && S.known[0]) {
+        // rounds 0 and 1 with the renaming of sha_compress (slot of a at round t = (64 - t) & 7)
+        sha_round_c(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], k256(0), S.val[0]);
+        uint32_t w1 = S.known[1] ? S.val[1] : w[1];
+        sha_round_c(v[7], v[0], v[1], v[2], v[3], v[4], v[5], v[6], k256(1), w1);
+        sha_steps_known<SHORT, KS>(v, w, std::integer_sequence<int, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17,
+                                                            18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34,
+                                                            35, 36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51,
+                                                            52, 53, 54, 55, 56, 57, 58, 59, 60, 61, 62, 63>{});
+    } else {
+        sha_steps_known<SHORT, KS>(v, w, std::make_integer_sequence<int, 64>{});
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += v[i];
+}
+
 #ifndef MKV_SHA_SHORT_DEFAULT
 #define MKV_SHA_SHORT_DEFAULT true
 #endif
@@ -157,8 +272,8 @@ __device__ __forceinline__ void sha_compress_pad64(uint32_t s[8]) {
 #pragma unroll
     for (int t = 0; t < 64; ++t) {
         const int A = (64 - t) & 7;
-        sha_round<SHORT>(v[A], v[(A + 1) & 7], v[(A + 2) & 7], v[(A + 3) & 7], v[(A + 4) & 7], v[(A + 5) & 7],
-                         v[(A + 6) & 7], v[(A + 7) & 7], KW.v[t], 0u);
+        sha_round_kw<SHORT>(v[A], v[(A + 1) & 7], v[(A + 2) & 7], v[(A + 3) & 7], v[(A + 4) & 7], v[(A + 5) & 7],
+                            v[(A + 6) & 7], v[(A + 7) & 7], KW.v[t]);
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] += v[i];

@@ -23,6 +23,30 @@ using namespace mkv;
 
 static thread_local std::string g_err;
 
+// Host-side phase trace of the last API call on this thread (mkv_debug_trace): labelled timestamps
+// (µs since the call started) at the call's blocking points, so a slow call names where its host time
+// went (a device wait, a readback, a copy) next to the device time the HIP events report.
+namespace {
+struct HostTrace {
+    std::chrono::steady_clock::time_point t0;
+    int n = 0;
+    const char *label[64];
+    double us[64];
+    void reset() {
+        n = 0;
+        t0 = std::chrono::steady_clock::now();
+    }
+    void mark(const char *l) {
+        if (n < 64) {
+            label[n] = l;
+            us[n++] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        }
+    }
+};
+thread_local HostTrace g_trace;
+}  // namespace
+#define HTRACE(l) g_trace.mark(l)
+
 int mkv::sha_variant() {
     static const int v = [] {
         const char *e = getenv("MKV_SHA_VARIANT");
@@ -425,6 +449,9 @@ static double spin_us() {
 void wait_idle(hipStream_t s) {
     hipError_t e = hipStreamQuery(s);
     if (e == hipSuccess) return;
+    struct Mark {
+        ~Mark() { HTRACE("wait-done"); }
+    } mark_on_exit;
     if (e != hipErrorNotReady) MKV_HIP(e);
     const auto t0 = std::chrono::steady_clock::now();
     const double spin = spin_us(), limit = wait_timeout_s() * 1e6;
@@ -986,6 +1013,25 @@ void mkv_tree_destroy(mkv_tree *t) {
         std::lock_guard<std::mutex> lk(g_pool_mu);
         pool_trim_locked();
     }
+}
+
+mkv_status mkv_debug_trace(char *buf, uint64_t cap, uint64_t *len) {
+    MKV_TRY({
+        NEED(len, "null argument");
+        std::string s;
+        for (int i = 0; i < g_trace.n; ++i) {
+            if (i) s += ';';
+            s += g_trace.label[i];
+            s += '=';
+            s += std::to_string((int64_t)g_trace.us[i]);
+        }
+        *len = s.size();
+        if (buf && cap) {
+            const size_t k = std::min<size_t>(cap - 1, s.size());
+            std::memcpy(buf, s.data(), k);
+            buf[k] = 0;
+        }
+    });
 }
 
 mkv_status mkv_pool_trim(void) {
@@ -1863,6 +1909,7 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
             prof_end(t, pk);
             MKV_HIP(hipMemcpyAsync(t->h_small, off + m, 8, hipMemcpyDeviceToHost, t->st));
             if (reject) MKV_HIP(hipMemcpyAsync(t->h_small + 1, reject, 4, hipMemcpyDeviceToHost, t->st));
+            HTRACE("keylens-queued");
             wait_stream(t, t->st);
             const uint64_t bytes = t->h_small[0];
             if (reject && reinterpret_cast<const uint32_t *>(t->h_small + 1)[0] != 0) {
@@ -1872,9 +1919,12 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
             }
             uint8_t *ob = ens<uint8_t>(t->d_out, bytes + 16);
             launch_diff_keys(refs, m, A, B, off, ob, t->st);
+            HTRACE("keys-queued");
             keylist_fill(t, l, off, ob, m, bytes);
+            HTRACE("copies-queued");
         }
         sync(t);
+        HTRACE("synced");
     } catch (...) {
         delete l;
         throw;
@@ -1886,6 +1936,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     mkv_tree *t = const_cast<mkv_tree *>(a);
     // b's last work must be complete before a's stream reads it
     wait_idle(b->st);
+    HTRACE("diff-start");
     DiffSide A = side_of(a), B = side_of(b);
     const uint64_t M = A.n + B.n;
     uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
@@ -1897,6 +1948,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
         const uint32_t *nbad = nullptr;
         done = topdown_diff(t, a, b, A, B, refs, &m, &nbad);
         prof_end(t, pd);
+        HTRACE("topdown-done");
         if (done) {
             // the leaf-key check (nbad) comes back with the key list's byte count
             mkv_keylist *l = keylist_from_refs(t, refs, m, A, B, nbad);
@@ -2017,6 +2069,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
 }
 
 mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out) {
+    g_trace.reset();
     MKV_TRY({
         NEED(a && b && out, "null argument");
         NEED(a->dev == b->dev, "trees on different devices");

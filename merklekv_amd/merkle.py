@@ -630,6 +630,14 @@ def pool_stats() -> dict:
             "pooled_blocks": a[4], "pooled_bytes": a[5]}
 
 
+def debug_trace() -> str:
+    """Host phase trace of this thread's last diff call (mkv_debug_trace)."""
+    n = C.c_uint64()
+    buf = C.create_string_buffer(4096)
+    check(lib().mkv_debug_trace(buf, 4096, C.byref(n)))
+    return buf.value.decode()
+
+
 def pool_trim() -> None:
     check(lib().mkv_pool_trim())
 
