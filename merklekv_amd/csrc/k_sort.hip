@@ -52,6 +52,31 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
     idx[i] = (uint32_t)i;
 }
 
+// Prefix extraction fused with the digit histograms (one read of the keys): pfx[i] = big-endian first
+// 8 key bytes (zero padded), counts[p*256 + d] += keys whose byte p (0 = least significant) is d. The
+// input index is not written: the first radix pass generates it (k_os_pass with vin == nullptr).
+__global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__restrict__ kb,
+                                                           const uint64_t *__restrict__ koff, uint64_t n,
+                                                           uint64_t *__restrict__ pfx, uint32_t *__restrict__ counts) {
+    sort_prio();
+    __shared__ uint32_t h[8][256];
+    for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS;
+    for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
+        const uint64_t a = koff[i], b = koff[i + 1];
+        const uint64_t k = key_chunk(kb + a, b - a, 0);
+        pfx[i] = k;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) {
+        const uint32_t c = (&h[0][0])[i];
+        if (c) atomicAdd(&counts[i], c);
+    }
+}
+
 // ---- onesweep LSD radix pass ----
 // Look-back word per (tile, digit): [31:30] status (0 not ready, 1 aggregate, 2 inclusive), [29:0] count.
 constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_VAL = (1u << 30) - 1u;
@@ -116,7 +141,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
         const uint64_t i = base + (uint64_t)s * 64;
         const bool ok = i < n;
         key[s] = ok ? kin[i] : 0ull;
-        val[s] = ok ? vin[i] : 0u;
+        val[s] = ok ? (vin ? vin[i] : (uint32_t)i) : 0u;  // vin == nullptr: values are the input indices
     }
 #pragma unroll
     for (int s = 0; s < RS_IPT; ++s) {
@@ -649,6 +674,17 @@ void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const
     MKV_LAUNCH_CHECK();
 }
 
+void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
+                        hipStream_t st) {
+    init_sort_prio();
+    uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
+    MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
+    if (!n) return;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
+    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, pfx, counts);
+    MKV_LAUNCH_CHECK();
+}
+
 void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st) {
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
@@ -659,8 +695,14 @@ void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t
 }
 
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
-                         void *scratch, hipStream_t st) {
-    if (n <= 1 || !digit_mask) return false;
+                         void *scratch, hipStream_t st, bool v_identity) {
+    if (n <= 1 || !digit_mask) {
+        if (v_identity && n) {
+            hipLaunchKernelGGL(k_iota_u32, grid1d(n), dim3(256), 0, st, v, n);
+            MKV_LAUNCH_CHECK();
+        }
+        return false;
+    }
     if (n >= (1ull << 30)) throw Error(ST_EINVAL, "radix sort: more than 2^30 - 1 keys per device");
     const uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
@@ -669,7 +711,8 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
     const int np = __builtin_popcount(digit_mask);
     MKV_HIP(hipMemsetAsync(lookback, 0, (size_t)np * nb * 256 * sizeof(uint32_t), st));
     uint64_t *ki = k, *ko = k2;
-    uint32_t *vi = v, *vo = v2;
+    uint32_t *vi = v_identity ? nullptr : v, *vo = v2;
+    uint32_t *valt = v;  // the ping-pong partner of vo once the first pass has produced real values
     bool swapped = false;
     int q = 0;
     for (int p = 0; p < 8; ++p) {
@@ -683,7 +726,9 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
         MKV_LAUNCH_CHECK();
         ++q;
         std::swap(ki, ko);
-        std::swap(vi, vo);
+        uint32_t *written = vo;
+        vo = vi ? vi : valt;
+        vi = written;
         swapped = !swapped;
     }
     return swapped;

@@ -36,8 +36,13 @@ void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *c
 // worth a pass (radix_prefix_passes: bit p of digit_mask = sort on byte p). Digits below the chosen
 // ones are left to the tie refinement; constant digits are skipped outright.
 void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st);
+// Fused form for builds: pfx[i] = prefix of key i AND all eight digit histograms, one read of the keys.
+void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
+                        hipStream_t st);
+// v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;
+// with no pass at all v is filled with them). The result is in (k, v) or, when true is returned, (k2, v2).
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
-                         void *scratch, hipStream_t st);
+                         void *scratch, hipStream_t st, bool v_identity = false);
 // Orders every tie run of <= 16 positions on the full key in place (one thread per run); tie[] becomes
 // full-key equality there. count[0] += duplicate positions, count[1] += longer runs (left as they are).
 // Visits only the *nheads run heads of launch_mark_ties (max_heads: a host-side upper bound on *nheads).

@@ -106,6 +106,7 @@ void pool_trim_locked() {
 
 struct PinnedBlock {
     uint8_t *p = nullptr;
+    uint8_t *dp = nullptr;  // the same memory as the device sees it (written by k_copy_to_host)
     size_t cap = 0;
     explicit PinnedBlock(size_t bytes) {
         {
@@ -121,15 +122,22 @@ struct PinnedBlock {
                 cap = g_pool[best].second;
                 g_pool_bytes -= cap;
                 g_pool.erase(g_pool.begin() + (long)best);
+                map_device();
                 return;
             }
         }
         cap = std::max<size_t>(bytes + bytes / 4, 4096);
         const auto t0 = std::chrono::steady_clock::now();
         MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&p), cap, hipHostMallocDefault));
+        map_device();
         g_pin_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         ++g_pin_allocs;
         g_pin_alloc_bytes += cap;
+    }
+    void map_device() {
+        void *d = nullptr;
+        MKV_HIP(hipHostGetDevicePointer(&d, p, 0));
+        dp = static_cast<uint8_t *>(d);
     }
     PinnedBlock(const PinnedBlock &) = delete;
     PinnedBlock &operator=(const PinnedBlock &) = delete;
@@ -215,6 +223,7 @@ struct mkv_tree {
     uint64_t bm_bits = 0;
     bool bm_dirty = false;
     uint64_t *h_small = nullptr;  // pinned host scalars
+    uint8_t *h_small_dev = nullptr;  // h_small as the device sees it (readbacks are kernel stores)
     uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
     uint8_t *h_seam = nullptr;     // pinned staging of seam-combine inputs
     size_t h_seam_cap = 0;
@@ -252,6 +261,32 @@ __global__ void k_clear_tomb(const uint8_t *__restrict__ tomb, const uint32_t *_
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n && tomb[perm[i]]) flags[i] = 0;
 }
+// Device -> pinned host copy done by a kernel on the tree's stream (16-B stores straight into the
+// mapped host block) instead of hipMemcpyAsync: the runtime's D2H path occasionally held the calling
+// thread for ~10 ms inside hipMemcpyAsync itself (r02 bench: diff host trace, "copies-queued").
+// src and dst 16-B aligned; the tail is copied bytewise.
+__global__ __launch_bounds__(256) void k_copy_to_host(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                      uint64_t bytes) {
+    const uint64_t nv = bytes / 16, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t v = t; v < nv; v += stride)
+        reinterpret_cast<uint4 *>(dst)[v] = reinterpret_cast<const uint4 *>(src)[v];
+    if (t < bytes - nv * 16) dst[nv * 16 + t] = src[nv * 16 + t];
+}
+void copy_to_host(const void *src, uint8_t *dst_dev_view, uint64_t bytes, hipStream_t st) {
+    if (!bytes) return;
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(bytes / 16 + 1, 256), 2048);
+    hipLaunchKernelGGL(k_copy_to_host, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<const uint8_t *>(src),
+                       dst_dev_view, bytes);
+    MKV_LAUNCH_CHECK();
+}
+
+// Scalar readback into the tree's pinned scratch (h_small), as a kernel store on stream st.
+void small_d2h(mkv_tree *t, const void *h_dst, const void *src, uint64_t bytes, hipStream_t st) {
+    const uint64_t off = static_cast<const uint8_t *>(h_dst) - reinterpret_cast<const uint8_t *>(t->h_small);
+    copy_to_host(src, t->h_small_dev + off, bytes, st);
+}
+
 // Fringe entry i (48 B: level, valid, idx, digest) gets the digest of node nodes[idx[i]] at byte 16.
 __global__ void k_fringe_digests(const uint8_t *__restrict__ nodes, const uint32_t *__restrict__ idx, uint32_t k,
                                  uint8_t *__restrict__ out) {
@@ -491,13 +526,13 @@ template <class T> T *ens(DevBuf &b, uint64_t count) { return reinterpret_cast<T
 // Scalar readback that waits only for the stream that produced it (the other stream keeps running).
 uint64_t d2h_u64(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
     if (!s) s = t->st;
-    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    small_d2h(t, t->h_small, dptr, sizeof(uint64_t), s);
     wait_stream(t, s);
     return t->h_small[0];
 }
 uint32_t d2h_u32(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
     if (!s) s = t->st;
-    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    small_d2h(t, t->h_small, dptr, sizeof(uint32_t), s);
     wait_stream(t, s);
     return reinterpret_cast<uint32_t *>(t->h_small)[0];
 }
@@ -507,7 +542,7 @@ uint32_t d2h_u32(mkv_tree *t, const void *dptr, hipStream_t s = nullptr) {
 const uint32_t *d2h_u32s(mkv_tree *t, const void *dptr, uint32_t words, hipStream_t s = nullptr) {
     if (!s) s = t->st;
     if (words > 64) throw std::runtime_error("d2h_u32s: more than 64 words");
-    MKV_HIP(hipMemcpyAsync(t->h_small, dptr, 4ull * words, hipMemcpyDeviceToHost, s));
+    small_d2h(t, t->h_small, dptr, 4ull * words, s);
     wait_stream(t, s);
     return reinterpret_cast<const uint32_t *>(t->h_small);
 }
@@ -725,16 +760,16 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n_in), scan_scratch_bytes(n_in + 1)));
 
     size_t ps = prof_begin(t, "sort", st);
-    launch_prefix64(kb, koff, n_in, k1, v1, st);
+    // one read of the keys: 8-byte prefixes + all eight digit histograms (the indices come from pass 1)
+    launch_prefix_hist(kb, koff, n_in, k1, radix, st);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
     if (n_in > 1) {
-        radix_prefix_hist(k1, n_in, radix, st);
         MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         wait_stream(t, st);
         digits = choose_prefix_digits(t->h_counts, n_in, &lo_bit);
     }
-    const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, radix, st);
+    const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, radix, st, true);
     DevBuf *pkbuf = sw ? &t->s_k2 : &t->s_k1, *pkalt = sw ? &t->s_k1 : &t->s_k2;
     DevBuf *pmbuf = sw ? &t->s_v2 : &t->s_v1, *pmalt = sw ? &t->s_v1 : &t->s_v2;
     uint64_t *pk = pkbuf->as<uint64_t>();
@@ -753,7 +788,7 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         MKV_HIP(hipMemsetAsync(misc + 4, 0, 8, st));
         // every run head is followed by >= 1 tie, so heads <= nties
         launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, heads, misc + 1, nties, st);
-        MKV_HIP(hipMemcpyAsync(t->h_small, misc + 4, 8, hipMemcpyDeviceToHost, st));
+        small_d2h(t, t->h_small, misc + 4, 8, st);
         wait_stream(t, st);
         const uint32_t dups = reinterpret_cast<uint32_t *>(t->h_small)[0];
         const uint32_t long_runs = reinterpret_cast<uint32_t *>(t->h_small)[1];
@@ -969,6 +1004,11 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             throw Error(ST_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e2));
         }
         e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 256, hipHostMallocDefault);
+        if (e2 == hipSuccess) {
+            void *d = nullptr;
+            e2 = hipHostGetDevicePointer(&d, t->h_small, 0);
+            t->h_small_dev = static_cast<uint8_t *>(d);
+        }
         if (e2 == hipSuccess)
             e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_counts), 8 * 256 * sizeof(uint32_t), hipHostMallocDefault);
         if (e2 == hipSuccess) {
@@ -1416,7 +1456,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         }
         for (size_t q = 0; q < g.size(); ++q) {
             mkv_tree *t = ts[g[q]];
-            MKV_HIP(hipMemcpyAsync(t->h_small, T.t[q].missing, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            small_d2h(t, t->h_small, T.t[q].missing, sizeof(uint32_t), st);
             if (!t->sharded) {
                 MKV_HIP(hipMemcpyAsync(t->root, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32,
                                        hipMemcpyDeviceToHost, st));
@@ -1522,7 +1562,7 @@ mkv_status mkv_tree_build_wire(mkv_tree *t, const uint8_t *scan, uint64_t scan_l
         launch_get_values(dgets, t->w_nl2.as<uint64_t>(), n, vs, vl, found, misc, t->st);
         void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n + 1), scan_scratch_bytes(n + 2)));
         exclusive_scan_u32(found, rank, n, misc + 1, radix, t->st);
-        MKV_HIP(hipMemcpyAsync(t->h_small, misc, 8, hipMemcpyDeviceToHost, t->st));
+        small_d2h(t, t->h_small, misc, 8, t->st);
         wait_stream(t, t->st);
         const uint32_t bad = reinterpret_cast<uint32_t *>(t->h_small)[0];
         const uint64_t m = reinterpret_cast<uint32_t *>(t->h_small)[1];
@@ -1709,11 +1749,12 @@ static void keylist_fill(mkv_tree *t, mkv_keylist *l, const uint64_t *d_off, con
                          uint64_t bytes) {
     l->n = m;
     if (!m) return;
-    l->blk = std::make_shared<PinnedBlock>(8 * (m + 1) + bytes + 16);
+    const uint64_t kpos = (8 * (m + 1) + 15) & ~uint64_t(15);  // key bytes 16-B aligned in the block
+    l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
     uint64_t *ho = reinterpret_cast<uint64_t *>(l->blk->p);
-    uint8_t *hb = l->blk->p + 8 * (m + 1);
-    MKV_HIP(hipMemcpyAsync(ho, d_off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st));
-    if (bytes) MKV_HIP(hipMemcpyAsync(hb, d_bytes, bytes, hipMemcpyDeviceToHost, t->st));
+    uint8_t *hb = l->blk->p + kpos;
+    copy_to_host(d_off, l->blk->dp, (m + 1) * 8, t->st);
+    copy_to_host(d_bytes, l->blk->dp + kpos, bytes, t->st);
     l->offsets = ho;
     l->bytes = hb;
 }
@@ -1907,8 +1948,8 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
             launch_diff_keylens(refs, m, A, B, lens, t->st);
             exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
             prof_end(t, pk);
-            MKV_HIP(hipMemcpyAsync(t->h_small, off + m, 8, hipMemcpyDeviceToHost, t->st));
-            if (reject) MKV_HIP(hipMemcpyAsync(t->h_small + 1, reject, 4, hipMemcpyDeviceToHost, t->st));
+            small_d2h(t, t->h_small, off + m, 8, t->st);
+            if (reject) small_d2h(t, t->h_small + 1, reject, 4, t->st);
             HTRACE("keylens-queued");
             wait_stream(t, t->st);
             const uint64_t bytes = t->h_small[0];
@@ -2225,7 +2266,7 @@ mkv_status mkv_tree_prefix_root(const mkv_tree *tc, const uint8_t *prefix, uint6
             MKV_HIP(hipMemcpyAsync(dp, prefix, plen, hipMemcpyHostToDevice, t->st));
             uint64_t *lohi = ens<uint64_t>(t->s_misc, 64);
             launch_prefix_bounds(side_of(t), dp, (uint32_t)plen, lohi, t->st);
-            MKV_HIP(hipMemcpyAsync(t->h_small, lohi, 16, hipMemcpyDeviceToHost, t->st));
+            small_d2h(t, t->h_small, lohi, 16, t->st);
             sync(t);
             lo = t->h_small[0];
             hi = t->h_small[1];
@@ -2480,7 +2521,7 @@ mkv_status mkv_shard_combine(mkv_tree *t, const uint8_t *fringes, uint32_t world
         MKV_HIP(hipMemsetAsync(droot, 0, 32, t->st));
         launch_seam_combine(dst + sbytes, (uint32_t)all.size(), reinterpret_cast<const uint64_t *>(dst),
                             (uint32_t)S.size(), nullptr, droot, t->st);
-        MKV_HIP(hipMemcpyAsync(t->h_small, droot, 32, hipMemcpyDeviceToHost, t->st));
+        small_d2h(t, t->h_small, droot, 32, t->st);
         wait_stream(t, t->st);
         std::memcpy(out32, t->h_small, 32);
         *has_root = 1;
@@ -2516,7 +2557,7 @@ mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32
         launch_seam_prep_combine(dfringes, world, stride_bytes, MKV_FRINGE_MAX_ENTRIES,
                                  reinterpret_cast<const uint64_t *>(dst), (uint32_t)S.size(), dst + sbytes,
                                  reinterpret_cast<uint32_t *>(droot + 32), droot, t->st);
-        MKV_HIP(hipMemcpyAsync(t->h_small, droot, 32, hipMemcpyDeviceToHost, t->st));
+        small_d2h(t, t->h_small, droot, 32, t->st);
         wait_stream(t, t->st);
         std::memcpy(out32, t->h_small, 32);
         *has_root = 1;
