@@ -293,7 +293,20 @@ constexpr int PF = LEAF_LDS_WAVE / (16 * 64);  // uint4 prefetch registers per l
 struct ChunkPlan {
     const uint8_t *kstart, *vstart;
     uint32_t kspan, vspan;
+    uint64_t kcopy_end;  // byte offset (from kb) one past the chunk's 16-B-rounded key span
     bool staged;
+};
+
+// Optional key-ownership copy fused into the leaf hash (tree builds from borrowed device inputs): the
+// wave already holds its chunk's key span in registers on the way to LDS, so it also stores it to the
+// tree's own key buffer at the same offsets (16-B stores; neighbouring chunks may both write the
+// granule they share, with identical bytes), and every lane stores its key offset. Chunks whose span
+// ends past kcap (a buffer sized for a smaller earlier build) are skipped; the host then falls back
+// to a plain copy.
+struct KeyOut {
+    uint8_t *kdst;    // null: no copy
+    uint64_t *odst;   // null: offsets not copied
+    uint64_t kcap;    // bytes available at kdst
 };
 
 __device__ __forceinline__ ChunkPlan plan_chunk(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
@@ -306,6 +319,7 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const uint8_t *kb, const uint64_
     const uint64_t ks = ((uint64_t)((kb + k1) - P.kstart) + 15) & ~uint64_t(15);
     const uint64_t vs = ((uint64_t)((vb + v1) - P.vstart) + 15) & ~uint64_t(15);
     P.staged = ks + vs + 32 <= LEAF_LDS_WAVE;
+    P.kcopy_end = (uint64_t)(P.kstart - kb) + ks;
     P.kspan = P.staged ? (uint32_t)ks : 0;
     P.vspan = P.staged ? (uint32_t)vs : 0;
     return P;
@@ -322,6 +336,25 @@ __device__ __forceinline__ void load_chunk(const ChunkPlan &P, uint32_t lane, ui
     }
 }
 
+// The key-ownership copy of chunk P (see KeyOut): from the staged registers, or straight from HBM when
+// the chunk is not staged.
+__device__ __forceinline__ void copy_keys_out(const ChunkPlan &P, uint32_t lane, const uint4 R[PF], const uint8_t *kb,
+                                              const KeyOut &KO) {
+    if (P.kcopy_end > KO.kcap) return;
+    uint8_t *d = KO.kdst + (P.kstart - kb);
+    if (P.staged) {
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+            const uint32_t idx = lane + 64u * i;
+            if (idx * 16u < P.kspan) reinterpret_cast<uint4 *>(d)[idx] = R[i];
+        }
+    } else {
+        const uint64_t span = P.kcopy_end - (uint64_t)(P.kstart - kb);
+        for (uint64_t b = 16ull * lane; b < span; b += 16ull * 64)
+            *reinterpret_cast<uint4 *>(d + b) = *reinterpret_cast<const uint4 *>(P.kstart + b);
+    }
+}
+
 __device__ __forceinline__ void store_chunk(const ChunkPlan &P, uint32_t lane, const uint4 R[PF], uint32_t *lds) {
     uint4 *l4 = reinterpret_cast<uint4 *>(lds);
 #pragma unroll
@@ -331,19 +364,46 @@ __device__ __forceinline__ void store_chunk(const ChunkPlan &P, uint32_t lane, c
     }
 }
 
-template <bool SHORT>
+// DYN: chunks are handed out by a device counter (`grain` chunks per atomic) instead of the static
+// round-robin, so waves on CUs that also run the ordering kernels simply take fewer chunks (no tail of
+// slow CUs). Every wave exits once the counter passes the last chunk.
+template <bool DYN>
+struct ChunkSource {
+    uint64_t next, left, stride;
+    uint32_t *ctr;
+    uint32_t grain;
+    __device__ __forceinline__ uint64_t get(uint32_t lane) {
+        if constexpr (DYN) {
+            if (left == 0) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(ctr, grain);
+                next = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
+                left = grain;
+            }
+            --left;
+            return next++;
+        } else {
+            const uint64_t c = next;
+            next += stride;
+            return c;
+        }
+    }
+};
+
+template <bool SHORT, bool DYN>
 __global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict__ kb,
                                                      const uint64_t *__restrict__ koff,
                                                      const uint8_t *__restrict__ vb,
                                                      const uint64_t *__restrict__ voff, uint64_t n,
-                                                     uint8_t *__restrict__ out) {
+                                                     uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
+                                                     uint32_t grain, KeyOut KO) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *lds = lds_all + wave * (LEAF_LDS_WAVE / 4);
     const uint64_t nchunks = (n + 63) / 64;
-    const uint64_t stride = (uint64_t)gridDim.x * LEAF_WAVES;
-    uint64_t c = (uint64_t)blockIdx.x * LEAF_WAVES + wave;
+    ChunkSource<DYN> src{(uint64_t)blockIdx.x * LEAF_WAVES + wave, 0, (uint64_t)gridDim.x * LEAF_WAVES, ctr, grain};
+    uint64_t c = src.get(lane);
     if (c >= nchunks) return;  // wave-private work: no workgroup barrier anywhere
 
     ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
@@ -355,9 +415,14 @@ __global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict_
     uint64_t vbeg = valid ? voff[r] : 0, vend = valid ? voff[r + 1] : 0;
     while (true) {
         if (P.staged) store_chunk(P, lane, R, lds);
+        if (KO.kdst) copy_keys_out(P, lane, R, kb, KO);
+        if (KO.odst && valid) {
+            KO.odst[r] = kbeg;
+            if (r + 1 == n) KO.odst[n] = kend;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes land before its reads
-        // ---- prefetch chunk c + stride (registers only; consumed next iteration) ----
-        const uint64_t cn = c + stride;
+        // ---- prefetch the next chunk (registers only; consumed next iteration) ----
+        const uint64_t cn = src.get(lane);
         ChunkPlan Pn = P;
         uint64_t nkb = 0, nke = 0, nvb = 0, nve = 0;
         const bool more = cn < nchunks;
@@ -417,9 +482,18 @@ static int leaf_kernel_variant() {
     return v;
 }
 
-void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                      uint8_t *out, hipStream_t st) {
-    if (n == 0) return;
+static uint32_t leaf_dyn_grain() {
+    static const uint32_t v = [] {
+        const char *e = getenv("MKV_LEAF_DYN");  // chunks per atomic grab; 0 = static round-robin
+        const int x = e ? atoi(e) : 4;
+        return (uint32_t)(x < 0 ? 0 : x);
+    }();
+    return v;
+}
+
+bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                      uint8_t *out, hipStream_t st, uint32_t *ctr, uint8_t *kcopy, uint64_t kcap, uint64_t *ocopy) {
+    if (n == 0) return false;
     uint64_t waves = ceil_div(n, 64);
     uint64_t blocks = ceil_div(waves, LEAF_WAVES);
     if (leaf_kernel_variant() == 1) {
@@ -437,14 +511,26 @@ void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
             return v < 1 ? 1 : (v > 4 ? 4 : v);
         }();
         const uint64_t pblocks = std::min<uint64_t>(blocks, (uint64_t)cus * wgs);
-        if (sha_variant() == 0)
-            hipLaunchKernelGGL(k_leaf_persist<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
-                               vb, voff, n, out);
-        else
-            hipLaunchKernelGGL(k_leaf_persist<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
-                               vb, voff, n, out);
+        const uint32_t grain = ctr ? leaf_dyn_grain() : 0;
+        // the fused copy needs kb 16-B aligned (same alignment as the destination)
+        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
+        if (grain) {
+            MKV_HIP(hipMemsetAsync(ctr, 0, sizeof(uint32_t), st));
+            if (sha_variant() == 0)
+                hipLaunchKernelGGL((k_leaf_persist<false, true>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st,
+                                   kb, koff, vb, voff, n, out, ctr, grain, KO);
+            else
+                hipLaunchKernelGGL((k_leaf_persist<true, true>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st,
+                                   kb, koff, vb, voff, n, out, ctr, grain, KO);
+        } else if (sha_variant() == 0) {
+            hipLaunchKernelGGL((k_leaf_persist<false, false>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st,
+                               kb, koff, vb, voff, n, out, ctr, 0u, KO);
+        } else {
+            hipLaunchKernelGGL((k_leaf_persist<true, false>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st,
+                               kb, koff, vb, voff, n, out, ctr, 0u, KO);
+        }
         MKV_LAUNCH_CHECK();
-        return;
+        return KO.kdst != nullptr;
     }
     if (sha_variant() == 0)
         hipLaunchKernelGGL(k_leaf_hash<false>, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff,
@@ -453,6 +539,7 @@ void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
         hipLaunchKernelGGL(k_leaf_hash<true>, dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb, voff,
                            n, out);
     MKV_LAUNCH_CHECK();
+    return false;
 }
 
 }  // namespace mkv

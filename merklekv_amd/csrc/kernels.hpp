@@ -6,8 +6,13 @@
 namespace mkv {
 
 // ---- Kernel A: leaf hashing (k_leaf.hip) ----
-void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                      uint8_t *out_digests, hipStream_t st);
+// ctr: optional device u32 for the dynamic chunk hand-out (MKV_LEAF_DYN grain > 0); zeroed by the launch.
+// kcopy/kcap/ocopy: optional fused key-ownership copy (keys at the same byte offsets into kcopy, at most
+// kcap bytes; offsets[0..n] into ocopy). Returns true when the key copy was fused (persistent kernel and
+// kb 16-B aligned; offsets are copied whenever ocopy is given to the persistent kernel).
+bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                      uint8_t *out_digests, hipStream_t st, uint32_t *ctr = nullptr, uint8_t *kcopy = nullptr,
+                      uint64_t kcap = 0, uint64_t *ocopy = nullptr);
 
 // ---- Kernel C: ordering (k_sort.hip) ----
 // pfx[i] = big-endian first 8 key bytes, zero padded (key i of kb/koff); idx[i] = i

@@ -23,6 +23,11 @@ using namespace mkv;
 
 static thread_local std::string g_err;
 
+static int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 // Host-side phase trace of the last API call on this thread (mkv_debug_trace): labelled timestamps
 // (µs since the call started) at the call's blocking points, so a slow call names where its host time
 // went (a device wait, a readback, a copy) next to the device time the HIP events report.
@@ -208,6 +213,7 @@ struct mkv_tree {
     DevBuf s_radix, s_misc;
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
     DevBuf s_nodes2;  // prefix-root scratch levels
+    DevBuf leaf_ctr;  // dynamic chunk counter of the leaf hash
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf td_bm, td_bc;            // divergent-position bitmap (all-zero between calls) + block counts
@@ -815,8 +821,11 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     return SortedSet{pkbuf, pmbuf, n};
 }
 
+// fused_kcap: the leaf hash already copied the borrowed keys into t->kb (capacity fused_kcap bytes;
+// complete when the key bytes + 16 fit) and the offsets into t->koff (fused_koff); 0 / false: copy here.
 void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
-                       bool staged_inputs, uint64_t staged_kbytes, bool defer_gather) {
+                       bool staged_inputs, uint64_t staged_kbytes, bool defer_gather, uint64_t fused_kcap = 0,
+                       bool fused_koff = false) {
     // Ordering work runs on the aux stream and overlaps the VALU-bound leaf hashing already enqueued on
     // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
     hipStream_t st = t->st2;
@@ -833,23 +842,29 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
     // a readback there would hold the host until the gather finishes and delay the reduce launches)
     const uint64_t kbytes = staged_inputs ? staged_kbytes : (n_in ? d2h_u64(t, koff + n_in, st) : 0);
-    // own the keys (storage order): adopt staged uploads, copy borrowed device inputs. The copy runs on
-    // st2 while the (VALU-bound) leaf hashing still occupies st, ahead of the join.
+    // The reduction on st needs only the sorted order: join here, before the key copy.
+    MKV_HIP(hipEventRecord(t->ev_join, st));
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
+    // Own the keys (storage order): adopt staged uploads, copy borrowed device inputs. The copy stays on
+    // st2 after the join, so its ~0.8 GB of memory traffic (10M keys) overlaps the VALU-bound reduction
+    // instead of lengthening the ordering stage that the reduction waits for; the call's final sync
+    // drains st2 before anything reads t->kb.
     t->nstore = n_in;
     t->kbytes = kbytes;
     if (staged_inputs) {
         swap_buf(t->kb, t->s_kb);
         swap_buf(t->koff, t->s_koff);
     } else {
-        uint8_t *dkb = ens<uint8_t>(t->kb, kbytes + 16);
+        const bool keys_done = fused_kcap && kbytes + 16 <= fused_kcap;
+        uint8_t *dkb = ens<uint8_t>(t->kb, kbytes + 16);  // (a regrowth syncs the device first)
         uint64_t *dko = ens<uint64_t>(t->koff, n_in + 1);
-        size_t pc = prof_begin(t, "keycopy", st);
-        if (kbytes) MKV_HIP(hipMemcpyAsync(dkb, kb, kbytes, hipMemcpyDeviceToDevice, st));
-        MKV_HIP(hipMemcpyAsync(dko, koff, (n_in + 1) * 8, hipMemcpyDeviceToDevice, st));
-        prof_end(t, pc);
+        if (!keys_done || !fused_koff) {
+            size_t pc = prof_begin(t, "keycopy", st);
+            if (kbytes && !keys_done) MKV_HIP(hipMemcpyAsync(dkb, kb, kbytes, hipMemcpyDeviceToDevice, st));
+            if (!fused_koff) MKV_HIP(hipMemcpyAsync(dko, koff, (n_in + 1) * 8, hipMemcpyDeviceToDevice, st));
+            prof_end(t, pc);
+        }
     }
-    MKV_HIP(hipEventRecord(t->ev_join, st));
-    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
     // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
     // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
     uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
@@ -1014,7 +1029,20 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess) {
             int lo = 0, hi = 0;  // aux (ordering) stream at the highest priority: its WGs dispatch first
             (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            e2 = hipStreamCreateWithPriority(&t->st2, hipStreamNonBlocking, hi);
+            const int sort_cus = env_int("MKV_SORT_CUS", 0);  // A/B knob: confine the ordering kernels to N CUs
+            if (sort_cus > 0) {
+                int ncu = 0;
+                (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device);
+                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+                const int k = std::min(sort_cus, ncu);
+                for (int i = 0; i < k; ++i) {  // spread over the chip (every ncu/k-th CU)
+                    const int cu = (int)((int64_t)i * ncu / k);
+                    mask[cu / 32] |= 1u << (cu % 32);
+                }
+                e2 = hipExtStreamCreateWithCUMask(&t->st2, (uint32_t)mask.size(), mask.data());
+            } else {
+                e2 = hipStreamCreateWithPriority(&t->st2, hipStreamNonBlocking, hi);
+            }
         }
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming);
@@ -1140,9 +1168,23 @@ static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *ko
     uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
     fork_streams(t);
     size_t pl = prof_begin(t, "leaf_hash");
-    launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
+    // borrowed device inputs: the leaf hash also copies the keys into the tree's own buffers (when the
+    // capacity of an earlier build suffices; otherwise sort_dedup_gather copies)
+    uint64_t kcap = 0;
+    bool ko_fused = false;
+    if (!staged) {
+        kcap = t->kb.p ? t->kb.cap : 0;
+        ko_fused = t->koff.p && t->koff.cap >= (n + 1) * 8;
+        if (!launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ens<uint32_t>(t->leaf_ctr, 4), t->kb.as<uint8_t>(), kcap,
+                              ko_fused ? t->koff.as<uint64_t>() : nullptr)) {
+            kcap = 0;
+            ko_fused = false;  // offsets are copied only together with the persistent kernel
+        }
+    } else {
+        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ens<uint32_t>(t->leaf_ctr, 4));
+    }
     prof_end(t, pl);
-    sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes, true);
+    sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes, true, kcap, ko_fused);
     finish_unsharded(t);
     prof_end(t, ptot);
     sync(t);
@@ -2343,7 +2385,7 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
         fork_streams(t);
         size_t pl = prof_begin(t, "leaf_hash");
-        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st);
+        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ens<uint32_t>(t->leaf_ctr, 4));
         prof_end(t, pl);
         sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes, true);  // gather fused into reduce
         prof_end(t, ptot);
