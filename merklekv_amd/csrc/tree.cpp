@@ -913,12 +913,13 @@ void finish_unsharded(mkv_tree *t) {
     t->gather_pending = false;
     prof_end(t, pr);
     t->has_root = t->n > 0;
+    uint8_t *hroot = reinterpret_cast<uint8_t *>(t->h_small + 16);
     if (t->has_root) {
         const size_t L = t->lev_S.size();
-        MKV_HIP(hipMemcpyAsync(t->root, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32, hipMemcpyDeviceToHost,
-                               t->st));
+        small_d2h(t, hroot, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32, t->st);
     }
     sync(t);
+    if (t->has_root) std::memcpy(t->root, hroot, 32);
 }
 
 // Upload a host blob into (bytes, offsets) device buffers with offsets rebased to 0.
@@ -1500,8 +1501,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             mkv_tree *t = ts[g[q]];
             small_d2h(t, t->h_small, T.t[q].missing, sizeof(uint32_t), st);
             if (!t->sharded) {
-                MKV_HIP(hipMemcpyAsync(t->root, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32,
-                                       hipMemcpyDeviceToHost, st));
+                small_d2h(t, t->h_small + 16, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32, st);
                 t->has_root = true;
             } else {
                 t->has_root = false;
@@ -1516,6 +1516,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             sync(t);
             t->bm_dirty = false;
             ok[g[q]] = reinterpret_cast<volatile uint32_t *>(t->h_small)[0] == 0;
+            if (ok[g[q]] && !t->sharded) std::memcpy(t->root, t->h_small + 16, 32);
             if (!ok[g[q]]) {  // tree untouched
                 t->has_root = had_root[q];
                 t->combine_pending = had_pending[q];

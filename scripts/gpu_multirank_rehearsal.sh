@@ -14,3 +14,11 @@ run() {
 run build --records 1000000
 run diff --workload diff --records 1000000
 run inc --workload incremental --records 1000000 --batch 1000 --replicas 4
+
+# RCCL (nccl backend) with one rank: the device-resident fringe path (mkv_shard_fringe_device -> RCCL
+# all_gather -> mkv_shard_combine_device) and the batched recombine, on the one GPU this box has.
+unset MKV_BENCH_SAME_GPU MKV_DIST_BACKEND
+export MKV_BENCH_FORCE_DIST=1
+NP=1
+run build_rccl1 --records 1000000 --no-diff
+run inc_rccl1 --workload incremental --records 1000000 --batch 1000 --replicas 4

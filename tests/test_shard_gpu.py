@@ -234,3 +234,40 @@ def test_sharded_mixed_diff_two_processes_gloo_same_gpu():
         assert off == len(got) and tot == len(want)
         got += keys
     assert got == want
+
+
+def _worker_rccl1(q):
+    import torch
+    import torch.distributed as dist
+
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.shard import shard_recombine_many, sharded_root
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 50_000)
+        trees = [MerkleTree(0) for _ in range(3)]
+        roots = [sharded_root(t, (kb, ko), (vb, vo), dist, device="cuda")[0] for t in trees]
+        again = shard_recombine_many(trees, dist, 50_000, device="cuda")
+        q.put((roots, again))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_single_rank_device_fringe_path():
+    """The RCCL path of shard.py (device-resident fringe buffers, one all-gather for several trees,
+    mkv_shard_combine_device) with the nccl backend at world size 1: same root as the unsharded tree."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_rccl1, args=(q,))
+    p.start()
+    roots, again = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 50_000)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    assert roots == [t.get_root_hash()] * 3 and again == roots
