@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libmerklekv_hip.so")
+# MKV_LIB_PATH: an alternative build of the same library (A/B runs of two kernel versions in one call)
+LIB_PATH = os.environ.get("MKV_LIB_PATH") or os.path.join(_HERE, "lib", "libmerklekv_hip.so")
 
 MKV_OK, MKV_EINVAL, MKV_EHIP, MKV_ENOMEM, MKV_ESTATE = 0, 1, 2, 3, 4
 FRINGE_ENTRY_BYTES = 48

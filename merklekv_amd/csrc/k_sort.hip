@@ -110,15 +110,19 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_hist(const uint64_t *__restri
 // In-wave stable ranks: LDS_RANK = one ds_add_rtn_u32 per item on the wave's digit counter (gfx950 returns
 // the pre-add values of lanes hitting one address in lane order — verified at first use by
 // rank_selftest, tools/lds_atomic_order.hip); otherwise 8 ballots build each lane's peer mask.
-template <bool LDS_RANK>
+// HALF: the local reorder goes through one key-sized LDS tile twice (keys, then values) instead of key
+// and value tiles side by side; the sorted digits of the thread's output slots stay in registers
+// between the two phases. IPT: items per thread (tile = 256 x IPT pairs).
+template <bool LDS_RANK, bool HALF, int IPT = RS_IPT>
 __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restrict__ kin,
                                                        const uint32_t *__restrict__ vin,
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                        uint64_t n, int shift, const uint32_t *__restrict__ gcount,
                                                        uint32_t *__restrict__ lookback, uint32_t *__restrict__ ctl) {
     sort_prio();
-    __shared__ uint64_t sk[RS_TILE];
-    __shared__ uint32_t sv[RS_TILE];
+    __shared__ uint64_t sk[(RS_THREADS * IPT)];
+    __shared__ uint32_t sv_full[HALF ? 1 : (RS_THREADS * IPT)];
+    uint32_t *sv = HALF ? reinterpret_cast<uint32_t *>(sk) : sv_full;
     __shared__ uint32_t wcnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint64_t gofs[256];
@@ -130,21 +134,21 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
     for (int i = threadIdx.x; i < 1024; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t bid = sbid;
-    const uint64_t tile0 = (uint64_t)bid * RS_TILE;
-    const uint64_t base = tile0 + (uint64_t)w * RS_WAVE_ITEMS + lane;
+    const uint64_t tile0 = (uint64_t)bid * (RS_THREADS * IPT);
+    const uint64_t base = tile0 + (uint64_t)w * (64 * IPT) + lane;
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint64_t key[RS_IPT];
-    uint32_t val[RS_IPT];
-    uint32_t rk[RS_IPT];
+    uint64_t key[IPT];
+    uint32_t val[IPT];
+    uint32_t rk[IPT];
 #pragma unroll
-    for (int s = 0; s < RS_IPT; ++s) {
+    for (int s = 0; s < IPT; ++s) {
         const uint64_t i = base + (uint64_t)s * 64;
         const bool ok = i < n;
         key[s] = ok ? kin[i] : 0ull;
         val[s] = ok ? (vin ? vin[i] : (uint32_t)i) : 0u;  // vin == nullptr: values are the input indices
     }
 #pragma unroll
-    for (int s = 0; s < RS_IPT; ++s) {
+    for (int s = 0; s < IPT; ++s) {
         const uint64_t i = base + (uint64_t)s * 64;
         const bool ok = i < n;
         const uint32_t d = (uint32_t)(key[s] >> shift) & 255u;
@@ -208,23 +212,58 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
     gofs[d] = gb + excl - ds;  // output position = gofs[digit] + local sorted position
     __syncthreads();
     // ---- local sort in LDS (stable: wave-major, slot, lane order) ----
+    const uint32_t cnt = (uint32_t)(n - tile0 < (RS_THREADS * IPT) ? n - tile0 : (RS_THREADS * IPT));
+    if constexpr (!HALF) {
 #pragma unroll
-    for (int s = 0; s < RS_IPT; ++s) {
-        const uint64_t i = base + (uint64_t)s * 64;
-        if (i < n) {
-            const uint32_t dd = (uint32_t)(key[s] >> shift) & 255u;
-            const uint32_t lp = dstart[dd] + wcnt[w][dd] + rk[s];
-            sk[lp] = key[s];
-            sv[lp] = val[s];
+        for (int s = 0; s < IPT; ++s) {
+            const uint64_t i = base + (uint64_t)s * 64;
+            if (i < n) {
+                const uint32_t dd = (uint32_t)(key[s] >> shift) & 255u;
+                const uint32_t lp = dstart[dd] + wcnt[w][dd] + rk[s];
+                sk[lp] = key[s];
+                sv[lp] = val[s];
+            }
         }
-    }
-    __syncthreads();
-    const uint32_t cnt = (uint32_t)(n - tile0 < RS_TILE ? n - tile0 : RS_TILE);
-    for (uint32_t p = threadIdx.x; p < cnt; p += RS_THREADS) {
-        const uint64_t k = sk[p];
-        const uint64_t pos = gofs[(uint32_t)(k >> shift) & 255u] + p;
-        kout[pos] = k;
-        vout[pos] = sv[p];
+        __syncthreads();
+        for (uint32_t p = threadIdx.x; p < cnt; p += RS_THREADS) {
+            const uint64_t k = sk[p];
+            const uint64_t pos = gofs[(uint32_t)(k >> shift) & 255u] + p;
+            kout[pos] = k;
+            vout[pos] = sv[p];
+        }
+    } else {
+        uint32_t lpos[IPT];
+#pragma unroll
+        for (int s = 0; s < IPT; ++s) {
+            const uint64_t i = base + (uint64_t)s * 64;
+            const uint32_t dd = (uint32_t)(key[s] >> shift) & 255u;
+            lpos[s] = dstart[dd] + wcnt[w][dd] + rk[s];
+            if (i < n) sk[lpos[s]] = key[s];
+        }
+        __syncthreads();
+        uint32_t dig[IPT / 4] = {};  // the digits of this thread's output slots, 8 bits each
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const uint32_t p = threadIdx.x + (uint32_t)m * RS_THREADS;
+            if (p < cnt) {
+                const uint64_t k = sk[p];
+                const uint32_t dd = (uint32_t)(k >> shift) & 255u;
+                dig[m >> 2] |= dd << (8 * (m & 3));
+                kout[gofs[dd] + p] = k;
+            }
+        }
+        __syncthreads();  // every key has left the tile: reuse it for the values
+#pragma unroll
+        for (int s = 0; s < IPT; ++s) {
+            const uint64_t i = base + (uint64_t)s * 64;
+            if (i < n) sv[lpos[s]] = val[s];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < IPT; ++m) {
+            const uint32_t p = threadIdx.x + (uint32_t)m * RS_THREADS;
+            if (p < cnt) vout[gofs[(dig[m >> 2] >> (8 * (m & 3))) & 255u] + p] = sv[p];
+        }
     }
 }
 
@@ -585,6 +624,19 @@ static bool lds_rank_ok(hipStream_t st) {
     return ok == 1;
 }
 
+// Items per thread of the tree builds' prefix-sort passes (MKV_SORT_IPT 16 / 24 / 32; default 24: 6,144
+// pairs per tile through the half-LDS reorder, ~53 KiB — the same LDS footprint as the 4,096-pair tile
+// with separate key and value tiles, 1.5x the pairs per look-back and 1.5x longer digit runs per write:
+// the build's ordering stage 1.27 -> 1.11 ms beside the leaf hash; 32 no longer fits beside it).
+static int sort_ipt() {
+    static const int v = [] {
+        const char *e = getenv("MKV_SORT_IPT");
+        const int x = e ? atoi(e) : 24;
+        return (x == 24 || x == 32) ? x : 16;
+    }();
+    return v;
+}
+
 static void init_sort_prio() {
     static bool done = [] {
         const char *e = getenv("MKV_SORT_PRIO");
@@ -632,10 +684,10 @@ bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint
     bool swapped = false;
     for (int p = 0; p < npass; ++p) {
         if (lds_rank_ok(st))
-            hipLaunchKernelGGL(k_os_pass<true>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
+            hipLaunchKernelGGL((k_os_pass<true, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
                                counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
         else
-            hipLaunchKernelGGL(k_os_pass<false>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
+            hipLaunchKernelGGL((k_os_pass<false, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
                                counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
         MKV_LAUNCH_CHECK();
         std::swap(ki, ko);
@@ -704,7 +756,8 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
         return false;
     }
     if (n >= (1ull << 30)) throw Error(ST_EINVAL, "radix sort: more than 2^30 - 1 keys per device");
-    const uint32_t nb = (uint32_t)ceil_div(n, RS_TILE);
+    const int ipt = sort_ipt();
+    const uint32_t nb = (uint32_t)ceil_div(n, (uint64_t)RS_THREADS * ipt);
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *ctl = counts + 8 * 256;
     uint32_t *lookback = ctl + 64;
@@ -717,12 +770,20 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
     int q = 0;
     for (int p = 0; p < 8; ++p) {
         if (!((digit_mask >> p) & 1u)) continue;
-        if (lds_rank_ok(st))
-            hipLaunchKernelGGL(k_os_pass<true>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lookback + (size_t)q * nb * 256, ctl + 4 * p);
+        const bool lr = lds_rank_ok(st);
+        uint32_t *lb = lookback + (size_t)q * nb * 256;
+        if (lr && ipt == 32)
+            hipLaunchKernelGGL((k_os_pass<true, true, 32>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
+        else if (lr && ipt == 24)
+            hipLaunchKernelGGL((k_os_pass<true, true, 24>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
+        else if (lr)
+            hipLaunchKernelGGL((k_os_pass<true, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
         else
-            hipLaunchKernelGGL(k_os_pass<false>, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lookback + (size_t)q * nb * 256, ctl + 4 * p);
+            hipLaunchKernelGGL((k_os_pass<false, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
         MKV_LAUNCH_CHECK();
         ++q;
         std::swap(ki, ko);
