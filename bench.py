@@ -330,6 +330,50 @@ def anchor_block(ctx, n, steps=5, warmup=2):
     return out
 
 
+def route_block(ctx, n, reps=2):
+    """n unpartitioned records per rank (keys from the whole key space) -> sampled
+    splitters -> one all-to-all -> key-range shards -> sharded build. Reports the redistribution time
+    (max over ranks), bytes each rank sent to other ranks, the shard balance and the global root."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.merkle import gen_records_device
+    from merklekv_amd.shard import redistribute, sharded_root
+    kb = torch.empty(n * KLEN + 64, dtype=torch.uint8, device=ctx.dev)
+    vb = torch.empty(n * VLEN + 64, dtype=torch.uint8, device=ctx.dev)
+    ko = torch.empty(n + 1, dtype=torch.int64, device=ctx.dev)
+    vo = torch.empty(n + 1, dtype=torch.int64, device=ctx.dev)
+    gen_records_device(ctx.local, SEED, ctx.rank * n, n, KLEN, VLEN, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
+                       vo.data_ptr())  # nshards = 1: every rank's keys span the whole key space
+    torch.cuda.synchronize()
+    t = MerkleTree(ctx.local)
+    times = []
+    for _ in range(reps + 1):
+        ctx.barrier()
+        t0 = time.perf_counter()
+        routed = redistribute(t, kb, ko, vb, vo, n, ctx.dist, ctx.coll)
+        ctx.barrier()
+        times.append(ctx.max_over_ranks(time.perf_counter() - t0))
+    ctx.barrier()
+    t0 = time.perf_counter()
+    root, counts = sharded_root(t, routed.blobs(), None, ctx.dist, device=ctx.coll, on_device=True, validate=True)
+    ctx.barrier()
+    build_s = ctx.max_over_ranks(time.perf_counter() - t0)
+    ctx.check_roots_agree(root)
+    me = ctx.rank
+    moved = int(routed.sent[:, 1].sum() + routed.sent[:, 2].sum() - routed.sent[me, 1] - routed.sent[me, 2])
+    moved_max = ctx.max_over_ranks(float(moved))
+    red = sorted(times[1:])[len(times[1:]) // 2]
+    out = {"records_per_rank": n, "global_keys": sum(counts), "redistribute_ms": red * 1e3,
+           "build_after_ms": build_s * 1e3, "bytes_to_other_ranks_max": moved_max,
+           "gb_per_s_per_rank": moved_max / red / 1e9, "shard_min": min(counts), "shard_max": max(counts),
+           "root": root.hex() if root else None,
+           "note": "median of %d redistributions after one warm-up; gb_per_s_per_rank = key+value bytes a "
+                   "rank sends to other ranks / time (xGMI all-to-all incl. sampling, plan and pack)" % reps}
+    del t, routed, kb, vb, ko, vo
+    torch.cuda.empty_cache()
+    return out
+
+
 def configs0_block(ctx, reps=5):
     """BASELINE configs[0] on the GPU: 100K-key tree A, replica B with 1 % 80/10/10 events, host blobs
     (what a server snapshot hands over): build A, build B, diff."""
@@ -435,6 +479,10 @@ def wl_build(ctx, args):
         if args.anchor_records:
             anchor = anchor_block(ctx, args.anchor_records)
 
+    route = None
+    if args.route_records and ctx.dist is not None:
+        route = route_block(ctx, args.route_records)
+
     cpu = None
     if ctx.rank == 0 and ctx.world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_build(args.cpu_seconds)
@@ -454,6 +502,8 @@ def wl_build(ctx, args):
         out["diff_100m"] = d100
         out["anchor_125m"] = anchor
         out["configs0_gpu"] = c0
+        if route is not None:
+            out["route"] = route
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
 
@@ -786,6 +836,9 @@ def main():
     ap.add_argument("--diff-records", type=int, default=100_000_000, help="build workload: diff_100m keys")
     ap.add_argument("--anchor-records", type=int, default=125_000_000,
                     help="build workload at N=1: anchor build size (0 = skip)")
+    ap.add_argument("--route-records", type=int, default=0,
+                    help="build workload with a process group: also time the all-to-all redistribution of "
+                         "this many unpartitioned records per rank (SURVEY 8f-3; 0 = skip)")
     args = ap.parse_args()
     if args.n is None:
         multi = int(os.environ.get("WORLD_SIZE", "1")) > 1

@@ -175,6 +175,34 @@ mkv_status mkv_shard_fringe_device(const mkv_tree *t, uint8_t *dout);
 mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32_t world, uint64_t stride_bytes,
                                     uint64_t global_n, uint8_t out32[32], int *has_root);
 
+/* ---------------- redistribution of unpartitioned input ----------------
+ * The sharded build needs rank r to hold every key of range r. Records that sit on the ranks in no key
+ * order (a store snapshot per GPU, as sync.rs:104-143 collects one) are moved there with one all-to-all:
+ *   mkv_route_sample(keys, m, s)        -> m evenly spaced 8-byte big-endian key prefixes (device)
+ *   [host all-gathers every rank's samples; m_r proportional to the rank's record count]
+ *   mkv_route_splitters(all, world, s)  -> world-1 splitters (host only, same result on every rank)
+ *   mkv_route_plan(keys, values, s)     -> per destination: records, key bytes, value bytes (host)
+ *   [host all-gathers the plans: what every rank receives from every rank]
+ *   mkv_route_pack(...)                 -> send buffers grouped by destination, source order kept
+ *   [all-to-all of key bytes, key lengths, value bytes, value lengths over RCCL]
+ *   mkv_route_offsets(lens, n, offs)    -> offsets of the received blobs, then mkv_shard_prepare(on_device)
+ * Range r = keys whose zero-padded 8-byte prefix p has s[r-1] <= p < s[r]: prefix order agrees with the
+ * reference's String order (R3), so ranges are ordered by rank, and equal prefixes (hence duplicate keys)
+ * always meet on one rank. Received records are ordered by (source rank, source position): a key present
+ * on several ranks resolves as if the ranks' inputs were concatenated in rank order (last write wins).
+ * All record arrays are device pointers; lengths travel as u32 (a key or value of 4 GiB or more is refused). */
+#define MKV_ROUTE_MAX_WORLD 256
+mkv_status mkv_route_sample(mkv_tree *t, mkv_blob keys, uint32_t m, uint64_t *samples_dev);
+mkv_status mkv_route_splitters(const uint64_t *samples, uint64_t ns, uint32_t world, uint64_t *splitters);
+mkv_status mkv_route_plan(mkv_tree *t, mkv_blob keys, mkv_blob values, uint32_t world, const uint64_t *splitters,
+                          uint64_t *counts /* world x 3: records, key bytes, value bytes */);
+/* After mkv_route_plan on the same tree and blobs: kout / vout = key / value bytes grouped by destination
+ * (sizes: the plan's byte totals), klen / vlen = u32 lengths (keys.n entries each). Complete on return. */
+mkv_status mkv_route_pack(mkv_tree *t, mkv_blob keys, mkv_blob values, uint8_t *kout, uint32_t *klen, uint8_t *vout,
+                          uint32_t *vlen);
+/* offs[0..n] = exclusive scan of n u32 lengths (offs[n] = total). Complete on return. */
+mkv_status mkv_route_offsets(mkv_tree *t, const uint32_t *lens, uint64_t n, uint64_t *offs);
+
 /* ---------------- measurement / test utilities (not part of the reference API) ---------------- */
 /* Per-kernel-group device time accumulated with HIP events on the tree's stream when enabled.
  * Groups: "leaf_hash", "sort", "gather", "reduce", "diff", "update", "total_build". */

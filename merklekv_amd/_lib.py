@@ -16,6 +16,7 @@ MKV_OK, MKV_EINVAL, MKV_EHIP, MKV_ENOMEM, MKV_ESTATE = 0, 1, 2, 3, 4
 FRINGE_ENTRY_BYTES = 48
 FRINGE_MAX_ENTRIES = 130
 FRINGE_BYTES = FRINGE_ENTRY_BYTES * FRINGE_MAX_ENTRIES
+ROUTE_MAX_WORLD = 256
 
 # Every symbol include/mkv_merkle.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -29,6 +30,7 @@ EXPORTS = [
     "mkv_prof_read", "mkv_gen_records_device", "mkv_leaf_digests", "mkv_version",
     "mkv_tree_build_digests", "mkv_tree_hash_pattern", "mkv_shard_fringe_device", "mkv_shard_combine_device",
     "mkv_pool_trim", "mkv_pool_stats", "mkv_debug_trace",
+    "mkv_route_sample", "mkv_route_splitters", "mkv_route_plan", "mkv_route_pack", "mkv_route_offsets",
 ]
 
 
@@ -99,6 +101,11 @@ def lib():
         "mkv_pool_trim": ([], i32),
         "mkv_pool_stats": ([vp], i32),
         "mkv_debug_trace": ([vp, u64, P(u64)], i32),
+        "mkv_route_sample": ([vp, Blob, u32, vp], i32),
+        "mkv_route_splitters": ([vp, u64, u32, vp], i32),
+        "mkv_route_plan": ([vp, Blob, Blob, u32, vp, vp], i32),
+        "mkv_route_pack": ([vp, Blob, Blob, vp, vp, vp, vp], i32),
+        "mkv_route_offsets": ([vp, vp, u64, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -26,7 +26,6 @@ namespace {
 constexpr int RS_THREADS = 256;
 constexpr int RS_IPT = 16;
 constexpr int RS_TILE = RS_THREADS * RS_IPT;
-constexpr int RS_WAVE_ITEMS = 64 * RS_IPT;
 
 constexpr int SC_THREADS = 256;
 constexpr int SC_IPT = 8;

@@ -247,6 +247,17 @@ void launch_found_lengths(const uint64_t *len, const uint32_t *found, const uint
 void launch_pack_records(const uint8_t *src, const uint64_t *start, const uint64_t *len, const uint32_t *found,
                          const uint32_t *rank, const uint64_t *off_out, uint64_t n, uint8_t *dst, hipStream_t st);
 
+// ---- redistribution into key-range shards (k_route.hip) ----
+constexpr uint32_t ROUTE_MAX_WORLD = 256;
+void launch_route_sample(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t m, uint64_t *out,
+                         hipStream_t st);
+// dkey[i] = destination rank of record i; counts (3 x world u64, zeroed): records, key bytes, value bytes.
+void launch_route_dest(const uint8_t *kb, const uint64_t *koff, const uint64_t *voff, uint64_t n, const uint64_t *spl,
+                       uint32_t world, uint64_t *dkey, uint64_t *counts, hipStream_t st);
+void launch_route_lens(const uint32_t *perm, const uint64_t *off, uint64_t n, uint32_t *out, uint32_t *bad,
+                       hipStream_t st);
+void launch_u32_to_u64(const uint32_t *in, uint64_t n, uint64_t *out, hipStream_t st);
+
 // ---- synthetic generator (k_gen.hip) — bench/test utility, not part of the reference API ----
 void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
                         uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb, uint64_t *voff,

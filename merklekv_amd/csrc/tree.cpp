@@ -222,6 +222,12 @@ struct mkv_tree {
     DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
     DevBuf w_scan, w_gets, w_nl1, w_nl2, w_scr, w_ks, w_kl, w_vs, w_vl, w_found, w_rank;  // wire ingestion
     DevBuf d_seam, d_S, d_fr;
+    // redistribution (mkv_route_*): splitters, per-destination counts, the destination-grouped permutation
+    DevBuf rt_spl, rt_cnt;
+    const uint32_t *rt_perm = nullptr;
+    uint64_t rt_n = 0;
+    const uint8_t *rt_kb = nullptr;
+    const uint64_t *rt_koff = nullptr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
     // batch merge (key-set changes): batch tombstones, merged prefixes / permutation / levels, count
@@ -937,6 +943,21 @@ void upload_blob(mkv_tree *t, const mkv_blob &b, DevBuf &bytes, DevBuf &offs, ui
     MKV_HIP(hipStreamSynchronize(t->st));  // tmp goes out of scope
 }
 
+// A plain host pointer handed to a device-side argument would fault the GPU instead of failing the call:
+// refuse anything the runtime does not know as device, managed or registered host memory.
+void need_device_ptr(const void *p, const char *what) {
+    if (!p) return;
+    hipPointerAttribute_t a{};
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess || a.type == hipMemoryTypeUnregistered)
+        throw Error(ST_EINVAL, std::string(what) + ": not device-accessible memory (pass device buffers)");
+}
+void need_device_blob(const mkv_blob &b, const char *what) {
+    need_device_ptr(b.bytes, what);
+    need_device_ptr(b.offsets, what);
+}
+
 void check_blob(const mkv_blob &b, const char *what) {
     if (b.n && (!b.offsets)) throw Error(ST_EINVAL, std::string(what) + ": null offsets");
     if (b.n >= 0xFFFFFFF0ull) throw Error(ST_EINVAL, std::string(what) + ": too many records (max 2^32-16)");
@@ -1242,6 +1263,8 @@ mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         NEED(keys.n < 0xFFFFFFF0ull, "too many records");
         NEED(keys.n == 0 || (keys.offsets && values.offsets), "null offsets");
         DevGuard g(t->dev);
+        need_device_blob(keys, "keys");
+        need_device_blob(values, "values");
         build_from_staged(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n, false, 0);
     });
 }
@@ -1679,6 +1702,8 @@ mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         DevGuard g(t->dev);
         if (keys.n == 0) return MKV_OK;
         NEED(!t->prepared, "shard_reduce pending");
+        need_device_blob(keys, "keys");
+        need_device_blob(values, "values");
         if (dirty_update(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n)) return MKV_OK;
         upsert_device_general(t, keys, values);
     });
@@ -1695,6 +1720,8 @@ mkv_status mkv_tree_upsert_device_many(mkv_tree *const *trees, const mkv_blob *k
             NEED(keys[i].n < 0xFFFFFFF0ull, "too many records");
             NEED(keys[i].n == 0 || (keys[i].offsets && values[i].offsets), "null offsets");
             NEED(keys[i].n == 0 || !trees[i]->prepared, "shard_reduce pending");
+            need_device_blob(keys[i], "keys");
+            need_device_blob(values[i], "values");
             for (uint32_t j = 0; j < i; ++j) NEED(trees[j] != trees[i], "a tree appears twice");
         }
         if (k == 0) return MKV_OK;
@@ -2361,6 +2388,8 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         const uint64_t *koff, *voff;
         uint64_t staged_kbytes = 0;
         if (on_device) {
+            need_device_blob(keys, "keys");
+            need_device_blob(values, "values");
             kb = keys.bytes;
             koff = keys.offsets;
             vb = values.bytes;
@@ -2607,6 +2636,129 @@ mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32
         std::memcpy(t->root, out32, 32);
         t->has_root = true;
         t->combine_pending = false;
+    });
+}
+
+// ---------------- redistribution of unpartitioned input ----------------
+mkv_status mkv_route_sample(mkv_tree *t, mkv_blob keys, uint32_t m, uint64_t *samples_dev) {
+    MKV_TRY({
+        NEED(t && (samples_dev || m == 0), "null argument");
+        NEED(keys.n == 0 || keys.offsets, "keys: null offsets");
+        NEED(m <= keys.n, "more samples than records");
+        DevGuard g(t->dev);
+        need_device_blob(keys, "keys");
+        need_device_ptr(samples_dev, "samples");
+        launch_route_sample(keys.bytes, keys.offsets, keys.n, m, samples_dev, t->st);
+        wait_stream(t, t->st);
+    });
+}
+
+mkv_status mkv_route_splitters(const uint64_t *samples, uint64_t ns, uint32_t world, uint64_t *splitters) {
+    MKV_TRY({
+        NEED(world >= 1 && world <= MKV_ROUTE_MAX_WORLD, "world must be 1..256");
+        NEED((samples || ns == 0) && (splitters || world == 1), "null argument");
+        std::vector<uint64_t> s(samples, samples + ns);
+        std::sort(s.begin(), s.end());
+        // splitter r cuts at the sample of rank (r + 1) / world: each range gets ~1/world of the samples
+        for (uint32_t r = 0; r + 1 < world; ++r)
+            splitters[r] = ns ? s[std::min<uint64_t>(ns - 1, ((uint64_t)(r + 1) * ns) / world)] : ~0ull;
+    });
+}
+
+mkv_status mkv_route_plan(mkv_tree *t, mkv_blob keys, mkv_blob values, uint32_t world, const uint64_t *splitters,
+                          uint64_t *counts) {
+    MKV_TRY({
+        NEED(t && counts && (splitters || world == 1), "null argument");
+        NEED(world >= 1 && world <= MKV_ROUTE_MAX_WORLD, "world must be 1..256");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        NEED(keys.n == 0 || (keys.offsets && values.offsets), "null offsets");
+        for (uint32_t r = 1; r + 1 < world; ++r) NEED(splitters[r - 1] <= splitters[r], "splitters not sorted");
+        DevGuard g(t->dev);
+        need_device_blob(keys, "keys");
+        need_device_blob(values, "values");
+        const uint64_t n = keys.n;
+        t->rt_perm = nullptr;
+        t->rt_n = 0;
+        uint8_t *h = seam_staging(t, 3 * 8 * (size_t)MKV_ROUTE_MAX_WORLD + 8 * (size_t)MKV_ROUTE_MAX_WORLD);
+        uint64_t *dspl = ens<uint64_t>(t->rt_spl, MKV_ROUTE_MAX_WORLD);
+        uint64_t *dcnt = ens<uint64_t>(t->rt_cnt, 3 * MKV_ROUTE_MAX_WORLD);
+        if (world > 1) {
+            std::memcpy(h, splitters, 8 * (world - 1));
+            MKV_HIP(hipMemcpyAsync(dspl, h, 8 * (world - 1), hipMemcpyHostToDevice, t->st));
+        }
+        MKV_HIP(hipMemsetAsync(dcnt, 0, 3 * 8 * world, t->st));
+        uint64_t *k1 = ens<uint64_t>(t->s_k1, n + 1);
+        uint64_t *k2 = ens<uint64_t>(t->s_k2, n + 1);
+        uint32_t *v1 = ens<uint32_t>(t->s_v1, n + 1);
+        uint32_t *v2 = ens<uint32_t>(t->s_v2, n + 1);
+        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n), scan_scratch_bytes(n + 1)));
+        launch_route_dest(keys.bytes, keys.offsets, values.offsets, n, dspl, world, k1, dcnt, t->st);
+        launch_iota_u32(v1, n, t->st);
+        int bits = 0;
+        while ((1u << bits) < world) ++bits;
+        // one stable 8-bit pass (world <= 256): records grouped by destination, source order kept
+        const bool sw = radix_sort_pairs(k1, v1, k2, v2, n, 0, bits, radix, t->st);
+        MKV_HIP(hipMemcpyAsync(h + 8 * MKV_ROUTE_MAX_WORLD, dcnt, 3 * 8 * world, hipMemcpyDeviceToHost, t->st));
+        wait_stream(t, t->st);
+        const uint64_t *hc = reinterpret_cast<const uint64_t *>(h + 8 * MKV_ROUTE_MAX_WORLD);
+        for (uint32_t r = 0; r < world; ++r) {  // counts is world x 3 (row per destination)
+            counts[3 * r + 0] = hc[r];
+            counts[3 * r + 1] = hc[world + r];
+            counts[3 * r + 2] = hc[2 * world + r];
+        }
+        t->rt_perm = sw ? v2 : v1;
+        t->rt_n = n;
+        t->rt_kb = keys.bytes;
+        t->rt_koff = keys.offsets;
+    });
+}
+
+mkv_status mkv_route_pack(mkv_tree *t, mkv_blob keys, mkv_blob values, uint8_t *kout, uint32_t *klen, uint8_t *vout,
+                          uint32_t *vlen) {
+    MKV_TRY({
+        NEED(t, "tree is null");
+        NEED(keys.n == values.n, "keys.n != values.n");
+        NEED(t->rt_perm || keys.n == 0, "mkv_route_plan first");
+        NEED(keys.n == t->rt_n && keys.bytes == t->rt_kb && keys.offsets == t->rt_koff,
+             "mkv_route_pack: not the blobs of the last mkv_route_plan");
+        const uint64_t n = keys.n;
+        if (n == 0) return MKV_OK;
+        NEED(kout && klen && vout && vlen, "null output");
+        DevGuard g(t->dev);
+        need_device_blob(values, "values");
+        for (const void *p : {(const void *)kout, (const void *)klen, (const void *)vout, (const void *)vlen})
+            need_device_ptr(p, "route_pack output");
+        uint64_t *off = ens<uint64_t>(t->s_lens, n + 1);
+        uint32_t *bad = ens<uint32_t>(t->s_misc, 64) + 8;
+        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n), scan_scratch_bytes(n + 1)));
+        MKV_HIP(hipMemsetAsync(bad, 0, 4, t->st));
+        for (int side = 0; side < 2; ++side) {
+            const mkv_blob &b = side ? values : keys;
+            launch_gather_keylens(t->rt_perm, b.offsets, n, off, t->st);
+            exclusive_scan_u64(off, off, n, off + n, radix, t->st);
+            launch_gather_keys(t->rt_perm, b.bytes, b.offsets, off, n, side ? vout : kout, t->st);
+            launch_route_lens(t->rt_perm, b.offsets, n, side ? vlen : klen, bad, t->st);
+        }
+        small_d2h(t, t->h_small, bad, 4, t->st);
+        wait_stream(t, t->st);
+        NEED(reinterpret_cast<const uint32_t *>(t->h_small)[0] == 0, "a key or value of 4 GiB or more");
+    });
+}
+
+mkv_status mkv_route_offsets(mkv_tree *t, const uint32_t *lens, uint64_t n, uint64_t *offs) {
+    MKV_TRY({
+        NEED(t && offs && (lens || n == 0), "null argument");
+        DevGuard g(t->dev);
+        need_device_ptr(lens, "lens");
+        need_device_ptr(offs, "offs");
+        if (n == 0) {
+            MKV_HIP(hipMemsetAsync(offs, 0, 8, t->st));
+        } else {
+            void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n), scan_scratch_bytes(n + 1)));
+            launch_u32_to_u64(lens, n, offs, t->st);
+            exclusive_scan_u64(offs, offs, n, offs + n, radix, t->st);
+        }
+        wait_stream(t, t->st);
     });
 }
 

@@ -565,7 +565,7 @@ class MerkleTree:
     def shard_prepare(self, keys, values, on_device: bool = False) -> int:
         n = C.c_uint64()
         if on_device:
-            kb, ko, vb, vo, cnt = keys
+            kb, ko, vb, vo, cnt = (x.data_ptr() if hasattr(x, "data_ptr") else x for x in keys)
             check(lib().mkv_shard_prepare(self._h, Blob(kb, ko, cnt), Blob(vb, vo, cnt), 1, C.byref(n)))
         else:
             pk, pv = pack_blob(keys), pack_blob(values)
@@ -600,6 +600,34 @@ class MerkleTree:
         check(lib().mkv_shard_combine_device(self._h, dptr, world, stride, global_n, out, C.byref(has)))
         return bytes(out) if has.value else None
 
+    # ------------------------------------------------------------------ redistribution (f-3)
+    # Tensor arguments are device tensors on this tree's GPU: key / value bytes (uint8), offsets (int64,
+    # n + 1 entries), lengths (int32 holding u32). See shard.redistribute for the collective flow.
+    def route_sample(self, kb, koff, n: int, m: int, out) -> None:
+        """m evenly spaced 8-byte big-endian key prefixes of the n records into out (int64, m entries)."""
+        check(lib().mkv_route_sample(self._h, Blob(kb.data_ptr(), koff.data_ptr(), n), m, out.data_ptr()))
+
+    def route_plan(self, kb, koff, vb, voff, n: int, splitters) -> np.ndarray:
+        """Destinations of the n records under world-1 splitters: (world, 3) uint64 = records, key bytes,
+        value bytes per destination rank."""
+        spl = np.ascontiguousarray(splitters, dtype=np.uint64)
+        world = len(spl) + 1
+        out = np.zeros((world, 3), np.uint64)
+        check(lib().mkv_route_plan(self._h, Blob(kb.data_ptr(), koff.data_ptr(), n),
+                                   Blob(vb.data_ptr(), voff.data_ptr(), n), world,
+                                   spl.ctypes.data if len(spl) else None, out.ctypes.data))
+        return out
+
+    def route_pack(self, kb, koff, vb, voff, n: int, kout, klen, vout, vlen) -> None:
+        """Send buffers grouped by destination (source order kept) after route_plan on the same records."""
+        check(lib().mkv_route_pack(self._h, Blob(kb.data_ptr(), koff.data_ptr(), n),
+                                   Blob(vb.data_ptr(), voff.data_ptr(), n), kout.data_ptr(), klen.data_ptr(),
+                                   vout.data_ptr(), vlen.data_ptr()))
+
+    def route_offsets(self, lens, n: int, out) -> None:
+        """out[0..n] (int64) = exclusive scan of n u32 lengths."""
+        check(lib().mkv_route_offsets(self._h, lens.data_ptr(), n, out.data_ptr()))
+
     def build_device(self, kb_ptr: int, koff_ptr: int, vb_ptr: int, voff_ptr: int, n: int) -> None:
         """Build from records already resident in HBM (device pointers)."""
         self._pending.clear()
@@ -620,6 +648,14 @@ def gen_records_device(device: int, seed: int, idx0: int, n: int, klen: int, vle
                        vb: int, voff: int, shard: int = 0, nshards: int = 1, vfield: int = 1) -> None:
     check(lib().mkv_gen_records_device(device, seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb,
                                        voff))
+
+
+def route_splitters(samples, world: int) -> np.ndarray:
+    """world-1 splitters (uint64) from every rank's prefix samples (mkv_route_splitters, host only)."""
+    smp = np.ascontiguousarray(samples, dtype=np.uint64)
+    out = np.zeros(max(world - 1, 1), np.uint64)
+    check(lib().mkv_route_splitters(smp.ctypes.data if len(smp) else None, len(smp), world, out.ctypes.data))
+    return out[:world - 1]
 
 
 def pool_stats() -> dict:

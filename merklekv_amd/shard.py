@@ -16,11 +16,17 @@ Range check: the seam protocol is exact only if rank r holds a contiguous key ra
 (the reference keeps one leaf per key, last write wins). `sharded_root(..., validate=True)` all-gathers
 each shard's first and last sorted key and raises unless last(r) < first(next non-empty rank).
 
-`tree` is anything with the shard_* methods of merklekv_amd.MerkleTree.
+Redistribution: `redistribute` moves records that sit on the ranks in no key order into
+key-range shards with one all-to-all (route kernels in csrc/k_route.hip); `sharded_root_unpartitioned`
+chains it with the sharded build.
+
+`tree` is anything with the shard_* (and route_*) methods of merklekv_amd.MerkleTree.
 """
 from __future__ import annotations
 
 import numpy as np
+
+from dataclasses import dataclass
 
 from ._lib import FRINGE_BYTES
 
@@ -148,3 +154,125 @@ def sharded_diff(a, b, dist, device="cpu", group=None):
     raw, offs = a.diff_keys_packed(b)
     counts = shard_counts(dist, len(offs) - 1, device, group)
     return (raw, offs), sum(counts[:rank]), sum(counts)
+
+
+# ---------------------------------------------------------------------------------------------------
+# Redistribution of unpartitioned input (SURVEY §8f-3, §8e "sampled splitters")
+# ---------------------------------------------------------------------------------------------------
+def _backend(dist, group) -> str:
+    try:
+        return str(dist.get_backend(group)).lower()
+    except Exception:  # pragma: no cover - non-default group objects
+        return ""
+
+
+def _all_gather_tensor(dist, t, group=None):
+    """All-gather of equal-size tensors into one (world * numel) tensor on t's device."""
+    import torch
+    world = dist.get_world_size(group)
+    if _is_gpu(t.device) and _backend(dist, group) == "nccl":
+        out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=group)
+        return out
+    src = t.cpu()
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    return torch.cat(parts).to(t.device)
+
+
+def _all_to_all(dist, out, inp, out_splits, in_splits, group=None) -> None:
+    """all_to_all_single over RCCL for device tensors; staged through host memory for gloo."""
+    outs = [int(x) for x in out_splits]
+    ins = [int(x) for x in in_splits]
+    if _is_gpu(out.device) and _backend(dist, group) == "nccl":
+        dist.all_to_all_single(out, inp, outs, ins, group=group)
+        return
+    o = out.cpu() if _is_gpu(out.device) else out
+    dist.all_to_all_single(o, inp.cpu(), outs, ins, group=group)
+    if o is not out:
+        out.copy_(o)
+
+
+@dataclass
+class Routed:
+    """This rank's key range after redistribute: device blobs (kb, koff int64, vb, voff int64) of n
+    records ordered by (source rank, source position), and the splitters that cut the ranges."""
+    kb: object
+    koff: object
+    vb: object
+    voff: object
+    n: int
+    splitters: np.ndarray
+    sent: np.ndarray      # (world, 3) records / key bytes / value bytes this rank sent to each rank
+    received: np.ndarray  # (world, 3) the same, received from each rank
+
+    def blobs(self):
+        return (self.kb, self.koff, self.vb, self.voff, self.n)
+
+
+def redistribute(tree, kb, koff, vb, voff, n: int, dist, device, group=None, samples: int = 4096) -> Routed:
+    """Move this rank's n records (device tensors: kb/vb uint8, koff/voff int64 with n + 1 entries, in any
+    key order) so that rank r ends with exactly the records of key range r, ranges ordered by rank.
+
+    1. all-gather the record counts; rank r contributes m_r ~ samples * n_r / N evenly spaced key
+       prefixes (so the splitters follow the global key distribution), all-gathered;
+    2. every rank derives the same world-1 splitters from the gathered samples (mkv_route_splitters);
+    3. route_plan: destination of every record + per-destination totals; the (world x world x 3) plan
+       matrix is all-gathered so every rank knows its receive sizes;
+    4. route_pack into send buffers grouped by destination, then one all-to-all each for key bytes,
+       key lengths, value bytes and value lengths (RCCL over xGMI on a GPU group);
+    5. route_offsets rebuilds the offsets of the received blobs.
+    """
+    import torch
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = kb.device  # the records' GPU: every buffer the library touches lives there; `device` is the
+    # collective device (cpu for gloo), the helpers stage through it as needed
+    counts = shard_counts(dist, n, device, group)
+    N = sum(counts)
+    m = [min(c, -(-samples * c // N)) if N else 0 for c in counts]
+    loc = torch.zeros(max(max(m), 1), dtype=torch.int64, device=dev)
+    if m[rank]:
+        tree.route_sample(kb, koff, n, m[rank], loc)
+    gathered = _all_gather_tensor(dist, loc, group).cpu().numpy().view(np.uint64)
+    L = loc.numel()
+    smp = np.concatenate([gathered[r * L:r * L + m[r]] for r in range(world)]) if N else np.zeros(0, np.uint64)
+    from .merkle import route_splitters
+    spl = route_splitters(smp, world)
+    plan = np.ascontiguousarray(tree.route_plan(kb, koff, vb, voff, n, spl), dtype=np.uint64)
+    allp = _all_gather_tensor(dist, torch.from_numpy(plan.view(np.int64).reshape(-1).copy()).to(dev), group)
+    allp = allp.cpu().numpy().view(np.uint64).reshape(world, world, 3)  # [source][destination]
+    recv = np.ascontiguousarray(allp[:, rank, :])
+    kout = torch.empty(max(int(plan[:, 1].sum()), 1), dtype=torch.uint8, device=dev)
+    vout = torch.empty(max(int(plan[:, 2].sum()), 1), dtype=torch.uint8, device=dev)
+    klen = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    vlen = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    tree.route_pack(kb, koff, vb, voff, n, kout, klen, vout, vlen)
+    nr = int(recv[:, 0].sum())
+    rk = torch.empty(max(int(recv[:, 1].sum()), 1), dtype=torch.uint8, device=dev)
+    rv = torch.empty(max(int(recv[:, 2].sum()), 1), dtype=torch.uint8, device=dev)
+    rkl = torch.empty(max(nr, 1), dtype=torch.int32, device=dev)
+    rvl = torch.empty(max(nr, 1), dtype=torch.int32, device=dev)
+    # all_to_all_single splits along dim 0: give exact-size views (the buffers carry a 1-element floor)
+    _all_to_all(dist, rk[:int(recv[:, 1].sum())], kout[:int(plan[:, 1].sum())], recv[:, 1], plan[:, 1], group)
+    _all_to_all(dist, rkl[:nr], klen[:n], recv[:, 0], plan[:, 0], group)
+    _all_to_all(dist, rv[:int(recv[:, 2].sum())], vout[:int(plan[:, 2].sum())], recv[:, 2], plan[:, 2], group)
+    _all_to_all(dist, rvl[:nr], vlen[:n], recv[:, 0], plan[:, 0], group)
+    if _is_gpu(dev):
+        torch.cuda.current_stream(dev).synchronize()  # the library runs on its own streams
+    rko = torch.empty(nr + 1, dtype=torch.int64, device=dev)
+    rvo = torch.empty(nr + 1, dtype=torch.int64, device=dev)
+    tree.route_offsets(rkl, nr, rko)
+    tree.route_offsets(rvl, nr, rvo)
+    return Routed(rk, rko, rv, rvo, nr, spl, plan, recv)
+
+
+def sharded_root_unpartitioned(tree, kb, koff, vb, voff, n: int, dist, device, group=None,
+                               samples: int = 4096, validate: bool = True):
+    """redistribute + sharded_root: the global root of the union of every rank's records (duplicates
+    resolved in rank order), from input in no key order. Returns (root, counts, Routed); keep the Routed
+    alive while the tree may still read its blobs (the shard build copies what it keeps)."""
+    routed = redistribute(tree, kb, koff, vb, voff, n, dist, device, group, samples)
+    root, counts = sharded_root(tree, routed.blobs(), None, dist, device, group, on_device=True,
+                                validate=validate)
+    return root, counts, routed

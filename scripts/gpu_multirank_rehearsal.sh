@@ -11,7 +11,7 @@ run() {
     > gpurun_out/mr_$tag.json 2> gpurun_out/mr_$tag.err || { echo "$tag failed"; tail -30 gpurun_out/mr_$tag.err; exit 1; }
   echo "== $tag"; cat gpurun_out/mr_$tag.json
 }
-run build --records 1000000
+run build --records 1000000 --route-records 1000000
 run diff --workload diff --records 1000000
 run inc --workload incremental --records 1000000 --batch 1000 --replicas 4
 
@@ -20,5 +20,5 @@ run inc --workload incremental --records 1000000 --batch 1000 --replicas 4
 unset MKV_BENCH_SAME_GPU MKV_DIST_BACKEND
 export MKV_BENCH_FORCE_DIST=1
 NP=1
-run build_rccl1 --records 1000000 --no-diff
+run build_rccl1 --records 1000000 --no-diff --route-records 2000000
 run inc_rccl1 --workload incremental --records 1000000 --batch 1000 --replicas 4

@@ -10,6 +10,11 @@ import numpy as np
 
 from oracle.merkle_oracle import PyMerkleTree, node_hash, pack
 
+
+def torch_u8(b: bytes):
+    import torch
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8) if b else torch.zeros(0, dtype=torch.uint8)
+
 ENTRY = struct.Struct("<IIQ32s")  # level, valid, idx, digest  (MKV_FRINGE_ENTRY_BYTES = 48)
 MAX_ENTRIES = 130
 
@@ -28,8 +33,55 @@ def plan_levels(o: int, n: int, N: int):
     return out
 
 
+def _split_np(b, o, n):
+    raw = b.numpy().tobytes()
+    offs = o.numpy()
+    return [raw[int(offs[i]):int(offs[i + 1])] for i in range(n)]
+
+
+def prefix8(k: bytes) -> int:
+    """Zero-padded 8-byte big-endian prefix (k_route.hip be_prefix8)."""
+    return int.from_bytes(k[:8].ljust(8, b"\0"), "big")
+
+
 class ModelShardTree:
+    # ---- redistribution model (k_route.hip) over CPU tensors ----
+    def route_sample(self, kb, koff, n, m, out):
+        keys = _split_np(kb, koff, n)
+        for i in range(m):
+            out[i] = np.uint64(prefix8(keys[((2 * i + 1) * n) // (2 * m)])).view(np.int64)
+
+    def route_plan(self, kb, koff, vb, voff, n, splitters):
+        keys, vals = _split_np(kb, koff, n), _split_np(vb, voff, n)
+        spl = [int(x) for x in np.asarray(splitters, np.uint64)]
+        world = len(spl) + 1
+        dest = [sum(1 for s in spl if s <= prefix8(k)) for k in keys]
+        self._route = sorted(range(n), key=lambda i: dest[i])  # stable: source order within a destination
+        out = np.zeros((world, 3), np.uint64)
+        for i in range(n):
+            out[dest[i]] += np.array([1, len(keys[i]), len(vals[i])], np.uint64)
+        self._route_recs = (keys, vals)
+        return out
+
+    def route_pack(self, kb, koff, vb, voff, n, kout, klen, vout, vlen):
+        keys, vals = self._route_recs
+        ks = b"".join(keys[i] for i in self._route)
+        vs = b"".join(vals[i] for i in self._route)
+        kout[:len(ks)] = torch_u8(ks)
+        vout[:len(vs)] = torch_u8(vs)
+        for j, i in enumerate(self._route):
+            klen[j] = len(keys[i])
+            vlen[j] = len(vals[i])
+
+    def route_offsets(self, lens, n, out):
+        out[0] = 0
+        if n:
+            out[1:n + 1] = lens[:n].to(out.dtype).cumsum(0)
+
     def shard_prepare(self, keys, values, on_device=False):
+        if on_device:  # (kb, koff, vb, voff, n) CPU tensors, as redistribute returns them
+            kb, ko, vb, vo, n = keys
+            keys, values = _split_np(kb, ko, n), _split_np(vb, vo, n)
         t = PyMerkleTree()
         for k, v in zip(keys, values):
             t.insert(k, v)

@@ -288,3 +288,72 @@ def test_sharded_mixed_diff_gloo():
         assert off == len(got) and tot == len(want)
         got += keys_r
     assert got == want
+
+
+def _fn_redistribute(rank, dist, inputs, samples):
+    import numpy as np
+    import torch
+
+    from merklekv_amd.shard import sharded_root_unpartitioned
+    from tests.shard_model import ModelShardTree, torch_u8
+    keys, vals = inputs[rank]
+    kb, vb = torch_u8(b"".join(keys)), torch_u8(b"".join(vals))
+    ko = torch.tensor([0] + list(np.cumsum([len(k) for k in keys], dtype=np.int64)), dtype=torch.int64)
+    vo = torch.tensor([0] + list(np.cumsum([len(v) for v in vals], dtype=np.int64)), dtype=torch.int64)
+    t = ModelShardTree()
+    root, counts, routed = sharded_root_unpartitioned(t, kb, ko, vb, vo, len(keys), dist, "cpu", samples=samples)
+    return root, counts, list(t.keys), [int(x) for x in routed.splitters], routed.sent.tolist()
+
+
+def _unpartitioned_inputs(world, seed, n_per_rank, empty_rank=None):
+    """Keys in no order on every rank: random suffixes under a few long shared prefixes (ties on the
+    8-byte routing prefix), short and empty keys, and duplicates across and within ranks."""
+    import random
+    rng = random.Random(seed)
+    pool = [b"tenant/%04d/object/%06d" % (rng.randrange(3), rng.randrange(10 ** 6)) for _ in range(3 * n_per_rank)]
+    pool += [b"", b"a", b"ab", b"tenant/", b"tenant/0", b"zz", b"\x00", b"\xff\xfe"]
+    pool += [b"k%05d" % rng.randrange(10 ** 5) for _ in range(2 * n_per_rank)]
+    inputs = []
+    for r in range(world):
+        if r == empty_rank:
+            inputs.append(([], []))
+            continue
+        ks = [rng.choice(pool) for _ in range(n_per_rank)]
+        inputs.append((ks, [b"v%d/%d/%d" % (r, i, rng.randrange(99)) for i in range(len(ks))]))
+    return inputs
+
+
+@pytest.mark.parametrize("world,n,empty,samples", [(2, 300, None, 64), (3, 250, 1, 16), (3, 40, None, 4096)])
+def test_redistribute_unpartitioned_gloo(world, n, empty, samples):
+    """records in no key order on every rank are routed into key-range shards with one
+    all-to-all; the sharded root equals the root of all ranks' records inserted in rank order (duplicates:
+    last write wins), each rank's range is contiguous, and equal 8-byte prefixes meet on one rank."""
+    inputs = _unpartitioned_inputs(world, 1234 + world * n, n, empty)
+    ref = PyMerkleTree()
+    for ks, vs in inputs:
+        for k, v in zip(ks, vs):
+            ref.insert(k, v)
+    res = _run_fn(world, _fn_redistribute, inputs, samples)
+    assert all(not (isinstance(r, tuple) and r and r[0] == "error") for r in res), res
+    want_keys = sorted(ref.leaf_map)
+    got_keys = []
+    for r, (root, counts, keys, spl, sent) in enumerate(res):
+        assert root == ref.get_root_hash(), r
+        assert counts == [len(x[2]) for x in res]
+        assert sum(row[0] for row in sent) == len(inputs[r][0])
+        assert spl == res[0][3]
+        got_keys += keys
+    assert got_keys == want_keys
+
+
+def test_route_splitters_host():
+    """mkv_route_splitters is host code: runs without a GPU (the library loads on CPU)."""
+    import numpy as np
+
+    from merklekv_amd.merkle import route_splitters
+    s = np.arange(1000, dtype=np.uint64)[::-1].copy()
+    assert list(route_splitters(s, 4)) == [250, 500, 750]
+    assert list(route_splitters(s, 1)) == []
+    assert list(route_splitters(np.zeros(0, np.uint64), 3)) == [2 ** 64 - 1] * 2
+    dup = np.array([5] * 10 + [9] * 2, np.uint64)
+    assert list(route_splitters(dup, 3)) == [5, 5]

@@ -237,6 +237,7 @@ def test_sharded_mixed_diff_two_processes_gloo_same_gpu():
 
 
 def _worker_rccl1(q):
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -251,7 +252,12 @@ def _worker_rccl1(q):
         trees = [MerkleTree(0) for _ in range(3)]
         roots = [sharded_root(t, (kb, ko), (vb, vo), dist, device="cuda")[0] for t in trees]
         again = shard_recombine_many(trees, dist, 50_000, device="cuda")
-        q.put((roots, again))
+        # redistribution over RCCL (all_to_all_single at world size 1) from device tensors
+        from merklekv_amd.shard import sharded_root_unpartitioned
+        dev = [torch.from_numpy(x.view(np.uint8) if x.dtype == np.uint8 else x.astype(np.int64)).cuda()
+               for x in (kb, ko, vb, vo)]
+        routed_root, _, routed = sharded_root_unpartitioned(MerkleTree(0), *dev, 50_000, dist, "cuda")
+        q.put((roots, again, routed_root, routed.n))
     finally:
         dist.destroy_process_group()
 
@@ -264,10 +270,161 @@ def test_rccl_single_rank_device_fringe_path():
     q = ctx.Queue()
     p = ctx.Process(target=_worker_rccl1, args=(q,))
     p.start()
-    roots, again = q.get(timeout=300)
+    roots, again, routed_root, routed_n = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
     kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 50_000)
     t = MerkleTree()
     t.build((kb, ko), (vb, vo))
     assert roots == [t.get_root_hash()] * 3 and again == roots
+    assert routed_root == t.get_root_hash() and routed_n == 50_000
+
+
+# ---------------------------------------------------------------------------------------------------
+# Redistribution of unpartitioned input (csrc/k_route.hip)
+# ---------------------------------------------------------------------------------------------------
+def _dev_blobs(kb, ko, vb, vo):
+    import numpy as np
+    import torch
+    return [torch.from_numpy(np.array(x, copy=True) if x.dtype == np.uint8 else x.astype(np.int64)).cuda()
+            for x in (kb, ko, vb, vo)]
+
+
+def _mixed_records(seed, n):
+    """Ragged records with duplicate keys (same key, different values) and short / shared-prefix keys."""
+    import numpy as np
+
+    from oracle.merkle_oracle import pack
+    kb, ko, vb, vo = gen_records(seed, 0, n, klen=12, vlen=40, ragged=True)
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    rng = np.random.default_rng(seed)
+    for i in rng.choice(n, size=n // 20, replace=False):
+        keys.append(keys[int(i)])
+        vals.append(b"dup-%d" % int(i))
+    keys += [b"", b"a", b"prefix--shared-%05d" % 7, b"prefix--shared-%05d" % 3, b"\xff" * 9]
+    vals += [b"e", b"", b"x", b"y", b"z"]
+    return pack(keys) + pack(vals), keys, vals
+
+
+def test_route_plan_pack_offsets_vs_model():
+    """Single process, no collective: destinations, per-destination totals, destination-grouped send
+    buffers (source order kept) and rebuilt offsets equal the host model (tests/shard_model.py)."""
+    import numpy as np
+    import torch
+
+    from merklekv_amd.merkle import route_splitters
+    from tests.shard_model import prefix8
+    (kb, ko, vb, vo), keys, vals = _mixed_records(99, 20_000)
+    n = len(keys)
+    dkb, dko, dvb, dvo = _dev_blobs(kb, ko, vb, vo)
+    t = MerkleTree()
+    smp = torch.zeros(257, dtype=torch.int64, device="cuda")
+    t.route_sample(dkb, dko, n, 257, smp)
+    want_smp = [prefix8(keys[((2 * i + 1) * n) // 514]) for i in range(257)]
+    assert smp.cpu().numpy().view(np.uint64).tolist() == want_smp
+    for world in (1, 2, 5, 256):
+        spl = route_splitters(np.array(want_smp, np.uint64), world)
+        plan = t.route_plan(dkb, dko, dvb, dvo, n, spl)
+        dest = np.searchsorted(spl, np.array([prefix8(k) for k in keys], np.uint64), side="right")
+        order = np.argsort(dest, kind="stable")
+        for r in range(world):
+            sel = dest == r
+            assert plan[r].tolist() == [int(sel.sum()), sum(len(keys[i]) for i in np.nonzero(sel)[0]),
+                                        sum(len(vals[i]) for i in np.nonzero(sel)[0])], (world, r)
+        kout = torch.empty(int(plan[:, 1].sum()) + 1, dtype=torch.uint8, device="cuda")
+        vout = torch.empty(int(plan[:, 2].sum()) + 1, dtype=torch.uint8, device="cuda")
+        klen = torch.empty(n, dtype=torch.int32, device="cuda")
+        vlen = torch.empty(n, dtype=torch.int32, device="cuda")
+        t.route_pack(dkb, dko, dvb, dvo, n, kout, klen, vout, vlen)
+        assert kout[:-1].cpu().numpy().tobytes() == b"".join(keys[i] for i in order)
+        assert vout[:-1].cpu().numpy().tobytes() == b"".join(vals[i] for i in order)
+        assert klen.cpu().numpy().tolist() == [len(keys[i]) for i in order]
+        assert vlen.cpu().numpy().tolist() == [len(vals[i]) for i in order]
+        offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        t.route_offsets(klen, n, offs)
+        assert offs.cpu().numpy().tolist() == [0] + np.cumsum([len(keys[i]) for i in order]).tolist()
+    with pytest.raises(Exception):  # pack needs the blobs of the last plan
+        t.route_pack(dvb, dvo, dkb, dko, n, kout, klen, vout, vlen)
+
+
+def _worker_route(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.shard import sharded_root_unpartitioned
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kb, ko, vb, vo = _route_input(rank)
+        dev = _dev_blobs(kb, ko, vb, vo)
+        t = MerkleTree(0)
+        root, counts, routed = sharded_root_unpartitioned(t, *dev, len(ko) - 1, dist, "cuda", samples=2048)
+        torch.cuda.synchronize()
+        q.put((rank, root, counts, routed.sent.tolist(), routed.received.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _route_input(rank, n=60_000):
+    """Unpartitioned records (keys from the whole key space): rank r holds ids [r n/2, r n/2 + n) with
+    value field r + 1, so ranks overlap by n/2 keys with different values (the later rank wins)."""
+    return gen_records(DEFAULT_SEED, rank * n // 2, n, vfield=rank + 1)
+
+
+def test_redistribute_two_processes_gloo_same_gpu():
+    """Route kernels + all-to-all (gloo, staged) + sharded build: every rank's root equals the oracle
+    root of the ranks' inputs inserted in rank order (duplicates across ranks: last write wins)."""
+    import torch.multiprocessing as mp
+
+    from oracle import coracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_route, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    parts = [_route_input(r) for r in range(world)]
+    keys, vals = [], []
+    for kb, ko, vb, vo in parts:
+        keys += split_blob(kb, ko)
+        vals += split_blob(vb, vo)
+    from oracle.merkle_oracle import pack
+    want = coracle.OracleTree.build(*pack(keys), *pack(vals))
+    for rank, root, counts, sent, received in res:
+        assert root == want.root(), rank
+        assert sum(counts) == len(want) == 90_000
+        assert min(counts) > 0.3 * 90_000  # sampled splitters balance the ranges
+    assert res[0][3][1] == res[1][4][0] and res[1][3][0] == res[0][4][1]  # what 0 sends to 1 = what 1 gets
+
+
+def test_device_entry_points_refuse_host_pointers():
+    """A pageable host buffer passed where the ABI wants device memory fails the call (MKV_EINVAL)
+    instead of faulting the GPU (tree.cpp need_device_ptr; the r02 rehearsal once passed the gloo
+    collective device as the sample buffer)."""
+    import numpy as np
+    import torch
+
+    from merklekv_amd._lib import MerkleError
+    (kb, ko, vb, vo), keys, vals = _mixed_records(5, 1000)
+    dkb, dko, dvb, dvo = _dev_blobs(kb, ko, vb, vo)
+    n = len(keys)
+    t = MerkleTree()
+    host_out = torch.zeros(16, dtype=torch.int64)  # CPU tensor
+    with pytest.raises(MerkleError, match="not device-accessible"):
+        t.route_sample(dkb, dko, n, 16, host_out)
+    hko = torch.from_numpy(ko.astype(np.int64))
+    with pytest.raises(MerkleError, match="not device-accessible"):
+        t.route_plan(dkb, hko, dvb, dvo, n, np.zeros(1, np.uint64))
+    with pytest.raises(MerkleError, match="not device-accessible"):
+        t.build_device(dkb.data_ptr(), hko.data_ptr(), dvb.data_ptr(), dvo.data_ptr(), n)
+    t.build_device(dkb.data_ptr(), dko.data_ptr(), dvb.data_ptr(), dvo.data_ptr(), n)  # still usable
+    ref = MerkleTree()
+    ref.build(keys, vals)
+    assert t.get_root_hash() == ref.get_root_hash()
