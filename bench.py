@@ -374,6 +374,42 @@ def route_block(ctx, n, reps=2):
     return out
 
 
+def shared_prefix_block(ctx, n, steps=5, warmup=2, prefix=b"tenant/0001/object/"):
+    """Realistic keys that share their first bytes: the default build at n keys
+    whose first len(prefix) bytes are common (the rest random base64), vs the same records unmodified."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    kb, ko, vb, vo = ctx.records(n)
+    t = MerkleTree(ctx.local)
+
+    def run():
+        for _ in range(warmup):
+            t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+        t.prof_enable(True)
+        t.prof_reset()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+            root = t.get_root_hash()
+        el = time.perf_counter() - t0
+        sort_ms = t.prof_read("sort")[0] / steps
+        t.prof_enable(False)
+        return el / steps * 1e3, sort_ms, root
+
+    base_ms, base_sort, _ = run()
+    pre = torch.frombuffer(bytearray(prefix), dtype=torch.uint8).to(ctx.dev)
+    kb[: n * KLEN].view(n, KLEN)[:, : len(prefix)] = pre  # every key now starts with `prefix`
+    torch.cuda.synchronize()
+    ms, sort_ms, root = run()
+    out = {"keys": n, "shared_prefix": prefix.decode(), "shared_bytes": len(prefix),
+           "ms_per_step": ms, "sort_ms_per_step": sort_ms, "random_keys_ms_per_step": base_ms,
+           "random_keys_sort_ms_per_step": base_sort, "leaves_per_s": n / ms * 1e3, "root": root.hex()}
+    del t, kb, vb, ko, vo
+    torch.cuda.empty_cache()
+    return out
+
+
 def configs0_block(ctx, reps=5):
     """BASELINE configs[0] on the GPU: 100K-key tree A, replica B with 1 % 80/10/10 events, host blobs
     (what a server snapshot hands over): build A, build B, diff."""
@@ -466,7 +502,7 @@ def wl_build(ctx, args):
     roofline = leaf_roofline(n, leaf_avg_ms, leaf_cnt)
 
     # ---------------- secondary, 1 GPU only ----------------
-    diff_info = upd_info = d100 = anchor = c0 = None
+    diff_info = upd_info = d100 = anchor = c0 = shared = None
     if not args.no_diff and ctx.world == 1:
         diff_info = diff_secondary(ctx, tree, kb, ko, vb, vo, n)
         upd_info = incremental_secondary(ctx, tree, kb, ko, vb, vo, n)
@@ -474,6 +510,7 @@ def wl_build(ctx, args):
     torch.cuda.empty_cache()
     if not args.no_diff and ctx.world == 1:
         c0 = configs0_block(ctx)
+        shared = shared_prefix_block(ctx, n)
         d100 = diff_modes(ctx, args.diff_records, steps=5, warmup=2)
         torch.cuda.empty_cache()
         if args.anchor_records:
@@ -502,6 +539,7 @@ def wl_build(ctx, args):
         out["diff_100m"] = d100
         out["anchor_125m"] = anchor
         out["configs0_gpu"] = c0
+        out["shared_prefix_10m"] = shared
         if route is not None:
             out["route"] = route
         out["cpu_baseline"] = cpu

@@ -54,26 +54,37 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
 // Prefix extraction fused with the digit histograms (one read of the keys): pfx[i] = big-endian first
 // 8 key bytes (zero padded), counts[p*256 + d] += keys whose byte p (0 = least significant) is d. The
 // input index is not written: the first radix pass generates it (k_os_pass with vin == nullptr).
+// Sort window = the 8 key bytes at byte offset `off` (zero-padded): off = 0 is the key prefix; the host
+// moves the window past bytes every key shares (tree.cpp sort_unique). counts[PH_MAXLEN_WORD] receives the
+// longest key length (saturated to u32), so the host knows when a window only holds padding. That word is
+// the last of the 64 onesweep control words after the histograms (the passes use words 0..31).
 __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__restrict__ kb,
                                                            const uint64_t *__restrict__ koff, uint64_t n,
-                                                           uint64_t *__restrict__ pfx, uint32_t *__restrict__ counts) {
+                                                           uint64_t off, uint64_t *__restrict__ pfx,
+                                                           uint32_t *__restrict__ counts) {
     sort_prio();
     __shared__ uint32_t h[8][256];
+    __shared__ uint32_t lmax;
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
+    if (threadIdx.x == 0) lmax = 0;
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS;
+    uint64_t mx = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
         const uint64_t a = koff[i], b = koff[i + 1];
-        const uint64_t k = key_chunk(kb + a, b - a, 0);
+        const uint64_t k = key_chunk(kb + a, b - a, off);
+        mx = b - a > mx ? b - a : mx;
         pfx[i] = k;
 #pragma unroll
         for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
     }
+    atomicMax(&lmax, (uint32_t)(mx > 0xFFFFFFFFull ? 0xFFFFFFFFull : mx));
     __syncthreads();
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) {
         const uint32_t c = (&h[0][0])[i];
         if (c) atomicAdd(&counts[i], c);
     }
+    if (threadIdx.x == 0 && lmax) atomicMax(&counts[PH_MAXLEN_WORD], lmax);
 }
 
 // ---- onesweep LSD radix pass ----
@@ -481,7 +492,7 @@ __global__ void k_fix_pfx(const uint32_t *__restrict__ pos, uint64_t m, const ui
                           const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff, uint64_t *__restrict__ pfx) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
-    const uint32_t p = pos[k], o = perm[p];
+    const uint32_t p = pos ? pos[k] : (uint32_t)k, o = perm[p];  // pos null: every position
     const uint64_t a = koff[o];
     pfx[p] = key_chunk(kb + a, koff[o + 1] - a, 0);
 }
@@ -726,13 +737,13 @@ void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const
 }
 
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st) {
+                        hipStream_t st, uint64_t off) {
     init_sort_prio();
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) return;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
-    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, pfx, counts);
+    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, pfx, counts);
     MKV_LAUNCH_CHECK();
 }
 

@@ -41,9 +41,12 @@ void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *c
 // worth a pass (radix_prefix_passes: bit p of digit_mask = sort on byte p). Digits below the chosen
 // ones are left to the tie refinement; constant digits are skipped outright.
 void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st);
-// Fused form for builds: pfx[i] = prefix of key i AND all eight digit histograms, one read of the keys.
+// Fused form for builds: pfx[i] = the 8 key bytes at byte offset `off` (0 = the prefix) AND all eight
+// digit histograms, one read of the keys; counts[PH_MAXLEN_WORD] = longest key length (a control word
+// the onesweep passes never touch: they use words 8 * 256 + 0..31).
+constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st);
+                        hipStream_t st, uint64_t off = 0);
 // v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;
 // with no pass at all v is filled with them). The result is in (k, v) or, when true is returned, (k2, v2).
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
@@ -55,6 +58,7 @@ void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, ui
                          uint8_t *tie, uint32_t *count, const uint32_t *heads, const uint32_t *nheads,
                          uint64_t max_heads, hipStream_t st);
 // pfx[pos[k]] = 8-byte prefix of sorted key pos[k] (after a refinement that re-ordered tie runs).
+// pfx[pos[k]] = prefix of key perm[pos[k]] (pos null: every position k < m)
 void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *kb, const uint64_t *koff,
                     uint64_t *pfx, hipStream_t st);
 // Refinement helpers (see tree.cpp refine_ties for the algorithm).

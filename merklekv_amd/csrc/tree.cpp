@@ -776,9 +776,24 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     launch_prefix_hist(kb, koff, n_in, k1, radix, st);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
+    uint64_t win = 0;  // byte offset of the sort window
     if (n_in > 1) {
-        MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        MKV_HIP(hipMemcpyAsync(t->h_counts, radix, (PH_MAXLEN_WORD + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                               st));
         wait_stream(t, st);
+        // Bytes every key shares (a constant digit, counted from the most significant one) carry no
+        // order: move the window past them ("tenant/0001/object/..." keys would otherwise tie on the
+        // whole prefix and leave all n keys to the chunk-by-chunk refinement). Stops at the longest key.
+        const uint64_t maxlen = t->h_counts[PH_MAXLEN_WORD];
+        for (int it = 0; it < 64; ++it) {
+            int c = 0;
+            while (c < 8 && *std::max_element(t->h_counts + (7 - c) * 256, t->h_counts + (8 - c) * 256) == n_in) ++c;
+            if (c == 0 || win + c >= maxlen) break;
+            win += c;
+            launch_prefix_hist(kb, koff, n_in, k1, radix, st, win);
+            MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            wait_stream(t, st);
+        }
         digits = choose_prefix_digits(t->h_counts, n_in, &lo_bit);
     }
     const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, radix, st, true);
@@ -804,7 +819,10 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         wait_stream(t, st);
         const uint32_t dups = reinterpret_cast<uint32_t *>(t->h_small)[0];
         const uint32_t long_runs = reinterpret_cast<uint32_t *>(t->h_small)[1];
-        if (long_runs) refine_ties(t, kb, koff, n_in, perm, tie, lo_bit ? 0 : 1, pk);
+        // chunks (8-byte aligned) fully ordered so far: bytes [0, win) are shared, window bytes above
+        // lo_bit are sorted
+        const uint32_t start_depth = (uint32_t)((win + 8 - lo_bit / 8) / 8);
+        if (long_runs) refine_ties(t, kb, koff, n_in, perm, tie, start_depth, pk);
         dedup = long_runs || dups;
         prof_end(t, pr);
     }
@@ -823,6 +841,11 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         std::swap(pkbuf, pkalt);
         std::swap(pmbuf, pmalt);
         perm = pmbuf->as<uint32_t>();
+    }
+    if (win) {  // the set's prefixes (diff, locate, merge) are the key prefixes, not the sort window
+        size_t pf = prof_begin(t, "sort", st);
+        launch_fix_pfx(nullptr, n, pmbuf->as<uint32_t>(), kb, koff, pkbuf->as<uint64_t>(), st);
+        prof_end(t, pf);
     }
     return SortedSet{pkbuf, pmbuf, n};
 }
@@ -1047,7 +1070,8 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             t->h_small_dev = static_cast<uint8_t *>(d);
         }
         if (e2 == hipSuccess)
-            e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_counts), 8 * 256 * sizeof(uint32_t), hipHostMallocDefault);
+            e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_counts), (8 * 256 + 64) * sizeof(uint32_t),
+                               hipHostMallocDefault);
         if (e2 == hipSuccess) {
             int lo = 0, hi = 0;  // aux (ordering) stream at the highest priority: its WGs dispatch first
             (void)hipDeviceGetStreamPriorityRange(&lo, &hi);

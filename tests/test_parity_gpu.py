@@ -458,3 +458,55 @@ def test_topdown_identical_trees_empty():
     a.build((kb, ko), (vb, vo))
     b.build((kb, ko), (vb, vo))
     assert a.diff_keys(b) == [] and a.diff_first_key(b) is None
+
+
+# ---------------------------------------------------------------- sort window past shared key bytes
+def _shared_prefix_pairs(rng, shape, n):
+    alpha = b"-0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ_abcdefghijklmnopqrstuvwxyz"
+    def rnd(m):
+        return bytes(rng.choice(alpha) for _ in range(m))
+    if shape == "tenant19":      # 19 shared bytes, 13 random: window at byte 19 after 3 hist passes
+        ks = [b"tenant/0001/object/" + rnd(13) for _ in range(n)]
+    elif shape == "user5":       # 5 shared bytes then digits: window at byte 5
+        ks = [b"user:%d" % rng.randrange(10 ** 9) for _ in range(n)]
+    elif shape == "long41":      # 41 shared bytes, short suffixes, some keys equal to the prefix
+        base = b"x" * 33 + b"/shared/"
+        ks = [base + (rnd(rng.randrange(0, 4)) if i % 50 else b"") for i in range(n)]
+    elif shape == "dups":        # shared 12 bytes + few distinct suffixes: duplicates, last write wins
+        ks = [b"bucket-0042/" + rnd(2) for _ in range(n)]
+    elif shape == "nul_pad":     # shared bytes that are NULs, keys of the prefix length and longer
+        ks = [b"\x00" * 9 + (rnd(rng.randrange(0, 6)) if i % 7 else b"") for i in range(n)]
+    else:                        # "mixed": one key breaks the sharing at byte 0 -> window stays at 0
+        ks = [b"tenant/0001/object/" + rnd(13) for _ in range(n - 1)] + [b"a"]
+    return [(k, b"v%d" % rng.randrange(10 ** 6)) for k in ks]
+
+
+@pytest.mark.parametrize("shape", ["tenant19", "user5", "long41", "dups", "nul_pad", "mixed"])
+def test_shared_prefix_sort_window_vs_oracle(oracle_lib, shape):
+    """Keys that share leading bytes (the realistic "tenant/..." / "user:" shapes): the prefix sort moves
+    its window past the shared bytes (tree.cpp sort_unique), the tree keeps offset-0 key prefixes for
+    diff / locate / merge. Build, diff against a mutated replica, and a key-set batch merge vs the oracle."""
+    rng = random.Random(hash(shape) & 0xFFFF)
+    pairs = _shared_prefix_pairs(rng, shape, 40_000)
+    t, o = _check_pairs(oracle_lib, pairs)
+    # replica with value changes, deletions and insertions of the same shape
+    cur = dict(pairs)
+    ks = sorted(cur)
+    other = dict(cur)
+    for k in ks[::97]:
+        other[k] = b"changed"
+    for k in ks[5::211]:
+        other.pop(k, None)
+    for k, v in _shared_prefix_pairs(rng, shape, 300):
+        other[k + b"~new"] = v
+    t2 = MerkleTree()
+    t2.build(list(other), list(other.values()))
+    o2 = oracle_lib.OracleTree.from_pairs(list(other.items()))
+    assert t2.get_root_hash() == o2.root()
+    assert t.diff_keys_bytes(t2) == o.diff(o2)
+    # key-set batch merged into the existing tree (sorted batch, offset-0 prefixes on both sides)
+    batch = [(k + b"~b", b"b") for k, _ in _shared_prefix_pairs(rng, shape, 500)] + [(ks[3], b"upd")]
+    t.upsert([k for k, _ in batch], [v for _, v in batch])
+    o3 = oracle_lib.OracleTree.from_pairs(pairs + batch)
+    assert t.get_root_hash() == o3.root()
+    assert t.diff_keys_bytes(t2) == o3.diff(o2)
