@@ -55,36 +55,72 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
 // 8 key bytes (zero padded), counts[p*256 + d] += keys whose byte p (0 = least significant) is d. The
 // input index is not written: the first radix pass generates it (k_os_pass with vin == nullptr).
 // Sort window = the 8 key bytes at byte offset `off` (zero-padded): off = 0 is the key prefix; the host
-// moves the window past bytes every key shares (tree.cpp sort_unique). counts[PH_MAXLEN_WORD] receives the
-// longest key length (saturated to u32), so the host knows when a window only holds padding. That word is
-// the last of the 64 onesweep control words after the histograms (the passes use words 0..31).
+// moves the window past the bytes every key shares (tree.cpp sort_unique). The pass also leaves, in
+// onesweep control words the radix passes never touch (they use 8 * 256 + 0..31): the longest key length
+// (PH_MAXLEN_WORD) and, with `lcp`, the complement of the shortest zero-padded common prefix of any key
+// with key 0 (PH_NLCP_WORD; bounded by the longer of the two keys, capped at PH_LCP_CAP) and key 0's
+// first 8 bytes (PH_K0_WORD, PH_K0_WORD + 1: high, low half).
+constexpr uint64_t PH_LCP_CAP = 1u << 16;
 __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__restrict__ kb,
                                                            const uint64_t *__restrict__ koff, uint64_t n,
-                                                           uint64_t off, uint64_t *__restrict__ pfx,
+                                                           uint64_t off, bool lcp, uint64_t *__restrict__ pfx,
                                                            uint32_t *__restrict__ counts) {
     sort_prio();
     __shared__ uint32_t h[8][256];
-    __shared__ uint32_t lmax;
+    __shared__ uint32_t lmax, lmin;
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
-    if (threadIdx.x == 0) lmax = 0;
+    if (threadIdx.x == 0) {
+        lmax = 0;
+        lmin = 0xFFFFFFFFu;
+    }
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS;
-    uint64_t mx = 0;
+    const uint64_t a0 = koff[0], l0 = koff[1] - a0;
+    const uint64_t k0w = key_chunk(kb + a0, l0, 0);
+    uint64_t mx = 0, mn = PH_LCP_CAP;
     for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
-        const uint64_t a = koff[i], b = koff[i + 1];
-        const uint64_t k = key_chunk(kb + a, b - a, off);
-        mx = b - a > mx ? b - a : mx;
+        const uint64_t a = koff[i], b = koff[i + 1], len = b - a;
+        const uint64_t k = key_chunk(kb + a, len, off);
+        mx = len > mx ? len : mx;
         pfx[i] = k;
 #pragma unroll
         for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
+        if (lcp && mn) {  // off == 0 here: k is key i's first chunk
+            uint64_t lim = len > l0 ? len : l0;
+            lim = lim < PH_LCP_CAP ? lim : PH_LCP_CAP;
+            uint64_t L = 0, x = k ^ k0w;
+            while (x == 0 && L + 8 < lim) {
+                L += 8;
+                x = key_chunk(kb + a, len, L) ^ key_chunk(kb + a0, l0, L);
+            }
+            L += x ? (uint64_t)(__builtin_clzll(x) >> 3) : 8;
+            L = L < lim ? L : lim;
+            mn = L < mn ? L : mn;
+        }
     }
     atomicMax(&lmax, (uint32_t)(mx > 0xFFFFFFFFull ? 0xFFFFFFFFull : mx));
+    if (lcp) atomicMin(&lmin, (uint32_t)mn);
     __syncthreads();
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) {
         const uint32_t c = (&h[0][0])[i];
         if (c) atomicAdd(&counts[i], c);
     }
-    if (threadIdx.x == 0 && lmax) atomicMax(&counts[PH_MAXLEN_WORD], lmax);
+    if (threadIdx.x == 0) {
+        if (lmax) atomicMax(&counts[PH_MAXLEN_WORD], lmax);
+        if (lcp) atomicMax(&counts[PH_NLCP_WORD], ~lmin);  // the words start at 0: max of ~x = min of x
+        if (lcp && blockIdx.x == 0) {
+            counts[PH_K0_WORD] = (uint32_t)(k0w >> 32);
+            counts[PH_K0_WORD + 1] = (uint32_t)k0w;
+        }
+    }
+}
+
+// Sorted set prefixes from sort windows at byte offset win > 0 (bytes [0, win) are shared by every key;
+// c = those bytes, big-endian at the top): the key prefix is c alone once win >= 8, else c followed by
+// the window's first 8 - win bytes.
+__global__ void k_pfx_from_window(uint64_t *__restrict__ pk, uint64_t n, uint64_t c, uint32_t win) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) pk[i] = win >= 8 ? c : (c | (pk[i] >> (8 * win)));
 }
 
 // ---- onesweep LSD radix pass ----
@@ -743,7 +779,14 @@ void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uin
     MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) return;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
-    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, pfx, counts);
+    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, off == 0, pfx,
+                       counts);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_pfx_from_window, grid1d(n), dim3(256), 0, st, pk, n, shared, win);
     MKV_LAUNCH_CHECK();
 }
 

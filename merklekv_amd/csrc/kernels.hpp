@@ -42,9 +42,13 @@ void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *c
 // ones are left to the tie refinement; constant digits are skipped outright.
 void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st);
 // Fused form for builds: pfx[i] = the 8 key bytes at byte offset `off` (0 = the prefix) AND all eight
-// digit histograms, one read of the keys; counts[PH_MAXLEN_WORD] = longest key length (a control word
-// the onesweep passes never touch: they use words 8 * 256 + 0..31).
+// digit histograms, one read of the keys. Control words the onesweep passes never touch (they use
+// 8 * 256 + 0..31): PH_MAXLEN_WORD = longest key length; with off == 0 also PH_NLCP_WORD = ~(shortest
+// zero-padded common prefix of any key with key 0) and PH_K0_WORD/+1 = key 0's first 8 bytes (hi, lo).
 constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
+constexpr uint32_t PH_NLCP_WORD = 8 * 256 + 62;
+constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;
+void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
                         hipStream_t st, uint64_t off = 0);
 // v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;

@@ -670,7 +670,7 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
     if (m == 0) return;
     const uint64_t m0 = m;
     uint32_t *pos0 = nullptr;
-    if (start_depth == 0) {  // keep the initial tie-run positions for the prefix rewrite
+    if (start_depth == 0 && pfx) {  // keep the initial tie-run positions for the prefix rewrite
         pos0 = ens<uint32_t>(t->s_pos0, m0 + 1);
         MKV_HIP(hipMemcpyAsync(pos0, pos, m0 * 4, hipMemcpyDeviceToDevice, st));
     }
@@ -776,20 +776,20 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     launch_prefix_hist(kb, koff, n_in, k1, radix, st);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
-    uint64_t win = 0;  // byte offset of the sort window
+    uint64_t win = 0;       // byte offset of the sort window
+    uint64_t shared8 = 0;   // the first min(win, 8) bytes every key shares, big-endian at the top
     if (n_in > 1) {
-        MKV_HIP(hipMemcpyAsync(t->h_counts, radix, (PH_MAXLEN_WORD + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                               st));
+        MKV_HIP(hipMemcpyAsync(t->h_counts, radix, (8 * 256 + 64) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         wait_stream(t, st);
-        // Bytes every key shares (a constant digit, counted from the most significant one) carry no
-        // order: move the window past them ("tenant/0001/object/..." keys would otherwise tie on the
-        // whole prefix and leave all n keys to the chunk-by-chunk refinement). Stops at the longest key.
+        // Bytes every key shares carry no order: move the window past them ("tenant/0001/object/..."
+        // keys would otherwise tie on the whole prefix and leave all n keys to the chunk-by-chunk
+        // refinement). One more histogram pass, at the shared prefix length the first pass measured.
         const uint64_t maxlen = t->h_counts[PH_MAXLEN_WORD];
-        for (int it = 0; it < 64; ++it) {
-            int c = 0;
-            while (c < 8 && *std::max_element(t->h_counts + (7 - c) * 256, t->h_counts + (8 - c) * 256) == n_in) ++c;
-            if (c == 0 || win + c >= maxlen) break;
-            win += c;
+        const uint64_t lcp = (uint32_t)~t->h_counts[PH_NLCP_WORD];
+        const uint64_t k0w = ((uint64_t)t->h_counts[PH_K0_WORD] << 32) | t->h_counts[PH_K0_WORD + 1];
+        if (lcp > 0 && lcp < maxlen) {
+            win = lcp;
+            shared8 = win >= 8 ? k0w : k0w & (~0ull << (64 - 8 * win));
             launch_prefix_hist(kb, koff, n_in, k1, radix, st, win);
             MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
             wait_stream(t, st);
@@ -822,7 +822,8 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         // chunks (8-byte aligned) fully ordered so far: bytes [0, win) are shared, window bytes above
         // lo_bit are sorted
         const uint32_t start_depth = (uint32_t)((win + 8 - lo_bit / 8) / 8);
-        if (long_runs) refine_ties(t, kb, koff, n_in, perm, tie, start_depth, pk);
+        // with a moved window pk keeps window values (no prefix rewrite): they become key prefixes below
+        if (long_runs) refine_ties(t, kb, koff, n_in, perm, tie, start_depth, win ? nullptr : pk);
         dedup = long_runs || dups;
         prof_end(t, pr);
     }
@@ -842,9 +843,9 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         std::swap(pmbuf, pmalt);
         perm = pmbuf->as<uint32_t>();
     }
-    if (win) {  // the set's prefixes (diff, locate, merge) are the key prefixes, not the sort window
+    if (win) {  // the set's prefixes (diff, locate, merge) are the key prefixes, not the sort windows
         size_t pf = prof_begin(t, "sort", st);
-        launch_fix_pfx(nullptr, n, pmbuf->as<uint32_t>(), kb, koff, pkbuf->as<uint64_t>(), st);
+        launch_pfx_from_window(pkbuf->as<uint64_t>(), n, shared8, (uint32_t)std::min<uint64_t>(win, 8), st);
         prof_end(t, pf);
     }
     return SortedSet{pkbuf, pmbuf, n};
