@@ -235,22 +235,36 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
     if (bid > 0) {
         int64_t j = (int64_t)bid - 1;
         uint32_t spins = 0;
+        // Look back LB_WIN predecessors per step: their coherent (agent-scope) loads are issued together,
+        // so a walk over k aggregate-only tiles costs ~k / LB_WIN load latencies instead of k.
+        constexpr int LB_WIN = 4;
         while (j >= 0) {
-            // coherent (agent-scope) load, not a read-modify-write: no trip through the atomic unit
-            const uint32_t v = __hip_atomic_load(&lookback[(uint64_t)j * 256 + d], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t stt = v >> 30;
-            if (stt == 0) {
+            uint32_t v[LB_WIN];
+#pragma unroll
+            for (int q = 0; q < LB_WIN; ++q)
+                v[q] = j - q >= 0 ? __hip_atomic_load(&lookback[(uint64_t)(j - q) * 256 + d], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)
+                                  : LB_INC;  // before tile 0: an inclusive zero
+            int used = 0;
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < LB_WIN; ++q) {
+                if (done || used < q) break;  // stopped at an inclusive or a not-ready tile
+                const uint32_t stt = v[q] >> 30;
+                if (stt == 0) break;
+                excl += v[q] & LB_VAL;
+                ++used;
+                done = stt == 2;
+            }
+            if (done) break;
+            j -= used;
+            if (used == 0) {  // j not ready yet
                 if (++spins > LB_SPIN_LIMIT) {
                     atomicOr(&ctl[1], 1u);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
-                continue;
             }
-            excl += v & LB_VAL;
-            if (stt == 2) break;
-            --j;
         }
         __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], LB_INC | (uint32_t)(excl + c), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
