@@ -510,7 +510,13 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
             int v = e ? atoi(e) : 2;
             return v < 1 ? 1 : (v > 4 ? 4 : v);
         }();
-        const uint64_t pblocks = std::min<uint64_t>(blocks, (uint64_t)cus * wgs);
+        // MKV_LEAF_GRID (A/B knob): total persistent workgroups instead of wgs per CU; with the dynamic
+        // chunk hand-out an uneven grid no longer leaves CUs with an extra workgroup finishing last.
+        static const int grid = [] {
+            const char *e = getenv("MKV_LEAF_GRID");
+            return e ? atoi(e) : 0;
+        }();
+        const uint64_t pblocks = std::min<uint64_t>(blocks, grid > 0 ? (uint64_t)grid : (uint64_t)cus * wgs);
         const uint32_t grain = ctr ? leaf_dyn_grain() : 0;
         // the fused copy needs kb 16-B aligned (same alignment as the destination)
         const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};

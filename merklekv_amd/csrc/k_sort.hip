@@ -13,6 +13,7 @@
 // digit-major count matrix -> stable scatter, with in-wave ranks from 8 ballots (peer mask of lanes
 // with the same digit) and per-wave LDS digit counters.
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "common.hpp"
@@ -688,10 +689,14 @@ static bool lds_rank_ok(hipStream_t st) {
 // pairs per tile through the half-LDS reorder, ~53 KiB — the same LDS footprint as the 4,096-pair tile
 // with separate key and value tiles, 1.5x the pairs per look-back and 1.5x longer digit runs per write:
 // the build's ordering stage 1.27 -> 1.11 ms beside the leaf hash; 32 no longer fits beside it).
+// Half-LDS tiles of 12 / 16 / 20 items ("12h" / "16h" / "20h"; 30-46 KiB) fit beside three leaf-hash
+// workgroups per CU (A/B knob with MKV_LEAF_WGS=3). Returned as -ipt for the half-LDS form of 12..20.
 static int sort_ipt() {
     static const int v = [] {
         const char *e = getenv("MKV_SORT_IPT");
-        const int x = e ? atoi(e) : 24;
+        if (!e) return 24;
+        const int x = atoi(e);
+        if (std::strchr(e, 'h') && (x == 12 || x == 16 || x == 20)) return -x;
         return (x == 24 || x == 32) ? x : 16;
     }();
     return v;
@@ -720,7 +725,8 @@ void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64
 size_t scan_scratch_bytes(uint64_t n) { return (ceil_div(n ? n : 1, SC_TILE) + 16) * sizeof(uint64_t); }
 
 size_t radix_scratch_bytes(uint64_t n) {
-    const uint64_t nb = ceil_div(n ? n : 1, RS_TILE);
+    // look-back words for the smallest tile any pass may use (12 items per thread, sort_ipt)
+    const uint64_t nb = ceil_div(n ? n : 1, (uint64_t)RS_THREADS * 12);
     // digit counts (8 x 256) + control words (8 passes x 4) + look-back words (8 passes x tiles x 256)
     return (8 * 256 + 64 + 8ull * nb * 256) * sizeof(uint32_t) + 1024 + scan_scratch_bytes(n);
 }
@@ -823,7 +829,8 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
         return false;
     }
     if (n >= (1ull << 30)) throw Error(ST_EINVAL, "radix sort: more than 2^30 - 1 keys per device");
-    const int ipt = sort_ipt();
+    const int ipt_sel = sort_ipt();
+    const int ipt = ipt_sel < 0 ? -ipt_sel : ipt_sel;
     const uint32_t nb = (uint32_t)ceil_div(n, (uint64_t)RS_THREADS * ipt);
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *ctl = counts + 8 * 256;
@@ -839,7 +846,16 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
         if (!((digit_mask >> p) & 1u)) continue;
         const bool lr = lds_rank_ok(st);
         uint32_t *lb = lookback + (size_t)q * nb * 256;
-        if (lr && ipt == 32)
+        if (lr && ipt_sel < 0 && ipt == 12)
+            hipLaunchKernelGGL((k_os_pass<true, true, 12>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
+        else if (lr && ipt_sel < 0 && ipt == 16)
+            hipLaunchKernelGGL((k_os_pass<true, true, 16>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
+        else if (lr && ipt_sel < 0 && ipt == 20)
+            hipLaunchKernelGGL((k_os_pass<true, true, 20>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
+                               counts + 256 * p, lb, ctl + 4 * p);
+        else if (lr && ipt == 32)
             hipLaunchKernelGGL((k_os_pass<true, true, 32>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
                                counts + 256 * p, lb, ctl + 4 * p);
         else if (lr && ipt == 24)
