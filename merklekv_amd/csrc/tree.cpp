@@ -7,6 +7,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -807,6 +808,10 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     launch_mark_ties(pk, n_in, tie, misc, heads, st, lo_bit);
     prof_end(t, ps);
     const uint32_t nties = n_in ? d2h_u32(t, misc, st) : 0;
+    static const bool dbg_sort = getenv("MKV_DEBUG_SORT") != nullptr;
+    if (dbg_sort)
+        fprintf(stderr, "[mkv sort] n=%llu win=%llu lo_bit=%d digits=0x%x ties=%u heads=%u\n", (unsigned long long)n_in,
+                (unsigned long long)win, lo_bit, digits, nties, d2h_u32(t, misc + 1, st));
     bool dedup = false;
     if (nties) {
         size_t pr = prof_begin(t, "sort", st);

@@ -510,3 +510,45 @@ def test_shared_prefix_sort_window_vs_oracle(oracle_lib, shape):
     o3 = oracle_lib.OracleTree.from_pairs(pairs + batch)
     assert t.get_root_hash() == o3.root()
     assert t.diff_keys_bytes(t2) == o3.diff(o2)
+
+
+# ---------------------------------------------------------------- key byte-entropy shapes (round 2)
+def _entropy_pairs(rng, shape, n):
+    b64 = b"-0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ_abcdefghijklmnopqrstuvwxyz"
+    if shape == "bits1":        # 1 bit per byte: every window byte sorted, long tie runs refined
+        ks = [bytes(rng.choice(b"ab") for _ in range(12)) for _ in range(n)]
+    elif shape == "bytes8":     # 8 bits per byte, ragged lengths
+        ks = [bytes(rng.randrange(256) for _ in range(rng.randrange(1, 12))) for _ in range(n)]
+    elif shape == "b64":   # 6 bits per byte
+        ks = [bytes(rng.choice(b64) for _ in range(10)) for _ in range(n)]
+    elif shape == "skew":       # a few values at some positions, a constant position, skewed frequencies
+        ks = [bytes([rng.choice(b"abc"), 0x2F, rng.choice(b"xy" * 30 + b"z")]) +
+              bytes(rng.choice(b64[:20]) for _ in range(rng.randrange(0, 7))) for _ in range(n)]
+    elif shape == "short_nul":  # lengths 0..3 incl. NUL bytes: zero padding vs real NULs
+        ks = [bytes(rng.choice(b"\x00\x01A") for _ in range(rng.randrange(0, 4))) for _ in range(n)]
+    else:                       # "dec": decimal digits, 10 values per position (4 bits, 3.3 bits entropy)
+        ks = [b"%012d" % rng.randrange(10 ** 12) for _ in range(n)]
+    return [(k, b"v%d" % i) for i, k in enumerate(ks)]
+
+
+@pytest.mark.parametrize("shape,n", [("bits1", 50_000), ("bytes8", 120_000), ("b64", 200_000),
+                                     ("skew", 60_000), ("short_nul", 5_000), ("dec", 150_000)])
+def test_key_entropy_shapes_vs_oracle(oracle_lib, shape, n):
+    """Key sets whose bytes carry 1, 3.3, 6 or 8 bits each (the adaptive digit choice of the prefix sort
+    stops at different bytes, mid-byte entropy), constant and skewed positions, NULs vs zero padding,
+    duplicates (last write wins): build + diff against the oracle."""
+    rng = random.Random(sum(shape.encode()))
+    pairs = _entropy_pairs(rng, shape, n)
+    t, o = _check_pairs(oracle_lib, pairs)
+    other = dict(pairs)
+    ks = sorted(other)
+    for k in ks[::53]:
+        other[k] = b"changed"
+    for k in ks[7::101]:
+        other.pop(k)
+    t2 = MerkleTree()
+    t2.build(list(other), list(other.values()))
+    o2 = oracle_lib.OracleTree.from_pairs(list(other.items()))
+    assert t2.get_root_hash() == o2.root()
+    assert t.diff_keys_bytes(t2) == o.diff(o2)
+
