@@ -309,6 +309,7 @@ struct KeyOut {
     uint64_t kcap;    // bytes available at kdst
 };
 
+template <uint32_t CAP = LEAF_LDS_WAVE>
 __device__ __forceinline__ ChunkPlan plan_chunk(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
                                                 const uint64_t *voff, uint64_t n, uint64_t r0) {
     ChunkPlan P;
@@ -318,7 +319,7 @@ __device__ __forceinline__ ChunkPlan plan_chunk(const uint8_t *kb, const uint64_
     P.vstart = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(vb + v0) & ~uintptr_t(15));
     const uint64_t ks = ((uint64_t)((kb + k1) - P.kstart) + 15) & ~uint64_t(15);
     const uint64_t vs = ((uint64_t)((vb + v1) - P.vstart) + 15) & ~uint64_t(15);
-    P.staged = ks + vs + 32 <= LEAF_LDS_WAVE;
+    P.staged = ks + vs + 32 <= CAP;
     P.kcopy_end = (uint64_t)(P.kstart - kb) + ks;
     P.kspan = P.staged ? (uint32_t)ks : 0;
     P.vspan = P.staged ? (uint32_t)vs : 0;
@@ -361,6 +362,31 @@ __device__ __forceinline__ void store_chunk(const ChunkPlan &P, uint32_t lane, c
     for (int i = 0; i < PF; ++i) {
         const uint32_t idx = lane + 64u * i;
         if (idx * 16u < P.kspan + P.vspan) l4[idx] = R[i];
+    }
+}
+
+// One record of a chunk planned by plan_chunk: from the wave's LDS copy when staged (fixed / runtime
+// uniform shape, else the generic byte-range assembly), straight from HBM otherwise.
+template <bool SHORT>
+__device__ __forceinline__ void hash_record(const ChunkPlan &P, const uint32_t *lds, const uint8_t *kb,
+                                            const uint8_t *vb, uint64_t kbeg, uint64_t kend, uint64_t vbeg,
+                                            uint64_t vend, uint32_t st[8]) {
+    const uint32_t klen = (uint32_t)(kend - kbeg), vlen = (uint32_t)(vend - vbeg);
+    if (P.staged) {
+        const uint32_t kbyte = (uint32_t)((kb + kbeg) - P.kstart);
+        const uint32_t vbyte = P.kspan + (uint32_t)((vb + vbeg) - P.vstart);
+        const uint32_t K0 = __shfl(klen, 0), V0 = __shfl(vlen, 0);
+        const bool mine = klen == K0 && vlen == V0 && ((K0 | V0 | kbyte | vbyte) & 3) == 0;
+        if (__all(mine)) {
+            hash_fast_any<SHORT>(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
+                                 __builtin_amdgcn_readfirstlane(V0), st);
+        } else {
+            LdsSrc src{lds, kbyte, vbyte};
+            hash_generic<SHORT>(src, klen, vlen, st);
+        }
+    } else {
+        GlbSrc src{kb + kbeg, vb + vbeg, kb + kend, vb + vend};
+        hash_generic<SHORT>(src, klen, vlen, st);
     }
 }
 
@@ -439,24 +465,8 @@ __global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict_
         }
         // ---- hash chunk c ----
         if (valid) {
-            const uint32_t klen = (uint32_t)(kend - kbeg), vlen = (uint32_t)(vend - vbeg);
             uint32_t st[8];
-            if (P.staged) {
-                const uint32_t kbyte = (uint32_t)((kb + kbeg) - P.kstart);
-                const uint32_t vbyte = P.kspan + (uint32_t)((vb + vbeg) - P.vstart);
-                const uint32_t K0 = __shfl(klen, 0), V0 = __shfl(vlen, 0);
-                const bool mine = klen == K0 && vlen == V0 && ((K0 | V0 | kbyte | vbyte) & 3) == 0;
-                if (__all(mine)) {
-                    hash_fast_any<SHORT>(lds, kbyte >> 2, vbyte >> 2, __builtin_amdgcn_readfirstlane(K0),
-                                         __builtin_amdgcn_readfirstlane(V0), st);
-                } else {
-                    LdsSrc src{lds, kbyte, vbyte};
-                    hash_generic<SHORT>(src, klen, vlen, st);
-                }
-            } else {
-                GlbSrc src{kb + kbeg, vb + vbeg, kb + kend, vb + vend};
-                hash_generic<SHORT>(src, klen, vlen, st);
-            }
+            hash_record<SHORT>(P, lds, kb, vb, kbeg, kend, vbeg, vend, st);
             store_digest(out + 32 * r, st);
         }
         if (!more) break;
@@ -472,12 +482,171 @@ __global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict_
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// DMA variant (round 2, MKV_LEAF_KERNEL=2): the next chunk goes global -> LDS with LDS-DMA loads
+// (global_load_lds_dwordx4: no VGPR destination) instead of the register prefetch, and on the
+// fixed-shape path (K0 / V0 = the configs' 32-B keys / 100-B values) every lane pulls its whole message
+// (kw + vw big-endian words) from LDS into registers at the start of a chunk, so the wave's LDS region is
+// free again before the compressions start and the DMA of the next chunk lands behind them. Without the
+// 36 prefetch VGPRs and with 8.5 KiB of LDS per wave, three workgroups per CU fit beside an ordering
+// workgroup (3 x 34 KiB + 55 KiB <= 160 KiB; 101 VGPRs). Chunks of any other shape are only listed
+// (ctr[1] = count, ctr[4..] = chunk ids) and hashed by k_leaf_list right after, so the general paths'
+// registers do not weigh on this kernel.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t LEAF_LDS_DMA = 8704;  // 64 x 132-B records + 2 x 16-B alignment slack + 32
+
+__device__ __forceinline__ void dma_chunk(const ChunkPlan &P, uint32_t lane, uint32_t *lds) {
+    const uint32_t tot = P.kspan + P.vspan;
+    const uint32_t ninst = (tot + 1023) / 1024;
+    for (uint32_t i = 0; i < ninst; ++i) {
+        const uint32_t byte = (lane + 64u * i) * 16u;
+        if (byte < tot) {
+            const uint8_t *g = byte < P.kspan ? P.kstart + byte : P.vstart + (byte - P.kspan);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), lds + 256u * i, 16, 0, 0);
+        }
+    }
+}
+
+template <bool SHORT, uint32_t K0, uint32_t V0, uint32_t BLK>
+__device__ __forceinline__ void hash_regs_block(uint32_t *m, uint32_t out[8]) {
+    using Sh = LeafShape<K0, V0>;
+    uint32_t w[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        uint32_t c = 0;
+        const uint32_t g = BLK * 16 + i;
+        const int kd = Sh::kind(g, &c);
+        w[i] = kd == 1 ? m[g - 1] : kd == 2 ? m[Sh::kw + g - Sh::vbeg] : c;
+    }
+    sha_compress_known<SHORT, LeafBlockKnown<K0, V0, BLK>, BLK == 0>(out, w);
+    if constexpr (BLK + 1 < Sh::NB) hash_regs_block<SHORT, K0, V0, BLK + 1>(m, out);
+}
+
+template <bool SHORT, uint32_t K0, uint32_t V0>
+__global__ __launch_bounds__(256) void k_leaf_dma(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                 const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                 uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
+                                                 uint32_t grain, KeyOut KO) {
+    using Sh = LeafShape<K0, V0>;
+    constexpr uint32_t MW = Sh::kw + Sh::vw;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_DMA / 4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *lds = lds_all + wave * (LEAF_LDS_DMA / 4);
+    const uint64_t nchunks = (n + 63) / 64;
+    ChunkSource<true> src{0, 0, 0, ctr, grain};
+    uint64_t c = src.get(lane);
+    if (c >= nchunks) return;  // wave-private work: no workgroup barrier anywhere
+
+    ChunkPlan P = plan_chunk<LEAF_LDS_DMA>(kb, koff, vb, voff, n, c * 64);
+    if (P.staged) dma_chunk(P, lane, lds);
+    uint64_t r = c * 64 + lane;
+    bool valid = r < n;
+    uint64_t kbeg = valid ? koff[r] : 0, kend = valid ? koff[r + 1] : 0;
+    uint64_t vbeg = valid ? voff[r] : 0, vend = valid ? voff[r + 1] : 0;
+    while (true) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c has landed in LDS
+        if (KO.kdst && P.kcopy_end <= KO.kcap) {  // key-ownership copy from the staged span
+            uint8_t *d = KO.kdst + (P.kstart - kb);
+            if (P.staged) {
+                const uint4 *l4 = reinterpret_cast<const uint4 *>(lds);
+                for (uint32_t i = lane; i * 16u < P.kspan; i += 64) reinterpret_cast<uint4 *>(d)[i] = l4[i];
+            } else {
+                const uint64_t span = P.kcopy_end - (uint64_t)(P.kstart - kb);
+                for (uint64_t b = 16ull * lane; b < span; b += 16ull * 64)
+                    *reinterpret_cast<uint4 *>(d + b) = *reinterpret_cast<const uint4 *>(P.kstart + b);
+            }
+        }
+        if (KO.odst && valid) {
+            KO.odst[r] = kbeg;
+            if (r + 1 == n) KO.odst[n] = kend;
+        }
+        const uint32_t klen = (uint32_t)(kend - kbeg), vlen = (uint32_t)(vend - vbeg);
+        const uint32_t kbyte = (uint32_t)((kb + kbeg) - P.kstart);
+        const uint32_t vbyte = P.kspan + (uint32_t)((vb + vbeg) - P.vstart);
+        const bool fixed = P.staged && __all(!valid || (klen == K0 && vlen == V0 && ((kbyte | vbyte) & 3) == 0));
+        if (!fixed && lane == 0) ctr[4 + atomicAdd(&ctr[1], 1u)] = (uint32_t)c;  // for k_leaf_list
+        uint32_t m[MW];
+        if (fixed) {
+#pragma unroll
+            for (uint32_t i = 0; i < Sh::kw; ++i) m[i] = bswap32(lds[(kbyte >> 2) + i]);
+#pragma unroll
+            for (uint32_t i = 0; i < Sh::vw; ++i) m[Sh::kw + i] = bswap32(lds[(vbyte >> 2) + i]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the region's reads are done: it may be refilled
+        // ---- next chunk: plan, offsets, and (fixed path) its DMA behind this chunk's compressions ----
+        const uint64_t cn = src.get(lane);
+        const bool more = cn < nchunks;
+        ChunkPlan Pn = P;
+        uint64_t nkb = 0, nke = 0, nvb = 0, nve = 0;
+        if (more) {
+            Pn = plan_chunk<LEAF_LDS_DMA>(kb, koff, vb, voff, n, cn * 64);
+            if (Pn.staged) dma_chunk(Pn, lane, lds);
+            const uint64_t rn = cn * 64 + lane;
+            if (rn < n) {
+                nkb = koff[rn];
+                nke = koff[rn + 1];
+                nvb = voff[rn];
+                nve = voff[rn + 1];
+            }
+        }
+        if (fixed && valid) {
+            uint32_t st[8];
+            sha_init(st);
+            hash_regs_block<SHORT, K0, V0, 0>(m, st);
+            store_digest(out + 32 * r, st);
+        }
+        if (!more) break;
+        c = cn;
+        P = Pn;
+        r = c * 64 + lane;
+        valid = r < n;
+        kbeg = nkb;
+        kend = nke;
+        vbeg = nvb;
+        vend = nve;
+    }
+}
+
+// The chunks k_leaf_dma listed (any shape but the fixed one): one wave per listed chunk, staged through
+// the wave's private LDS region exactly like k_leaf_persist.
+template <bool SHORT>
+__global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                  const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                  uint64_t n, uint8_t *__restrict__ out,
+                                                  const uint32_t *__restrict__ ctr) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *lds = lds_all + wave * (LEAF_LDS_WAVE / 4);
+    const uint32_t cnt = ctr[1];
+    for (uint64_t e = (uint64_t)blockIdx.x * LEAF_WAVES + wave; e < cnt; e += (uint64_t)gridDim.x * LEAF_WAVES) {
+        const uint64_t c = ctr[4 + e];
+        const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
+        if (P.staged) {
+            uint4 R[PF];
+            load_chunk(P, lane, R);
+            store_chunk(P, lane, R, lds);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        const uint64_t r = c * 64 + lane;
+        if (r < n) {
+            uint32_t st[8];
+            hash_record<SHORT>(P, lds, kb, vb, koff[r], koff[r + 1], voff[r], voff[r + 1], st);
+            store_digest(out + 32 * r, st);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the region is refilled
+    }
+}
+
 }  // namespace
+
+size_t leaf_ctr_words(uint64_t n) { return 4 + (size_t)((n + 63) / 64); }
 
 static int leaf_kernel_variant() {
     static const int v = [] {
-        const char *e = getenv("MKV_LEAF_KERNEL");
-        return e ? atoi(e) : 1;
+        const char *e = getenv("MKV_LEAF_KERNEL");  // 2 = k_leaf_dma (default), 1 = k_leaf_persist, 0 = k_leaf_hash
+        return e ? atoi(e) : 2;
     }();
     return v;
 }
@@ -496,7 +665,39 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
     if (n == 0) return false;
     uint64_t waves = ceil_div(n, 64);
     uint64_t blocks = ceil_div(waves, LEAF_WAVES);
-    if (leaf_kernel_variant() == 1) {
+    if (leaf_kernel_variant() == 2 && ctr) {
+        static int cus2 = [] {
+            int dev = 0, c = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+            return c > 0 ? c : 256;
+        }();
+        static int wgs2 = [] {
+            // 2 per CU: with 3 the leaf hash runs 1.27 instead of 1.45 ms but the co-running ordering
+            // stage stretches to 1.4-1.65 ms and becomes the critical path (build 2.32-2.60 vs 2.31 ms)
+            const char *e = getenv("MKV_LEAF_WGS");
+            int v = e ? atoi(e) : 2;
+            return v < 1 ? 1 : (v > 4 ? 4 : v);
+        }();
+        const uint64_t pblocks = std::min<uint64_t>(blocks, (uint64_t)cus2 * wgs2);
+        const uint32_t grain = std::max<uint32_t>(leaf_dyn_grain(), 1u);
+        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
+        MKV_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), st));
+        if (sha_variant() == 0) {
+            hipLaunchKernelGGL((k_leaf_dma<false, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                               vb, voff, n, out, ctr, grain, KO);
+            hipLaunchKernelGGL(k_leaf_list<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb,
+                               voff, n, out, ctr);
+        } else {
+            hipLaunchKernelGGL((k_leaf_dma<true, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                               vb, voff, n, out, ctr, grain, KO);
+            hipLaunchKernelGGL(k_leaf_list<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb,
+                               voff, n, out, ctr);
+        }
+        MKV_LAUNCH_CHECK();
+        return KO.kdst != nullptr;
+    }
+    if (leaf_kernel_variant() >= 1) {
         static int cus = [] {
             int dev = 0, c = 0;
             (void)hipGetDevice(&dev);

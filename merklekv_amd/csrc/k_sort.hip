@@ -393,30 +393,72 @@ template <class T> void scan_impl(const T *in, T *out, uint64_t n, T *total, voi
 
 // ---- ties / refinement ----
 // tie[i] = prefix of i equals prefix of i-1 (count[0] += ties). Run heads (positions starting a tie
-// run) are appended to heads[] (wave-aggregated, count[1] = number of heads), so the refinement visits
-// only the runs instead of scanning all n flags.
-__global__ void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, int shift, uint8_t *__restrict__ tie,
-                            uint32_t *__restrict__ count, uint32_t *__restrict__ heads) {
+// run) are appended to heads[] (count[1] = number of heads), so the refinement visits only the runs
+// instead of scanning all n flags. Same-address device atomics serialize across the XCDs (~10 ns each):
+// a per-wave append cost ~0.5 ms at 46K heads, so each 1024-thread block walks a contiguous span,
+// buffers its heads in LDS and publishes them with one atomic per 4,096 heads (plus one for its ties).
+constexpr int MT_THREADS = 1024;
+constexpr uint32_t MT_BUF = 4096;
+__global__ __launch_bounds__(MT_THREADS) void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, int shift,
+                                                         uint8_t *__restrict__ tie, uint32_t *__restrict__ count,
+                                                         uint32_t *__restrict__ heads) {
     sort_prio();
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool t = false, h = false;
-    if (i < n) {
-        const uint64_t p = pfx[i] >> shift;
-        t = i > 0 && p == (pfx[i - 1] >> shift);
-        h = !t && i + 1 < n && (pfx[i + 1] >> shift) == p;
-        tie[i] = t;
-    } else if (i == n) {
-        tie[n] = 0;
+    __shared__ uint32_t buf[MT_BUF];
+    __shared__ uint32_t wcnt[MT_THREADS / 64];
+    __shared__ uint32_t sbase;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t tot_n = n + 1;  // position n writes the tie[n] = 0 sentinel
+    const uint64_t per = ((tot_n + gridDim.x - 1) / gridDim.x + MT_THREADS - 1) / MT_THREADS * MT_THREADS;
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = lo + per < tot_n ? lo + per : tot_n;
+    uint32_t nt = 0, nb = 0;  // nb: block-uniform count of buffered heads
+    auto flush = [&]() {
+        if (threadIdx.x == 0) sbase = atomicAdd(&count[1], nb);
+        __syncthreads();
+        const uint32_t b = sbase;
+        for (uint32_t j = threadIdx.x; j < nb; j += MT_THREADS) heads[b + j] = buf[j];
+        __syncthreads();
+        nb = 0;
+    };
+    for (uint64_t i0 = lo; i0 < hi; i0 += MT_THREADS) {
+        const uint64_t i = i0 + threadIdx.x;
+        bool t = false, h = false;
+        if (i < n) {
+            const uint64_t p = pfx[i] >> shift;
+            t = i > 0 && p == (pfx[i - 1] >> shift);
+            h = !t && i + 1 < n && (pfx[i + 1] >> shift) == p;
+            tie[i] = t;
+        } else if (i == n && i < hi) {
+            tie[n] = 0;
+        }
+        nt += t;
+        const uint64_t hm = __ballot(h);
+        if (lane == 0) wcnt[w] = (uint32_t)__popcll(hm);
+        __syncthreads();
+        uint32_t off = 0, tot = 0;
+#pragma unroll
+        for (int k = 0; k < MT_THREADS / 64; ++k) {
+            const uint32_t c = wcnt[k];
+            off += k < (int)w ? c : 0u;
+            tot += c;
+        }
+        if (tot && nb + tot > MT_BUF) flush();
+        if (h) buf[nb + off + (uint32_t)__popcll(hm & lt)] = (uint32_t)i;
+        nb += tot;
+        __syncthreads();  // wcnt is rewritten by the next iteration
     }
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t m = __ballot(t);
-    if (lane == 0 && m) atomicAdd(&count[0], (uint32_t)__popcll(m));
-    const uint64_t hm = __ballot(h);
-    if (hm) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&count[1], (uint32_t)__popcll(hm));
-        base = __shfl(base, 0);
-        if (h) heads[base + (uint32_t)__popcll(hm & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    if (nb) flush();
+    // ties: wave sums, then one atomic per block
+    uint32_t x = nt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) wcnt[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tt = 0;
+        for (int k = 0; k < MT_THREADS / 64; ++k) tt += wcnt[k];
+        if (tt) atomicAdd(&count[0], tt);
     }
 }
 
@@ -774,7 +816,8 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
 
 void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, uint32_t *heads,
                       hipStream_t st, int shift) {
-    hipLaunchKernelGGL(k_mark_ties, grid1d(n + 1), dim3(256), 0, st, pfx, n, shift, tie, count, heads);
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n + 1, (uint64_t)MT_THREADS * 4), 512);
+    hipLaunchKernelGGL(k_mark_ties, dim3(blocks), dim3(MT_THREADS), 0, st, pfx, n, shift, tie, count, heads);
     MKV_LAUNCH_CHECK();
 }
 void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint64_t *pfx,

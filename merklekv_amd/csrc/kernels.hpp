@@ -6,6 +6,8 @@
 namespace mkv {
 
 // ---- Kernel A: leaf hashing (k_leaf.hip) ----
+// Words of the leaf hash's device counter block (ctr): chunk hand-out counter + listed-chunk count + list.
+size_t leaf_ctr_words(uint64_t n);
 // ctr: optional device u32 for the dynamic chunk hand-out (MKV_LEAF_DYN grain > 0); zeroed by the launch.
 // kcopy/kcap/ocopy: optional fused key-ownership copy (keys at the same byte offsets into kcopy, at most
 // kcap bytes; offsets[0..n] into ocopy). Returns true when the key copy was fused (persistent kernel and

@@ -2,7 +2,7 @@
 """Summarise a scripts/gpu_prof.sh run (gpurun_out/prof) into profiles/:
   <tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   <tag>_pmc.json           per-kernel averages of every PMC counter collected + derived metrics
-  pmc_leaf_hash.json       HBM bytes per k_leaf_hash launch (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction)
+  pmc_leaf_hash.json       HBM bytes per leaf-hash launch (k_leaf_dma / k_leaf_persist / k_leaf_hash) (FETCH_SIZE x 2 + WRITE_SIZE, gfx950 correction)
   pmc_diff_merge.json      HBM bytes per merge-join diff (sum over its kernels), when k_diff_pass1 ran
 Usage: python scripts/prof_summary.py <tag> [n_records] [prof_dir under gpurun_out/]
 """
@@ -60,11 +60,12 @@ def main():
             e["issue_stall_frac"] = e["SQ_WAIT_INST_ANY"] / e["SQ_WAVE_CYCLES"]
         summary[k] = e
     json.dump(summary, open(os.path.join(OUT, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    lh = summary.get("k_leaf_persist") or summary.get("k_leaf_hash")
+    lk = next((k for k in ("k_leaf_dma", "k_leaf_persist", "k_leaf_hash") if k in summary), None)
+    lh = summary.get(lk) if lk else None
     diff_run = "k_diff_pass1" in summary  # the diff workload also builds trees: keep the build's leaf figure
     if lh and "hbm_bytes_corrected" in lh and not diff_run:
         rec = {"n": n, "hbm_bytes_per_launch": lh["hbm_bytes_corrected"], "source": f"{tag}_pmc.json",
-               "kernel": "k_leaf_persist" if "k_leaf_persist" in summary else "k_leaf_hash",
+               "kernel": lk,
                "algorithmic_bytes_per_launch": 172 * n,
                "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes; VALU counters per "
                        "launch with the duration of the pass that collected GRBM_GUI_ACTIVE"}
