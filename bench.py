@@ -164,12 +164,12 @@ def random_values(torch, m, dev, gen):
 
 # ============================================================================================ build
 def leaf_roofline(n, leaf_avg_ms, launches):
-    """roofline of the dominant kernel (the leaf hash, k_leaf_dma). achieved = 172 B/leaf x n / live launch time (HIP
+    """roofline of the dominant kernel (the leaf hash, k_leaf_direct). achieved = 172 B/leaf x n / live launch time (HIP
     events on the tree's stream, sort co-running); traffic and the VALU fractions come from the PMC file
     of the same tree (profiles/pmc_leaf_hash.json, written by scripts/prof_summary.py)."""
     achieved = LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_leaf_dma",
+           "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_leaf_direct",
            "bytes_per_leaf": LEAF_BYTES, "avg_launch_ms": leaf_avg_ms, "launches": launches,
            "gb_per_s_hashed": (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9,
            "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): the HBM frac ceiling is ~0.39; "
@@ -179,7 +179,7 @@ def leaf_roofline(n, leaf_avg_ms, launches):
         pm = json.load(open(pmc_path))
     except (OSError, ValueError):
         pm = None
-    if pm and pm.get("n") == n and pm.get("kernel", "k_leaf_dma") == out["kernel"]:
+    if pm and pm.get("n") == n and pm.get("kernel") == out["kernel"]:
         out["traffic"] = pm.get("hbm_bytes_per_launch")
         out["traffic_source"] = pm.get("source")
         vi, gui, dur = pm.get("SQ_INSTS_VALU"), pm.get("GRBM_GUI_ACTIVE"), pm.get("avg_duration_us")

@@ -608,7 +608,95 @@ __global__ __launch_bounds__(256) void k_leaf_dma(const uint8_t *__restrict__ kb
     }
 }
 
-// The chunks k_leaf_dma listed (any shape but the fixed one): one wave per listed chunk, staged through
+// ---------------------------------------------------------------------------------------------
+// Direct variant (round 2, MKV_LEAF_KERNEL=3): no LDS at all. On the fixed-shape path every lane loads
+// its own record's message straight from HBM into registers (16-B loads at 4-B alignment: gfx950 serves
+// unaligned global loads; the 64 lanes' spans are contiguous, so the L1/L2 lines a wave touches are the
+// ones a coalesced copy would fetch). Without an LDS region the leaf hash no longer competes with the
+// co-running ordering kernels for LDS, and at ~70 VGPRs several more waves fit per SIMD to hide the
+// load latency. Non-fixed chunks are listed for k_leaf_list as in k_leaf_dma.
+// ---------------------------------------------------------------------------------------------
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+template <uint32_t NW>
+__device__ __forceinline__ void load_words_a4(const uint8_t *p, uint32_t *w) {
+    const u32x4_a4 *q = reinterpret_cast<const u32x4_a4 *>(p);
+#pragma unroll
+    for (uint32_t i = 0; i < NW / 4; ++i) {
+        const u32x4_a4 x = q[i];
+        w[4 * i] = x.x;
+        w[4 * i + 1] = x.y;
+        w[4 * i + 2] = x.z;
+        w[4 * i + 3] = x.w;
+    }
+#pragma unroll
+    for (uint32_t i = NW / 4 * 4; i < NW; ++i) w[i] = reinterpret_cast<const uint32_t *>(p)[i];
+}
+
+template <uint32_t NW>
+__device__ __forceinline__ void store_words_a4(uint8_t *p, const uint32_t *w) {
+    u32x4_a4 *q = reinterpret_cast<u32x4_a4 *>(p);
+#pragma unroll
+    for (uint32_t i = 0; i < NW / 4; ++i) q[i] = u32x4_a4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+#pragma unroll
+    for (uint32_t i = NW / 4 * 4; i < NW; ++i) reinterpret_cast<uint32_t *>(p)[i] = w[i];
+}
+
+template <bool SHORT, uint32_t K0, uint32_t V0>
+__global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                    const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                    uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
+                                                    uint32_t grain, KeyOut KO) {
+    using Sh = LeafShape<K0, V0>;
+    constexpr uint32_t MW = Sh::kw + Sh::vw;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nchunks = (n + 63) / 64;
+    ChunkSource<true> src{0, 0, 0, ctr, grain};
+    for (uint64_t c = src.get(lane); c < nchunks; c = src.get(lane)) {
+        const uint64_t r = c * 64 + lane;
+        const bool valid = r < n;
+        const uint64_t kbeg = valid ? koff[r] : 0, kend = valid ? koff[r + 1] : 0;
+        const uint64_t vbeg = valid ? voff[r] : 0, vend = valid ? voff[r + 1] : 0;
+        const uint8_t *kp = kb + kbeg, *vp = vb + vbeg;
+        const bool fixed =
+            __all(!valid || (kend - kbeg == K0 && vend - vbeg == V0 &&
+                             ((reinterpret_cast<uintptr_t>(kp) | reinterpret_cast<uintptr_t>(vp)) & 3) == 0));
+        if (!fixed) {
+            if (lane == 0) ctr[4 + atomicAdd(&ctr[1], 1u)] = (uint32_t)c;  // hashed by k_leaf_list
+            if (KO.kdst) {  // key-ownership copy of the chunk's span
+                const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
+                if (P.kcopy_end <= KO.kcap) {
+                    uint8_t *d = KO.kdst + (P.kstart - kb);
+                    const uint64_t span = P.kcopy_end - (uint64_t)(P.kstart - kb);
+                    for (uint64_t b = 16ull * lane; b < span; b += 16ull * 64)
+                        *reinterpret_cast<uint4 *>(d + b) = *reinterpret_cast<const uint4 *>(P.kstart + b);
+                }
+            }
+            if (KO.odst && valid) {
+                KO.odst[r] = kbeg;
+                if (r + 1 == n) KO.odst[n] = kend;
+            }
+            continue;
+        }
+        if (!valid) continue;
+        uint32_t m[MW];
+        load_words_a4<Sh::kw>(kp, m);
+        load_words_a4<Sh::vw>(vp, m + Sh::kw);
+        if (KO.kdst && kend <= KO.kcap) store_words_a4<Sh::kw>(KO.kdst + kbeg, m);
+        if (KO.odst) {
+            KO.odst[r] = kbeg;
+            if (r + 1 == n) KO.odst[n] = kend;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < MW; ++i) m[i] = bswap32(m[i]);
+        uint32_t st[8];
+        sha_init(st);
+        hash_regs_block<SHORT, K0, V0, 0>(m, st);
+        store_digest(out + 32 * r, st);
+    }
+}
+
+// The chunks k_leaf_dma / k_leaf_direct listed (any shape but the fixed one): one wave per listed chunk, staged through
 // the wave's private LDS region exactly like k_leaf_persist.
 template <bool SHORT>
 __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
@@ -643,10 +731,21 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
 
 size_t leaf_ctr_words(uint64_t n) { return 4 + (size_t)((n + 63) / 64); }
 
+// SHA round form of k_leaf_direct (MKV_LEAF_SHA, default 0 = plain association, fewer instructions):
+// with the LDS-free kernel the short-chain form (1) measured slower (leaf 1.38 vs 1.32 ms beside the sort)
+static int leaf_sha_variant() {
+    static const int v = [] {
+        const char *e = getenv("MKV_LEAF_SHA");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 static int leaf_kernel_variant() {
     static const int v = [] {
-        const char *e = getenv("MKV_LEAF_KERNEL");  // 2 = k_leaf_dma (default), 1 = k_leaf_persist, 0 = k_leaf_hash
-        return e ? atoi(e) : 2;
+        // 3 = k_leaf_direct (default), 2 = k_leaf_dma, 1 = k_leaf_persist, 0 = k_leaf_hash
+        const char *e = getenv("MKV_LEAF_KERNEL");
+        return e ? atoi(e) : 3;
     }();
     return v;
 }
@@ -665,6 +764,41 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
     if (n == 0) return false;
     uint64_t waves = ceil_div(n, 64);
     uint64_t blocks = ceil_div(waves, LEAF_WAVES);
+    if (leaf_kernel_variant() == 3 && ctr) {
+        static int cus3 = [] {
+            int dev = 0, c = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+            return c > 0 ? c : 256;
+        }();
+        static int wgs3 = [] {
+            const char *e = getenv("MKV_LEAF_WGS");
+            int v = e ? atoi(e) : 2;
+            return v < 1 ? 1 : (v > 8 ? 8 : v);
+        }();
+        static const int grid3 = [] {  // MKV_LEAF_GRID (A/B knob): total workgroups instead of wgs per CU
+            const char *e = getenv("MKV_LEAF_GRID");
+            return e ? atoi(e) : 0;
+        }();
+        const uint64_t pblocks = std::min<uint64_t>(blocks, grid3 > 0 ? (uint64_t)grid3 : (uint64_t)cus3 * wgs3);
+        const uint32_t grain = std::max<uint32_t>(leaf_dyn_grain(), 1u);
+        // the span copy of listed chunks rounds to 16 B like the staged paths: kb must be 16-B aligned
+        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
+        MKV_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), st));
+        if (leaf_sha_variant() == 0) {
+            hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
+                               koff, vb, voff, n, out, ctr, grain, KO);
+            hipLaunchKernelGGL(k_leaf_list<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb,
+                               voff, n, out, ctr);
+        } else {
+            hipLaunchKernelGGL((k_leaf_direct<true, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
+                               koff, vb, voff, n, out, ctr, grain, KO);
+            hipLaunchKernelGGL(k_leaf_list<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb,
+                               voff, n, out, ctr);
+        }
+        MKV_LAUNCH_CHECK();
+        return KO.kdst != nullptr;
+    }
     if (leaf_kernel_variant() == 2 && ctr) {
         static int cus2 = [] {
             int dev = 0, c = 0;

@@ -60,7 +60,7 @@ def main():
             e["issue_stall_frac"] = e["SQ_WAIT_INST_ANY"] / e["SQ_WAVE_CYCLES"]
         summary[k] = e
     json.dump(summary, open(os.path.join(OUT, f"{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
-    lk = next((k for k in ("k_leaf_dma", "k_leaf_persist", "k_leaf_hash") if k in summary), None)
+    lk = next((k for k in ("k_leaf_direct", "k_leaf_dma", "k_leaf_persist", "k_leaf_hash") if k in summary), None)
     lh = summary.get(lk) if lk else None
     diff_run = "k_diff_pass1" in summary  # the diff workload also builds trees: keep the build's leaf figure
     if lh and "hbm_bytes_corrected" in lh and not diff_run:
