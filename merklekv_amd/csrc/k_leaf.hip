@@ -218,13 +218,13 @@ __device__ __forceinline__ void hash_fast_any(const uint32_t *lds, uint32_t kwor
     else hash_fast<SHORT>(lds, kword, vword, K0, V0, out);
 }
 
+// One workgroup tile (LEAF_WAVES x 64 records starting at record 256 x bx) of k_leaf_hash / k_leaf_multi.
 template <bool SHORT>
-__global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
-                                                  const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
-                                                  uint64_t n, uint8_t *__restrict__ out) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
+__device__ __forceinline__ void leaf_hash_tile(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                               const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                               uint64_t n, uint8_t *__restrict__ out, uint64_t bx, uint32_t *lds_all) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t r0 = ((uint64_t)blockIdx.x * LEAF_WAVES + wave) * 64;
+    const uint64_t r0 = (bx * LEAF_WAVES + wave) * 64;
     const bool wave_live = r0 < n;
     const uint64_t r = r0 + lane;
     const bool valid = r < n;
@@ -279,6 +279,24 @@ __global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ k
         hash_generic<SHORT>(src, klen, vlen, st);
     }
     store_digest(out + 32 * r, st);
+}
+
+template <bool SHORT>
+__global__ __launch_bounds__(256) void k_leaf_hash(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                  const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                  uint64_t n, uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
+    leaf_hash_tile<SHORT>(kb, koff, vb, voff, n, out, blockIdx.x, lds_all);
+}
+
+// k batches at once (grid.y = batch): batch b's digests go to out + 32 x base[b] (dirty-path updates of
+// several replicas in one launch instead of one small launch per replica).
+template <bool SHORT>
+__global__ __launch_bounds__(256) void k_leaf_multi(LeafBatches B, uint8_t *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[LEAF_WAVES * LEAF_LDS_WAVE / 4];
+    const uint32_t b = blockIdx.y;
+    if ((uint64_t)blockIdx.x * LEAF_WAVES * 64 >= B.m[b]) return;  // uniform per workgroup
+    leaf_hash_tile<SHORT>(B.kb[b], B.koff[b], B.vb[b], B.voff[b], B.m[b], out + 32 * B.base[b], blockIdx.x, lds_all);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -728,6 +746,16 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
 }
 
 }  // namespace
+
+void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uint8_t *out, hipStream_t st) {
+    if (!k || !mmax) return;
+    const dim3 grid((uint32_t)ceil_div(mmax, (uint64_t)LEAF_WAVES * 64), k);
+    if (sha_variant() == 0)
+        hipLaunchKernelGGL(k_leaf_multi<false>, grid, dim3(64 * LEAF_WAVES), 0, st, B, out);
+    else
+        hipLaunchKernelGGL(k_leaf_multi<true>, grid, dim3(64 * LEAF_WAVES), 0, st, B, out);
+    MKV_LAUNCH_CHECK();
+}
 
 size_t leaf_ctr_words(uint64_t n) { return 4 + (size_t)((n + 63) / 64); }
 

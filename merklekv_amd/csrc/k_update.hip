@@ -38,56 +38,79 @@ __device__ __forceinline__ const uint8_t *tree_key(const DiffSide &T, uint64_t i
     return T.kb + a;
 }
 
+// Sorted position of key k in tree T, UINT64_MAX when it is not a leaf.
+__device__ __forceinline__ uint64_t locate_one(const uint8_t *k, uint64_t len, const DiffSide &T) {
+    const uint64_t c0 = key_chunk(k, len, 0);
+    uint64_t lo = 0, hi = T.n;  // first position with pfx >= c0
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (T.pfx[mid] < c0) lo = mid + 1;
+        else hi = mid;
+    }
+    uint64_t found = UINT64_MAX;
+    if (lo < T.n && T.pfx[lo] == c0) {
+        // Equal-prefix run [lo, e): keys sharing >= 8 leading bytes ("tenant/0001/obj/...") can make
+        // it the whole tree, so it is binary-searched on the full key (lower_bound with key_cmp),
+        // never walked: O(log n) full-key compares per batch key.
+        uint64_t e = lo + 1;
+        if (e < T.n && T.pfx[e] == c0) {
+            uint64_t a = e, b = T.n;  // first position with pfx > c0
+            while (a < b) {
+                const uint64_t mid = (a + b) >> 1;
+                if (T.pfx[mid] <= c0) a = mid + 1;
+                else b = mid;
+            }
+            e = a;
+        }
+        uint64_t a = lo, b = e;
+        while (a < b) {
+            const uint64_t mid = (a + b) >> 1;
+            uint64_t tl;
+            const uint8_t *tk = tree_key(T, mid, &tl);
+            if (key_cmp(tk, tl, c0, k, len, c0) < 0) a = mid + 1;
+            else b = mid;
+        }
+        if (a < e) {
+            uint64_t tl;
+            const uint8_t *tk = tree_key(T, a, &tl);
+            if (key_cmp(k, len, c0, tk, tl, c0) == 0) found = a;
+        }
+    }
+    return found;
+}
+
 __global__ __launch_bounds__(256) void k_locate(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                 uint64_t m, DiffSide T, uint64_t *__restrict__ pos,
                                                 uint32_t *__restrict__ idx, uint32_t *__restrict__ missing) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool miss = false;
     if (i < m) {
-        const uint64_t a = koff[i], len = koff[i + 1] - a;
-        const uint8_t *k = kb + a;
-        const uint64_t c0 = key_chunk(k, len, 0);
-        uint64_t lo = 0, hi = T.n;  // first position with pfx >= c0
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (T.pfx[mid] < c0) lo = mid + 1;
-            else hi = mid;
-        }
-        uint64_t found = UINT64_MAX;
-        if (lo < T.n && T.pfx[lo] == c0) {
-            // Equal-prefix run [lo, e): keys sharing >= 8 leading bytes ("tenant/0001/obj/...") can make
-            // it the whole tree, so it is binary-searched on the full key (lower_bound with key_cmp),
-            // never walked: O(log n) full-key compares per batch key.
-            uint64_t e = lo + 1;
-            if (e < T.n && T.pfx[e] == c0) {
-                uint64_t a = e, b = T.n;  // first position with pfx > c0
-                while (a < b) {
-                    const uint64_t mid = (a + b) >> 1;
-                    if (T.pfx[mid] <= c0) a = mid + 1;
-                    else b = mid;
-                }
-                e = a;
-            }
-            uint64_t a = lo, b = e;
-            while (a < b) {
-                const uint64_t mid = (a + b) >> 1;
-                uint64_t tl;
-                const uint8_t *tk = tree_key(T, mid, &tl);
-                if (key_cmp(tk, tl, c0, k, len, c0) < 0) a = mid + 1;
-                else b = mid;
-            }
-            if (a < e) {
-                uint64_t tl;
-                const uint8_t *tk = tree_key(T, a, &tl);
-                if (key_cmp(k, len, c0, tk, tl, c0) == 0) found = a;
-            }
-        }
+        const uint64_t a = koff[i];
+        const uint64_t found = locate_one(kb + a, koff[i + 1] - a, T);
         miss = found == UINT64_MAX;
         pos[i] = found;
         idx[i] = (uint32_t)i;
     }
     const uint64_t b = __ballot(miss);
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(missing, (uint32_t)__popcll(b));
+}
+
+__global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti L, int pbits,
+                                                      uint64_t *__restrict__ pos, uint32_t *__restrict__ idx) {
+    const uint32_t t = blockIdx.y;
+    const uint64_t m = B.m[t];
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool miss = false;
+    if (i < m) {
+        const uint64_t a = B.koff[t][i];
+        const uint64_t found = locate_one(B.kb[t] + a, B.koff[t][i + 1] - a, L.T[t]);
+        miss = found == UINT64_MAX;
+        const uint64_t g = B.base[t] + i;
+        pos[g] = ((uint64_t)t << pbits) | (miss ? (1ull << pbits) - 1ull : found);
+        idx[g] = (uint32_t)g;
+    }
+    const uint64_t b = __ballot(miss);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(L.missing[t], (uint32_t)__popcll(b));
 }
 
 __device__ __forceinline__ void set_bit(uint32_t *bm, uint64_t b) { atomicOr(bm + (b >> 5), 1u << (b & 31)); }
@@ -102,7 +125,8 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
                                                       const uint32_t *__restrict__ bidx, uint64_t m,
                                                       const uint8_t *__restrict__ bdig, uint8_t *__restrict__ nodes0,
                                                       uint32_t *__restrict__ bm, uint32_t *__restrict__ list,
-                                                      uint32_t *__restrict__ count, const uint32_t *__restrict__ missing) {
+                                                      uint32_t *__restrict__ count, const uint32_t *__restrict__ missing,
+                                                      uint64_t pmask) {
     __shared__ uint32_t sapp[17];
     if (*missing) return;  // some batch key is not a leaf: the caller takes the merge path, tree untouched
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -111,7 +135,7 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
     if (s < m) {
         const uint64_t q = pos[s];
         act = (s + 1 == m) || pos[s + 1] != q;
-        p = (uint32_t)q;
+        p = (uint32_t)(q & pmask);
         if (act) {
             const uint4 *src = reinterpret_cast<const uint4 *>(bdig + 32ull * bidx[s]);
             uint4 *dst = reinterpret_cast<uint4 *>(nodes0 + 32ull * p);
@@ -380,10 +404,18 @@ void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const Di
 }
 
 void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
-                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st) {
+                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st,
+                         uint64_t pmask) {
     if (!m) return;
     hipLaunchKernelGGL(k_dirty_leaves, grid1d(m), dim3(256), 0, st, pos, bidx, m, bdig, nodes0, bm, list, count,
-                       missing);
+                       missing, pmask);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
+                         uint64_t *pos, uint32_t *idx, hipStream_t st) {
+    if (!k || !mmax) return;
+    hipLaunchKernelGGL(k_locate_multi, dim3((uint32_t)ceil_div(mmax, 256), k), dim3(256), 0, st, B, L, pbits, pos, idx);
     MKV_LAUNCH_CHECK();
 }
 

@@ -6,6 +6,17 @@
 namespace mkv {
 
 // ---- Kernel A: leaf hashing (k_leaf.hip) ----
+// Up to 16 record batches hashed in one launch (dirty-path updates of several replicas).
+constexpr int LEAF_MULTI_MAX = 16;
+struct LeafBatches {
+    const uint8_t *kb[LEAF_MULTI_MAX];
+    const uint64_t *koff[LEAF_MULTI_MAX];
+    const uint8_t *vb[LEAF_MULTI_MAX];
+    const uint64_t *voff[LEAF_MULTI_MAX];
+    uint64_t m[LEAF_MULTI_MAX];
+    uint64_t base[LEAF_MULTI_MAX];  // batch b's digests at out + 32 x base[b]
+};
+void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uint8_t *out, hipStream_t st);
 // Words of the leaf hash's device counter block (ctr): chunk hand-out counter + listed-chunk count + list.
 size_t leaf_ctr_words(uint64_t n);
 // ctr: optional device u32 for the dynamic chunk hand-out (MKV_LEAF_DYN grain > 0); zeroed by the launch.
@@ -195,9 +206,20 @@ void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t ple
 // *missing += keys that are not leaves.
 void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, uint64_t *pos,
                    uint32_t *idx, uint32_t *missing, hipStream_t st);
+// k trees at once (grid.y = tree): batch b of tree b (keys B.kb/B.koff, B.m records) located in T[b];
+// pos[base_b + i] = (b << pbits) | position (position (1 << pbits) - 1 when the key is not a leaf: then
+// *missing[b] += 1), idx[base_b + i] = base_b + i.
+struct LocateMulti {
+    DiffSide T[LEAF_MULTI_MAX];
+    uint32_t *missing[LEAF_MULTI_MAX];
+};
+void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
+                         uint64_t *pos, uint32_t *idx, hipStream_t st);
 // (pos, bidx) sorted by pos (stable): scatter the last write per position into level 0, mark dirty.
+// Positions are pos & pmask (multi-tree sort keys carry the tree above the position bits).
 void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
-                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st);
+                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st,
+                         uint64_t pmask = ~0ull);
 // Level l of the local plan: owned global range [a, a+c) stored at node offset off, global size S;
 // parent level (l+1) and child level (l-1) ranges for ownership tests and bit clearing.
 struct DirtyLevel {

@@ -1501,20 +1501,66 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             had_root[q] = t->has_root;
             had_pending[q] = t->combine_pending;
         }
-        MKV_HIP(hipEventRecord(t0->ev_in, st));
         DirtyTrees T{};
         uint64_t mmax = 0;
-        for (size_t q = 0; q < g.size(); ++q) {
-            mkv_tree *t = ts[g[q]];
-            if (q) MKV_HIP(hipStreamWaitEvent(t->st, t0->ev_in, 0));
-            T.t[q] = dirty_prepare(t, bs[g[q]]);
-            mmax = std::max(mmax, bs[g[q]].m);
-            if (q) {
-                MKV_HIP(hipEventRecord(t->ev_join, t->st));
-                MKV_HIP(hipStreamWaitEvent(st, t->ev_join, 0));
-            }
-        }
         const uint32_t k2 = (uint32_t)g.size();
+        if (k2 == 1) {
+            T.t[0] = dirty_prepare(t0, bs[g[0]]);
+            mmax = bs[g[0]].m;
+        } else {
+            // Phase 1 of all k2 trees in single launches on st (round 2): one locate (grid.y = tree), one
+            // hash of all batches, one sort of (tree, position) keys, then per-tree scatters. One launch
+            // chain per tree on its own stream serialised on the device's few hardware queues (~1.06 ms
+            // for 7 replicas at 125K keys each).
+            for (size_t q = 1; q < g.size(); ++q) {  // any earlier work on the other trees' streams first
+                mkv_tree *t = ts[g[q]];
+                MKV_HIP(hipEventRecord(t->ev_in, t->st));
+                MKV_HIP(hipStreamWaitEvent(st, t->ev_in, 0));
+            }
+            LeafBatches B{};
+            LocateMulti LM{};
+            uint64_t M = 0;
+            for (size_t q = 0; q < g.size(); ++q) {
+                mkv_tree *t = ts[g[q]];
+                const DirtyBatch &b = bs[g[q]];
+                B.kb[q] = b.kb;
+                B.koff[q] = b.koff;
+                B.vb[q] = b.vb;
+                B.voff[q] = b.voff;
+                B.m[q] = b.m;
+                B.base[q] = M;
+                M += b.m;
+                mmax = std::max(mmax, b.m);
+                const uint64_t nn = total_nodes(t);
+                const uint64_t words = (nn + 63) / 32 + 2;
+                uint32_t *bm = ens<uint32_t>(t->u_bm, words);
+                if (t->bm_bits < nn || t->bm_dirty) {
+                    MKV_HIP(hipMemsetAsync(bm, 0, words * 4, st));
+                    t->bm_bits = words * 32 - 64;
+                }
+                uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);
+                MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, st));
+                uint32_t *l0 = ens<uint32_t>(t->u_l0, b.m + 1), *l1 = ens<uint32_t>(t->u_l1, b.m + 1);
+                T.t[q] = DirtyTree{t->nodes.as<uint8_t>(), bm, l0, l1, cnt, cnt + L + 1};
+                LM.T[q] = side_of(t);
+                LM.missing[q] = cnt + L + 1;
+                t->bm_dirty = true;
+            }
+            const int pbits = bits_for(t0->n);
+            uint64_t *pos = ens<uint64_t>(t0->u_pos, M + 1), *pos2 = ens<uint64_t>(t0->u_pos2, M + 1);
+            uint32_t *idx = ens<uint32_t>(t0->u_idx, M + 1), *idx2 = ens<uint32_t>(t0->u_idx2, M + 1);
+            uint8_t *bdig = ens<uint8_t>(t0->u_dig, M * 32);
+            launch_locate_multi(B, LM, k2, mmax, pbits, pos, idx, st);
+            launch_leaf_hash_multi(B, k2, mmax, bdig, st);
+            void *radix = t0->s_radix.ensure(std::max(radix_scratch_bytes(M), scan_scratch_bytes(M + 1)));
+            const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, M, 0, std::max(8, pbits + bits_for(k2 - 1)), radix, st);
+            const uint64_t *ps = sw ? pos2 : pos;
+            const uint32_t *is = sw ? idx2 : idx;
+            const uint64_t pmask = (1ull << pbits) - 1ull;
+            for (size_t q = 0; q < g.size(); ++q)
+                launch_dirty_leaves(ps + B.base[q], is + B.base[q], B.m[q], bdig, T.t[q].nodes, T.t[q].bm, T.t[q].l0,
+                                    T.t[q].cnt, T.t[q].missing, st, pmask);
+        }
         // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest
         // of the climb in one fused launch (the dirty count never exceeds min(m, level size))
         size_t ltop = 0;
