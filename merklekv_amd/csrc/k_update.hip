@@ -38,10 +38,21 @@ __device__ __forceinline__ const uint8_t *tree_key(const DiffSide &T, uint64_t i
     return T.kb + a;
 }
 
-// Sorted position of key k in tree T, UINT64_MAX when it is not a leaf.
-__device__ __forceinline__ uint64_t locate_one(const uint8_t *k, uint64_t len, const DiffSide &T) {
+// Sorted position of key k in tree T, UINT64_MAX when it is not a leaf. ps[j] = T.pfx[LOC_STRIDE * j]
+// (ns samples, a 1/64 copy that stays in the MALL / L2): the lower bound is first narrowed on the samples
+// to a window of LOC_STRIDE prefixes (one or two HBM lines) instead of ~log2(n / LOC_STRIDE) random
+// HBM reads into the full prefix array.
+__device__ __forceinline__ uint64_t locate_one(const uint8_t *k, uint64_t len, const DiffSide &T,
+                                               const uint64_t *__restrict__ ps, uint64_t ns) {
     const uint64_t c0 = key_chunk(k, len, 0);
-    uint64_t lo = 0, hi = T.n;  // first position with pfx >= c0
+    uint64_t j0 = 0, j1 = ns;  // first sample >= c0
+    while (j0 < j1) {
+        const uint64_t mid = (j0 + j1) >> 1;
+        if (ps[mid] < c0) j0 = mid + 1;
+        else j1 = mid;
+    }
+    uint64_t lo = j0 ? (j0 - 1) * LOC_STRIDE + 1 : 0;
+    uint64_t hi = j0 * LOC_STRIDE < T.n ? j0 * LOC_STRIDE : T.n;  // first position with pfx >= c0
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
         if (T.pfx[mid] < c0) lo = mid + 1;
@@ -80,13 +91,14 @@ __device__ __forceinline__ uint64_t locate_one(const uint8_t *k, uint64_t len, c
 }
 
 __global__ __launch_bounds__(256) void k_locate(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
-                                                uint64_t m, DiffSide T, uint64_t *__restrict__ pos,
-                                                uint32_t *__restrict__ idx, uint32_t *__restrict__ missing) {
+                                                uint64_t m, DiffSide T, const uint64_t *__restrict__ ps, uint64_t ns,
+                                                uint64_t *__restrict__ pos, uint32_t *__restrict__ idx,
+                                                uint32_t *__restrict__ missing) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool miss = false;
     if (i < m) {
         const uint64_t a = koff[i];
-        const uint64_t found = locate_one(kb + a, koff[i + 1] - a, T);
+        const uint64_t found = locate_one(kb + a, koff[i + 1] - a, T, ps, ns);
         miss = found == UINT64_MAX;
         pos[i] = found;
         idx[i] = (uint32_t)i;
@@ -103,7 +115,7 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
     bool miss = false;
     if (i < m) {
         const uint64_t a = B.koff[t][i];
-        const uint64_t found = locate_one(B.kb[t] + a, B.koff[t][i + 1] - a, L.T[t]);
+        const uint64_t found = locate_one(B.kb[t] + a, B.koff[t][i + 1] - a, L.T[t], L.ps[t], L.ns[t]);
         miss = found == UINT64_MAX;
         const uint64_t g = B.base[t] + i;
         pos[g] = ((uint64_t)t << pbits) | (miss ? (1ull << pbits) - 1ull : found);
@@ -396,10 +408,21 @@ inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_d
 
 }  // namespace
 
-void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, uint64_t *pos,
-                   uint32_t *idx, uint32_t *missing, hipStream_t st) {
+void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, const uint64_t *ps,
+                   uint64_t ns, uint64_t *pos, uint32_t *idx, uint32_t *missing, hipStream_t st) {
     if (!m) return;
-    hipLaunchKernelGGL(k_locate, grid1d(m), dim3(256), 0, st, kb, koff, m, T, pos, idx, missing);
+    hipLaunchKernelGGL(k_locate, grid1d(m), dim3(256), 0, st, kb, koff, m, T, ps, ns, pos, idx, missing);
+    MKV_LAUNCH_CHECK();
+}
+
+__global__ void k_strided_u64(const uint64_t *__restrict__ src, uint64_t ns, uint64_t *__restrict__ dst) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < ns) dst[j] = src[j * LOC_STRIDE];
+}
+void launch_locate_samples(const uint64_t *pfx, uint64_t n, uint64_t *ps, hipStream_t st) {
+    const uint64_t ns = locate_samples(n);
+    if (!ns) return;
+    hipLaunchKernelGGL(k_strided_u64, grid1d(ns), dim3(256), 0, st, pfx, ns, ps);
     MKV_LAUNCH_CHECK();
 }
 

@@ -204,13 +204,21 @@ void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t ple
 // ---- incremental dirty-path update (k_update.hip) ----
 // pos[i] = sorted leaf position of batch key i (UINT64_MAX if it is not a leaf), idx[i] = i;
 // *missing += keys that are not leaves.
-void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, uint64_t *pos,
-                   uint32_t *idx, uint32_t *missing, hipStream_t st);
+// ps / ns: the locate samples of T's prefixes (launch_locate_samples).
+void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, const uint64_t *ps,
+                   uint64_t ns, uint64_t *pos, uint32_t *idx, uint32_t *missing, hipStream_t st);
+// Every LOC_STRIDE-th sorted prefix (ps[j] = pfx[LOC_STRIDE x j], locate_samples(n) entries): the upper
+// part of the locate binary search runs on this 1/64 copy.
+constexpr uint64_t LOC_STRIDE = 64;
+inline uint64_t locate_samples(uint64_t n) { return (n + LOC_STRIDE - 1) / LOC_STRIDE; }
+void launch_locate_samples(const uint64_t *pfx, uint64_t n, uint64_t *ps, hipStream_t st);
 // k trees at once (grid.y = tree): batch b of tree b (keys B.kb/B.koff, B.m records) located in T[b];
 // pos[base_b + i] = (b << pbits) | position (position (1 << pbits) - 1 when the key is not a leaf: then
 // *missing[b] += 1), idx[base_b + i] = base_b + i.
 struct LocateMulti {
     DiffSide T[LEAF_MULTI_MAX];
+    const uint64_t *ps[LEAF_MULTI_MAX];  // locate samples of T[b] (launch_locate_samples)
+    uint64_t ns[LEAF_MULTI_MAX];
     uint32_t *missing[LEAF_MULTI_MAX];
 };
 void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,

@@ -197,6 +197,8 @@ struct mkv_tree {
     // avoids a random-access gather of every key on each build.
     uint64_t nstore = 0, kbytes = 0;
     DevBuf kb, koff, perm, pfx, nodes;
+    DevBuf pfx_s;                          // locate samples of pfx (every LOC_STRIDE-th), built on demand
+    uint64_t pfx_gen = 1, pfx_s_gen = 0;   // pfx_s is current while pfx_s_gen == pfx_gen
     std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
     bool has_root = false;
     uint8_t root[32] = {0};
@@ -874,6 +876,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     t->n = n;
     // adopt the sorted prefixes and the permutation
     swap_buf(t->pfx, *pkbuf);
+    ++t->pfx_gen;
     swap_buf(t->perm, *pmbuf);
     perm = t->perm.as<uint32_t>();
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
@@ -1189,6 +1192,7 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         uint64_t *ko = ens<uint64_t>(dst->koff, src->nstore + 1);
         uint32_t *pm = ens<uint32_t>(dst->perm, src->n + 1);
         uint64_t *pf = ens<uint64_t>(dst->pfx, src->n + 1);
+        ++dst->pfx_gen;
         uint8_t *nd = ens<uint8_t>(dst->nodes, 32 * (2 * src->n + 66));
         if (src->kbytes) MKV_HIP(hipMemcpyAsync(kb, src->kb.p, src->kbytes, hipMemcpyDeviceToDevice, dst->st));
         if (src->koff.p)
@@ -1377,6 +1381,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     swap_buf(t->kb, t->s_kb);
     swap_buf(t->koff, t->s_koff);
     swap_buf(t->pfx, t->m_pfx);
+    ++t->pfx_gen;
     swap_buf(t->perm, t->m_perm);
     swap_buf(t->nodes, t->m_nodes);
     t->kbytes = kbytes + kbn;
@@ -1431,6 +1436,18 @@ struct DirtyBatch {
     uint64_t m;
 };
 
+// The tree's locate samples (every LOC_STRIDE-th sorted prefix), rebuilt on stream st when the prefixes
+// changed since the last call (builds, merges, clones); value-only updates keep them.
+static const uint64_t *locate_samples_of(mkv_tree *t, hipStream_t st, uint64_t *ns) {
+    *ns = locate_samples(t->n);
+    uint64_t *ps = ens<uint64_t>(t->pfx_s, *ns + 1);
+    if (t->pfx_s_gen != t->pfx_gen) {
+        launch_locate_samples(t->pfx.as<uint64_t>(), t->n, ps, st);
+        t->pfx_s_gen = t->pfx_gen;
+    }
+    return ps;
+}
+
 // Phase 1 on the tree's own stream: locate the batch keys, hash the batch, sort by position, scatter the
 // last write per position into level 0 (level-0 dirty list in u_l0, counts in u_cnt).
 static DirtyTree dirty_prepare(mkv_tree *t, const DirtyBatch &b) {
@@ -1452,7 +1469,9 @@ static DirtyTree dirty_prepare(mkv_tree *t, const DirtyBatch &b) {
     // device and does nothing when it is non-zero, so the whole climb is enqueued without a host round
     // trip and the host reads the count once at the end (then the caller takes the merge path).
     const uint32_t *missing = cnt + L + 1;
-    launch_locate(b.kb, b.koff, m, side_of(t), pos, idx, cnt + L + 1, st);
+    uint64_t ns = 0;
+    const uint64_t *ps = locate_samples_of(t, st, &ns);
+    launch_locate(b.kb, b.koff, m, side_of(t), ps, ns, pos, idx, cnt + L + 1, st);
     uint8_t *bdig = ens<uint8_t>(t->u_dig, m * 32);
     launch_leaf_hash(b.kb, b.koff, b.vb, b.voff, m, bdig, st);
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
@@ -1543,6 +1562,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
                 uint32_t *l0 = ens<uint32_t>(t->u_l0, b.m + 1), *l1 = ens<uint32_t>(t->u_l1, b.m + 1);
                 T.t[q] = DirtyTree{t->nodes.as<uint8_t>(), bm, l0, l1, cnt, cnt + L + 1};
                 LM.T[q] = side_of(t);
+                LM.ps[q] = locate_samples_of(t, st, &LM.ns[q]);
                 LM.missing[q] = cnt + L + 1;
                 t->bm_dirty = true;
             }
