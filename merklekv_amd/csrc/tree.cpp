@@ -1570,8 +1570,13 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             uint64_t *pos = ens<uint64_t>(t0->u_pos, M + 1), *pos2 = ens<uint64_t>(t0->u_pos2, M + 1);
             uint32_t *idx = ens<uint32_t>(t0->u_idx, M + 1), *idx2 = ens<uint32_t>(t0->u_idx2, M + 1);
             uint8_t *bdig = ens<uint8_t>(t0->u_dig, M * 32);
+            // the batch hash (VALU) runs beside the locate (random prefix / key reads) on the aux stream
+            MKV_HIP(hipEventRecord(t0->ev_in, st));
+            MKV_HIP(hipStreamWaitEvent(t0->st2, t0->ev_in, 0));
+            launch_leaf_hash_multi(B, k2, mmax, bdig, t0->st2);
+            MKV_HIP(hipEventRecord(t0->ev_join, t0->st2));
             launch_locate_multi(B, LM, k2, mmax, pbits, pos, idx, st);
-            launch_leaf_hash_multi(B, k2, mmax, bdig, st);
+            MKV_HIP(hipStreamWaitEvent(st, t0->ev_join, 0));
             void *radix = t0->s_radix.ensure(std::max(radix_scratch_bytes(M), scan_scratch_bytes(M + 1)));
             const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, M, 0, std::max(8, pbits + bits_for(k2 - 1)), radix, st);
             const uint64_t *ps = sw ? pos2 : pos;
@@ -1584,7 +1589,16 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest
         // of the climb in one fused launch (the dirty count never exceeds min(m, level size))
         size_t ltop = 0;
-        while (ltop < L && std::min<uint64_t>(mmax, t0->lev_cnt[ltop]) > DIRTY_TOP_CAP) ++ltop;
+        // The fused top runs in one workgroup per tree: a level of more than ~1K dirty nodes takes it
+        // several serial hash rounds on one CU (4,096 nodes: ~70 us), while a per-level launch spreads
+        // them over the chip; so the per-level launches continue down to MKV_DIRTY_TOP (default 1,024)
+        // entries (configs[4]: fused top 227 -> ~110 us per step).
+        static const uint64_t top_switch = [] {
+            const char *e = getenv("MKV_DIRTY_TOP");
+            const long v = e ? atol(e) : 1024;
+            return (uint64_t)std::min<long>(std::max<long>(v, 1), (long)DIRTY_TOP_CAP);
+        }();
+        while (ltop < L && std::min<uint64_t>(mmax, t0->lev_cnt[ltop]) > top_switch) ++ltop;
         if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
         for (size_t l = 0; l < ltop; ++l) {
             DirtyLevel D{};
