@@ -543,7 +543,7 @@ def wl_build(ctx, args):
         if route is not None:
             out["route"] = route
         out["cpu_baseline"] = cpu
-        print(json.dumps(out), flush=True)
+        emit(out)
 
 
 # ============================================================================================= diff
@@ -654,7 +654,7 @@ def wl_diff(ctx, args):
         out["roofline"] = diff_roofline(res)
         out["diff"] = res
         out["cpu_baseline"] = cpu
-        print(json.dumps(out), flush=True)
+        emit(out)
 
 
 # ====================================================================================== incremental
@@ -723,7 +723,7 @@ def wl_incremental(ctx, args):
                               "diff_sizes_match_unique_updates": ok,
                               "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
         out["cpu_baseline"] = None if (args.no_cpu_baseline or ctx.world > 1) else cpu_baseline_update()
-        print(json.dumps(out), flush=True)
+        emit(out)
 
 
 # ===================================================================================== CPU baselines
@@ -858,7 +858,20 @@ def _cpu_model():
     return None
 
 
+_RESULT_OUT = None
+
+
+def emit(out):
+    """The one JSON result line, on the process's original stdout (see main)."""
+    f = _RESULT_OUT or sys.stdout
+    f.write(json.dumps(out) + "\n")
+    f.flush()
+
+
 def main():
+    global _RESULT_OUT
+    # The result line is the only thing on stdout: fd 1 is pointed at stderr for the rest of the process,
+    # so banners the communication libraries print (RCCL's version block, gloo's peer counts) land there.
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -878,6 +891,9 @@ def main():
                     help="build workload with a process group: also time the all-to-all redistribution of "
                          "this many unpartitioned records per rank (SURVEY 8f-3; 0 = skip)")
     args = ap.parse_args()
+    sys.stdout.flush()
+    _RESULT_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     if args.n is None:
         multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
         args.n = {"build": 125_000_000 if multi else 10_000_000, "diff": 100_000_000,
