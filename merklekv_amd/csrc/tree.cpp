@@ -2927,8 +2927,9 @@ mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint
             upload_blob(t, keys, t->s_kb, t->s_koff);
             upload_blob(t, values, t->s_vb, t->s_voff);
             uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
+            // the build's leaf-hash path (k_leaf_direct + k_leaf_list for other shapes)
             launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), t->s_vb.as<uint8_t>(),
-                             t->s_voff.as<uint64_t>(), n, dig, t->st);
+                             t->s_voff.as<uint64_t>(), n, dig, t->st, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)));
             if (n) MKV_HIP(hipMemcpyAsync(out, dig, 32 * n, hipMemcpyDeviceToHost, t->st));
             MKV_HIP(hipStreamSynchronize(t->st));
         } catch (...) {

@@ -58,6 +58,24 @@ def test_leaf_digest_uniform_fast_path():
             assert g == hashlib.sha256(len(k).to_bytes(4, "big") + k + len(v).to_bytes(4, "big") + v).digest()
 
 
+def test_leaf_digest_mixed_fixed_and_listed_chunks():
+    """k_leaf_direct hashes 64-record chunks of 32-B keys / 100-B values from registers and lists every
+    other chunk for k_leaf_list: chunks with one odd record, odd records at chunk edges, a partial last
+    chunk, all against hashlib."""
+    rng = random.Random(17)
+    n = 64 * 90 + 23
+    odd = {0, 63, 64, 700, 701, 1279, 2048, 4000, n - 1}
+    keys, vals = [], []
+    for i in range(n):
+        kl = 33 if i in odd and i % 2 == 0 else 32
+        vl = 101 if i in odd and i % 2 == 1 else 100
+        keys.append(bytes(rng.randrange(256) for _ in range(kl)))
+        vals.append(bytes(rng.randrange(256) for _ in range(vl)))
+    got = leaf_digests(keys, vals)
+    for k, v, g in zip(keys, vals, got):
+        assert g == hashlib.sha256(len(k).to_bytes(4, "big") + k + len(v).to_bytes(4, "big") + v).digest()
+
+
 def test_leaf_digest_oversized_wave_global_path():
     """A wave whose span does not fit its LDS region hashes straight from HBM."""
     keys = [b"k%d" % i for i in range(70)]
