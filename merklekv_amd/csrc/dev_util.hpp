@@ -21,6 +21,10 @@ __device__ __forceinline__ uint32_t be_word_guarded(const uint8_t *p, const uint
 // 0x00 is the smallest byte.
 __device__ __forceinline__ uint64_t key_chunk(const uint8_t *k, uint64_t len, uint64_t off) {
     if (off >= len) return 0;
+    if (off + 8 <= len && (reinterpret_cast<uintptr_t>(k + off) & 3) == 0) {  // whole, 4-B aligned: 2 loads
+        const uint32_t *q = reinterpret_cast<const uint32_t *>(k + off);
+        return ((uint64_t)__builtin_bswap32(q[0]) << 32) | __builtin_bswap32(q[1]);
+    }
     const uint8_t *end = k + len;
     uint64_t v = ((uint64_t)be_word_guarded(k + off, end) << 32) | be_word_guarded(k + off + 4, end);
     uint64_t rem = len - off;

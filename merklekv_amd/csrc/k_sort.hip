@@ -78,6 +78,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
     const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS;
     const uint64_t a0 = koff[0], l0 = koff[1] - a0;
     const uint64_t k0w = key_chunk(kb + a0, l0, 0);
+    // key 0's chunks 1..3, once per thread: the common-prefix test below loads a key's chunks 1..3 in
+    // one go (independent loads, one memory latency) instead of one dependent chunk per iteration
+    const uint64_t k01 = lcp ? key_chunk(kb + a0, l0, 8) : 0, k02 = lcp ? key_chunk(kb + a0, l0, 16) : 0;
+    const uint64_t k03 = lcp ? key_chunk(kb + a0, l0, 24) : 0;
     uint64_t mx = 0, mn = PH_LCP_CAP;
     for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
         const uint64_t a = koff[i], b = koff[i + 1], len = b - a;
@@ -86,10 +90,24 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
         pfx[i] = k;
 #pragma unroll
         for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
-        if (lcp && mn) {  // off == 0 here: k is key i's first chunk
+        if (lcp && mn) {  // common prefix with key 0, from the key's first chunk
             uint64_t lim = len > l0 ? len : l0;
             lim = lim < PH_LCP_CAP ? lim : PH_LCP_CAP;
-            uint64_t L = 0, x = k ^ k0w;
+            uint64_t L = 0, x = (off == 0 ? k : key_chunk(kb + a, len, 0)) ^ k0w;
+            if (x == 0 && 8 < lim) {
+                const uint64_t x1 = key_chunk(kb + a, len, 8) ^ k01, x2 = key_chunk(kb + a, len, 16) ^ k02;
+                const uint64_t x3 = key_chunk(kb + a, len, 24) ^ k03;
+                L = 8;
+                x = x1;
+                if (x == 0 && L + 8 < lim) {
+                    L = 16;
+                    x = x2;
+                    if (x == 0 && L + 8 < lim) {
+                        L = 24;
+                        x = x3;
+                    }
+                }
+            }
             while (x == 0 && L + 8 < lim) {
                 L += 8;
                 x = key_chunk(kb + a, len, L) ^ key_chunk(kb + a0, l0, L);
@@ -836,13 +854,13 @@ void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const
 }
 
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st, uint64_t off) {
+                        hipStream_t st, uint64_t off, bool lcp) {
     init_sort_prio();
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) return;
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
-    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, off == 0, pfx,
+    hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, lcp, pfx,
                        counts);
     MKV_LAUNCH_CHECK();
 }

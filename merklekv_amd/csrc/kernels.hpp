@@ -62,8 +62,10 @@ constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
 constexpr uint32_t PH_NLCP_WORD = 8 * 256 + 62;
 constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;
 void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
+// lcp: also measure the shared prefix with key 0 (PH_NLCP_WORD) and key 0's first bytes (PH_K0_WORD),
+// for any window offset.
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st, uint64_t off = 0);
+                        hipStream_t st, uint64_t off = 0, bool lcp = true);
 // v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;
 // with no pass at all v is filled with them). The result is in (k, v) or, when true is returned, (k2, v2).
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,

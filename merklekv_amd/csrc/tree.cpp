@@ -197,6 +197,7 @@ struct mkv_tree {
     // avoids a random-access gather of every key on each build.
     uint64_t nstore = 0, kbytes = 0;
     DevBuf kb, koff, perm, pfx, nodes;
+    uint64_t sort_win_hint = 0;            // shared key prefix length found by the last sort (sort_unique)
     DevBuf pfx_s;                          // locate samples of pfx (every LOC_STRIDE-th), built on demand
     uint64_t pfx_gen = 1, pfx_s_gen = 0;   // pfx_s is current while pfx_s_gen == pfx_gen
     std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
@@ -777,28 +778,35 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n_in), scan_scratch_bytes(n_in + 1)));
 
     size_t ps = prof_begin(t, "sort", st);
-    // one read of the keys: 8-byte prefixes + all eight digit histograms (the indices come from pass 1)
-    launch_prefix_hist(kb, koff, n_in, k1, radix, st);
+    // one read of the keys: 8-byte windows + all eight digit histograms (the indices come from pass 1),
+    // plus the prefix every key shares. The window starts at the shared length the previous sort of this
+    // handle found (sort_win_hint; repeated builds of one key space share it), so the second histogram
+    // pass below only runs when the hint is off.
+    const uint64_t hint = n_in > 1 ? t->sort_win_hint : 0;
+    launch_prefix_hist(kb, koff, n_in, k1, radix, st, hint, true);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
-    uint64_t win = 0;       // byte offset of the sort window
+    uint64_t win = hint;    // byte offset of the sort window
     uint64_t shared8 = 0;   // the first min(win, 8) bytes every key shares, big-endian at the top
     if (n_in > 1) {
         MKV_HIP(hipMemcpyAsync(t->h_counts, radix, (8 * 256 + 64) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         wait_stream(t, st);
         // Bytes every key shares carry no order: move the window past them ("tenant/0001/object/..."
         // keys would otherwise tie on the whole prefix and leave all n keys to the chunk-by-chunk
-        // refinement). One more histogram pass, at the shared prefix length the first pass measured.
+        // refinement). One more histogram pass when the shared length the first pass measured is not
+        // the window it used.
         const uint64_t maxlen = t->h_counts[PH_MAXLEN_WORD];
         const uint64_t lcp = (uint32_t)~t->h_counts[PH_NLCP_WORD];
         const uint64_t k0w = ((uint64_t)t->h_counts[PH_K0_WORD] << 32) | t->h_counts[PH_K0_WORD + 1];
-        if (lcp > 0 && lcp < maxlen) {
-            win = lcp;
-            shared8 = win >= 8 ? k0w : k0w & (~0ull << (64 - 8 * win));
-            launch_prefix_hist(kb, koff, n_in, k1, radix, st, win);
+        const uint64_t want = lcp > 0 && lcp < maxlen ? lcp : 0;
+        if (want != hint) {
+            win = want;
+            launch_prefix_hist(kb, koff, n_in, k1, radix, st, win, false);
             MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
             wait_stream(t, st);
         }
+        shared8 = win == 0 ? 0 : win >= 8 ? k0w : k0w & (~0ull << (64 - 8 * win));
+        t->sort_win_hint = win;
         digits = choose_prefix_digits(t->h_counts, n_in, &lo_bit);
     }
     const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, radix, st, true);
