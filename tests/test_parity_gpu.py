@@ -570,3 +570,21 @@ def test_key_entropy_shapes_vs_oracle(oracle_lib, shape, n):
     assert t2.get_root_hash() == o2.root()
     assert t.diff_keys_bytes(t2) == o.diff(o2)
 
+
+
+def test_sort_window_hint_across_builds(oracle_lib):
+    """One handle rebuilt over key sets with different shared prefixes: the first histogram pass starts
+    at the previous build's shared length (tree.cpp sort_unique) and must fall back to a second pass
+    whenever that hint is wrong (longer, shorter, none, single key)."""
+    rng = random.Random(23)
+    t = MerkleTree()
+    shapes = ["tenant19", "tenant19", "user5", "mixed", "tenant19", "one", "long41", "tenant19", "b64"]
+    for shape in shapes:
+        if shape == "one":
+            pairs = [(b"tenant/0001/object/zz", b"v")]
+        elif shape == "b64":
+            pairs = _entropy_pairs(rng, "b64", 20_000)
+        else:
+            pairs = _shared_prefix_pairs(rng, shape, 20_000)
+        t.build([k for k, _ in pairs], [v for _, v in pairs])
+        assert_tree_equal(t, oracle_lib.OracleTree.from_pairs(pairs), check_levels=False)
