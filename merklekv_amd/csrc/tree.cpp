@@ -1228,27 +1228,37 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
     });
 }
 
+// The leaf hash of a build. Borrowed device inputs (!staged): it also copies the keys (and offsets) into
+// the tree's own buffers when the capacity of an earlier build suffices (*kcap / *ko_fused say what was
+// fused; otherwise sort_dedup_gather copies them).
+static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
+                                  const uint64_t *voff, uint64_t n, uint8_t *dig, bool staged, uint64_t *kcap,
+                                  bool *ko_fused) {
+    *kcap = 0;
+    *ko_fused = false;
+    uint32_t *ctr = ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n));
+    if (!staged) {
+        *kcap = t->kb.p ? t->kb.cap : 0;
+        *ko_fused = t->koff.p && t->koff.cap >= (n + 1) * 8;
+        if (!launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ctr, t->kb.as<uint8_t>(), *kcap,
+                              *ko_fused ? t->koff.as<uint64_t>() : nullptr)) {
+            *kcap = 0;
+            *ko_fused = false;  // offsets are copied only together with the persistent kernels
+        }
+    } else {
+        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ctr);
+    }
+}
+
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
                               const uint64_t *voff, uint64_t n, bool staged, uint64_t staged_kbytes) {
     size_t ptot = prof_begin(t, "total_build");
     uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
     fork_streams(t);
     size_t pl = prof_begin(t, "leaf_hash");
-    // borrowed device inputs: the leaf hash also copies the keys into the tree's own buffers (when the
-    // capacity of an earlier build suffices; otherwise sort_dedup_gather copies)
     uint64_t kcap = 0;
     bool ko_fused = false;
-    if (!staged) {
-        kcap = t->kb.p ? t->kb.cap : 0;
-        ko_fused = t->koff.p && t->koff.cap >= (n + 1) * 8;
-        if (!launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)), t->kb.as<uint8_t>(), kcap,
-                              ko_fused ? t->koff.as<uint64_t>() : nullptr)) {
-            kcap = 0;
-            ko_fused = false;  // offsets are copied only together with the persistent kernel
-        }
-    } else {
-        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)));
-    }
+    leaf_hash_owning_keys(t, kb, koff, vb, voff, n, dig, staged, &kcap, &ko_fused);
     prof_end(t, pl);
     sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes, true, kcap, ko_fused);
     finish_unsharded(t);
@@ -2535,9 +2545,13 @@ mkv_status mkv_shard_prepare(mkv_tree *t, mkv_blob keys, mkv_blob values, int on
         uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
         fork_streams(t);
         size_t pl = prof_begin(t, "leaf_hash");
-        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)));
+        // device inputs: the key-ownership copy rides on the leaf hash as in the unsharded build (at 125M
+        // keys per rank a separate copy is 4 GB of keys + 1 GB of offsets on the critical stream)
+        uint64_t kcap = 0;
+        bool ko_fused = false;
+        leaf_hash_owning_keys(t, kb, koff, vb, voff, n, dig, !on_device, &kcap, &ko_fused);
         prof_end(t, pl);
-        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes, true);  // gather fused into reduce
+        sort_dedup_gather(t, kb, koff, n, nullptr, !on_device, staged_kbytes, true, kcap, ko_fused);  // gather fused into reduce
         prof_end(t, ptot);
         sync(t);
         t->prepared = true;
