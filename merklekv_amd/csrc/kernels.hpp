@@ -19,10 +19,12 @@ struct LeafBatches {
 void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uint8_t *out, hipStream_t st);
 // Words of the leaf hash's device counter block (ctr): chunk hand-out counter + listed-chunk count + list.
 size_t leaf_ctr_words(uint64_t n);
-// ctr: optional device u32 for the dynamic chunk hand-out (MKV_LEAF_DYN grain > 0); zeroed by the launch.
+// ctr: optional device counter block (leaf_ctr_words(n) words) for the persistent kernels' chunk
+// hand-out and the list of chunks k_leaf_direct leaves to k_leaf_list; zeroed by the launch. Without it
+// the launch takes the static round-robin k_leaf_persist.
 // kcopy/kcap/ocopy: optional fused key-ownership copy (keys at the same byte offsets into kcopy, at most
-// kcap bytes; offsets[0..n] into ocopy). Returns true when the key copy was fused (persistent kernel and
-// kb 16-B aligned; offsets are copied whenever ocopy is given to the persistent kernel).
+// kcap bytes; offsets[0..n] into ocopy). Returns true when the key copy was fused (persistent kernels and
+// kb 16-B aligned; offsets are copied whenever ocopy is given to a persistent kernel).
 bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                       uint8_t *out_digests, hipStream_t st, uint32_t *ctr = nullptr, uint8_t *kcopy = nullptr,
                       uint64_t kcap = 0, uint64_t *ocopy = nullptr);
