@@ -162,6 +162,9 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
 // One dirty entry x (local index at level l): clears its children's bits, and, when its parent is owned
 // and its left sibling is not dirty (the left one owns the pair), rehashes the parent (or promotes past
 // an odd level end, R5), marks it dirty and returns true with the parent's local index in *qloc.
+// SHORT: the short-chain round form (latency-bound fused top); the per-level launches are throughput-bound
+// and take the plain form (fewer instructions).
+template <bool SHORT>
 __device__ __forceinline__ bool dirty_step(const DirtyLevel &L, uint64_t x, uint8_t *nodes, uint32_t *bm,
                                            uint32_t *qloc) {
     const uint64_t xg = L.a + x;
@@ -185,7 +188,7 @@ __device__ __forceinline__ bool dirty_step(const DirtyLevel &L, uint64_t x, uint
     if (lg + 1 < L.S) {
         uint32_t rw[8];
         load_digest(lp + 32, rw);
-        sha_node<true>(lw, rw, ow);
+        sha_node<SHORT>(lw, rw, ow);
     } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) ow[q] = lw[q];  // R5 promotion
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, int l, DirtyT
     if ((uint64_t)blockIdx.x * blockDim.x >= cnt) return;  // whole workgroup idle (wave-uniform exit)
     bool act = false;
     uint32_t qloc = 0;
-    if (i < cnt) act = dirty_step(L, lin[i], D.nodes, D.bm, &qloc);
+    if (i < cnt) act = dirty_step<false>(L, lin[i], D.nodes, D.bm, &qloc);
     block_append<uint32_t>(act, qloc, lout, D.cnt + l + 1, sapp);
 }
 
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(DIRTY_TOP_THREADS) void k_dirty_top(LevelPlan P, in
         const DirtyLevel D = level_of(P, l);
         for (uint32_t e = threadIdx.x; e < n; e += DIRTY_TOP_THREADS) {
             uint32_t q;
-            if (dirty_step(D, list[cur][e], nodes, bm, &q)) list[cur ^ 1][atomicAdd(&ncnt[cur ^ 1], 1u)] = q;
+            if (dirty_step<true>(D, list[cur][e], nodes, bm, &q)) list[cur ^ 1][atomicAdd(&ncnt[cur ^ 1], 1u)] = q;
         }
         __threadfence();  // parents' digests and bits visible to every wave of the next level
         __syncthreads();
