@@ -226,7 +226,7 @@ __device__ __forceinline__ DirtyLevel level_of(const LevelPlan &P, int l) {
         D.c_par = P.cnt[l + 1];
         D.off_par = P.off[l + 1];
     }
-    D.has_child = l > 0;
+    D.has_child = l > 0 && !P.keep_bits;
     if (l > 0) {
         D.a_child = P.base[l - 1];
         D.c_child = P.cnt[l - 1];

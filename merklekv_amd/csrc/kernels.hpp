@@ -261,6 +261,7 @@ constexpr int MKV_MAXLEV = 48;
 struct LevelPlan {
     uint64_t base[MKV_MAXLEV], cnt[MKV_MAXLEV], off[MKV_MAXLEV], S[MKV_MAXLEV];
     int L;
+    int keep_bits;  // 1: entries leave their children's dirty bits set (the caller clears the bitmap)
 };
 constexpr int DIRTY_TOP_THREADS = 1024;
 constexpr uint64_t DIRTY_TOP_CAP = 4096;  // dirty entries per level the fused climb holds in LDS
