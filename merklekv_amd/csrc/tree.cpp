@@ -297,6 +297,18 @@ void copy_to_host(const void *src, uint8_t *dst_dev_view, uint64_t bytes, hipStr
     MKV_LAUNCH_CHECK();
 }
 
+// Several small device -> mapped-pinned copies in one launch (one workgroup per copy, <= 32 copies of
+// <= 4 KiB): the per-tree scalar readbacks of a multi-tree call.
+struct SmallCopies {
+    const uint8_t *src[32];
+    uint8_t *dst[32];
+    uint32_t bytes[32];
+};
+__global__ __launch_bounds__(64) void k_copy_small_many(SmallCopies C) {
+    const uint32_t c = blockIdx.x;
+    for (uint32_t b = threadIdx.x; b < C.bytes[c]; b += 64) C.dst[c][b] = C.src[c][b];
+}
+
 // Scalar readback into the tree's pinned scratch (h_small), as a kernel store on stream st.
 void small_d2h(mkv_tree *t, const void *h_dst, const void *src, uint64_t bytes, hipStream_t st) {
     const uint64_t off = static_cast<const uint8_t *>(h_dst) - reinterpret_cast<const uint8_t *>(t->h_small);
@@ -1662,18 +1674,27 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             }
             launch_dirty_top(P, (int)ltop, T, k2, st);
         }
+        // every tree's missing-key count and root, read back by one launch
+        SmallCopies SC{};
+        uint32_t nc = 0;
         for (size_t q = 0; q < g.size(); ++q) {
             mkv_tree *t = ts[g[q]];
-            small_d2h(t, t->h_small, T.t[q].missing, sizeof(uint32_t), st);
+            SC.src[nc] = reinterpret_cast<const uint8_t *>(T.t[q].missing);
+            SC.dst[nc] = t->h_small_dev;
+            SC.bytes[nc++] = sizeof(uint32_t);
             if (!t->sharded) {
-                small_d2h(t, t->h_small + 16, t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1], 32, st);
+                SC.src[nc] = t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1];
+                SC.dst[nc] = t->h_small_dev + 16 * sizeof(uint64_t);
+                SC.bytes[nc++] = 32;
                 t->has_root = true;
             } else {
                 t->has_root = false;
                 t->combine_pending = true;  // seam + global root: mkv_shard_fringe + all-gather + combine
             }
-            prof_end(t, prof[q]);
         }
+        hipLaunchKernelGGL(k_copy_small_many, dim3(nc), dim3(64), 0, st, SC);
+        MKV_LAUNCH_CHECK();
+        for (size_t q = 0; q < g.size(); ++q) prof_end(ts[g[q]], prof[q]);
         MKV_HIP(hipEventRecord(t0->ev_join, st));
         for (size_t q = 1; q < g.size(); ++q) MKV_HIP(hipStreamWaitEvent(ts[g[q]]->st, t0->ev_join, 0));
         for (size_t q = 0; q < g.size(); ++q) {
