@@ -695,29 +695,27 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_level_batch(const uint8_
 // set differs there: nbad[v]); refs[k] = the base's sorted index; count[v] = first entry of variant v
 // (left untouched — the caller presets all-ones — when v has none).
 __global__ void k_topdown_leaves_batch(const uint64_t *__restrict__ ent, uint64_t m, int pb, DiffSide A,
-                                       const DiffSide *__restrict__ Bs, uint64_t *__restrict__ refs,
+                                       const DiffSide *__restrict__ Bs, uint64_t check, uint64_t *__restrict__ refs,
                                        uint32_t *__restrict__ nbad, uint32_t *__restrict__ count) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
     const uint64_t e = ent[k];  // (variant << pb) | position
     const uint32_t v = (uint32_t)(e >> pb);
     const uint64_t i = e & ((1ull << pb) - 1ull);
-    const DiffSide B = Bs[v];
     refs[k] = i;
     if (k == 0 || (uint32_t)(ent[k - 1] >> pb) != v) count[v] = (uint32_t)k;  // segment start of variant v
-    if (!key_eq_at(A, B, i)) atomicAdd(&nbad[v], 1u);
+    if (((check >> v) & 1ull) && !key_eq_at(A, Bs[v], i)) atomicAdd(&nbad[v], 1u);
 }
 
 // Divergent leaf positions (sorted): refs of keys equal on both sides; counts positions whose keys
 // differ (then the key sets differ there and the caller falls back to the merge-join).
-__global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, DiffSide A, DiffSide B,
+__global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, DiffSide A, DiffSide B, int check,
                                  uint64_t *__restrict__ refs, uint32_t *__restrict__ nbad) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= m) return;
     const uint64_t i = pos[k];
-    const bool same = key_eq_at(A, B, i);
     refs[k] = i;
-    if (!same) atomicAdd(nbad, 1u);
+    if (check && !key_eq_at(A, B, i)) atomicAdd(nbad, 1u);
 }
 
 __global__ void k_widen_u32(const uint32_t *__restrict__ c, uint64_t *__restrict__ o, uint64_t n) {
@@ -797,9 +795,9 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
 }
 
 void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs,
-                                 uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st) {
+                                 uint64_t check, uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st) {
     if (!m) return;
-    hipLaunchKernelGGL(k_topdown_leaves_batch, grid1d(m), dim3(256), 0, st, ent, m, pb, A, Bs, refs, nbad, count);
+    hipLaunchKernelGGL(k_topdown_leaves_batch, grid1d(m), dim3(256), 0, st, ent, m, pb, A, Bs, check, refs, nbad, count);
     MKV_LAUNCH_CHECK();
 }
 
@@ -869,10 +867,10 @@ void launch_compare_nodes(const uint8_t *lvl, uint64_t count, const uint64_t *id
     MKV_LAUNCH_CHECK();
 }
 
-void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
-                           uint32_t *nbad, hipStream_t st) {
+void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, bool check,
+                           uint64_t *refs, uint32_t *nbad, hipStream_t st) {
     if (!m) return;
-    hipLaunchKernelGGL(k_topdown_leaves, grid1d(m), dim3(256), 0, st, pos, m, A, B, refs, nbad);
+    hipLaunchKernelGGL(k_topdown_leaves, grid1d(m), dim3(256), 0, st, pos, m, A, B, (int)check, refs, nbad);
     MKV_LAUNCH_CHECK();
 }
 

@@ -169,7 +169,8 @@ void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_c
 // *count += sampled positions whose sorted key prefixes differ (key-set screen for the top-down walk).
 void launch_sample_pfx(const uint64_t *pa, const uint64_t *pb, uint64_t n, uint32_t samples, uint32_t *count,
                        hipStream_t st);
-void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *refs,
+// check == false: the caller knows both key sequences are equal (same key-set id): refs only.
+void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, bool check, uint64_t *refs,
                            uint32_t *nbad, hipStream_t st);
 void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
                          hipStream_t st);
@@ -192,7 +193,8 @@ void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t 
                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
                                uint64_t max_desc, hipStream_t st);
 // ent: sorted (variant << pb) | position.
-void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs,
+// check: bit v set = variant v's keys at its divergent positions are compared with the base's.
+void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs, uint64_t check,
                                  uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st);
 // key[k] = (variant << pb) | position of frontier entry (variant << 32) | position; val[k] = k.
 void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st);

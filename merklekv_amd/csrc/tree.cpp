@@ -184,6 +184,12 @@ struct mkv_keylist {
     mkv_keylist() { offsets = &zero; }
 };
 
+// Key-set identity: two trees with the same id hold the same sorted key sequence (a clone inherits its
+// source's id; every build or merge draws a fresh one; value-only updates keep it), so a diff between
+// them can skip checking that divergent leaf positions hold equal keys.
+static std::atomic<uint64_t> g_keyset_ids{0};
+static uint64_t next_keyset() { return g_keyset_ids.fetch_add(1, std::memory_order_relaxed) + 1; }
+
 struct mkv_tree {
     int dev = 0;
     hipStream_t st = nullptr;   // main stream: leaf hashing, digest gather, reduction, diff
@@ -200,6 +206,7 @@ struct mkv_tree {
     uint64_t sort_win_hint = 0;            // shared key prefix length found by the last sort (sort_unique)
     DevBuf pfx_s;                          // locate samples of pfx (every LOC_STRIDE-th), built on demand
     uint64_t pfx_gen = 1, pfx_s_gen = 0;   // pfx_s is current while pfx_s_gen == pfx_gen
+    uint64_t keyset = next_keyset();       // key-set identity (see next_keyset)
     std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
     bool has_root = false;
     uint8_t root[32] = {0};
@@ -238,7 +245,7 @@ struct mkv_tree {
     DevBuf u_tomb, m_pfx, m_perm, m_nodes, m_cnt;
     uint64_t bm_bits = 0;
     bool bm_dirty = false;
-    uint64_t *h_small = nullptr;  // pinned host scalars
+    uint64_t *h_small = nullptr;  // pinned host scalars (1 KB: bytes [512, 1024) = batched-walk counters)
     uint8_t *h_small_dev = nullptr;  // h_small as the device sees it (readbacks are kernel stores)
     uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
     uint8_t *h_seam = nullptr;     // pinned staging of seam-combine inputs
@@ -307,6 +314,34 @@ struct SmallCopies {
 __global__ __launch_bounds__(64) void k_copy_small_many(SmallCopies C) {
     const uint32_t c = blockIdx.x;
     for (uint32_t b = threadIdx.x; b < C.bytes[c]; b += 64) C.dst[c][b] = C.src[c][b];
+}
+
+// Zero-fill of up to 32 device ranges in one launch (grid.y = range): a multi-replica update clears
+// every replica's dirty bitmap and level counters with one launch instead of one memset call each
+// (each ~10 µs of host enqueue and ~5 µs of device time, serialised).
+struct ZeroRanges {
+    uint8_t *p[32];
+    uint64_t bytes[32];
+};
+__global__ __launch_bounds__(256) void k_zero_many(ZeroRanges Z) {
+    uint8_t *p = Z.p[blockIdx.y];
+    const uint64_t bytes = Z.bytes[blockIdx.y];
+    const uint64_t head = std::min<uint64_t>(bytes, (16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15);
+    const uint64_t nv = (bytes - head) >> 4;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    uint4 *v = reinterpret_cast<uint4 *>(p + head);
+    for (uint64_t i = t; i < nv; i += stride) v[i] = make_uint4(0, 0, 0, 0);
+    if (t < head) p[t] = 0;
+    const uint64_t tail = head + (nv << 4);
+    if (t < bytes - tail) p[tail + t] = 0;
+}
+static void launch_zero_many(const ZeroRanges &Z, uint32_t nz, hipStream_t st) {
+    if (!nz) return;
+    uint64_t mx = 0;
+    for (uint32_t i = 0; i < nz; ++i) mx = std::max(mx, Z.bytes[i]);
+    const uint32_t bx = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(ceil_div(mx, 16 * 256 * 4), 1), 1024);
+    hipLaunchKernelGGL(k_zero_many, dim3(bx, nz), dim3(256), 0, st, Z);
+    MKV_LAUNCH_CHECK();
 }
 
 // Scalar readback into the tree's pinned scratch (h_small), as a kernel store on stream st.
@@ -897,6 +932,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // adopt the sorted prefixes and the permutation
     swap_buf(t->pfx, *pkbuf);
     ++t->pfx_gen;
+    t->keyset = next_keyset();
     swap_buf(t->perm, *pmbuf);
     perm = t->perm.as<uint32_t>();
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
@@ -1094,7 +1130,7 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
             delete t;
             throw Error(ST_EHIP, std::string("hipStreamCreate: ") + hipGetErrorString(e2));
         }
-        e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 256, hipHostMallocDefault);
+        e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_small), 1024, hipHostMallocDefault);
         if (e2 == hipSuccess) {
             void *d = nullptr;
             e2 = hipHostGetDevicePointer(&d, t->h_small, 0);
@@ -1225,6 +1261,7 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         MKV_HIP(hipStreamSynchronize(dst->st));
         dst->n = src->n;
         dst->nstore = src->nstore;
+        dst->keyset = src->keyset;
         dst->kbytes = src->kbytes;
         dst->lev_cnt = src->lev_cnt;
         dst->lev_off = src->lev_off;
@@ -1412,6 +1449,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     swap_buf(t->koff, t->s_koff);
     swap_buf(t->pfx, t->m_pfx);
     ++t->pfx_gen;
+    t->keyset = next_keyset();
     swap_buf(t->perm, t->m_perm);
     swap_buf(t->nodes, t->m_nodes);
     t->kbytes = kbytes + kbn;
@@ -1568,6 +1606,9 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             }
             LeafBatches B{};
             LocateMulti LM{};
+            static_assert(2 * DIRTY_MAX_TREES <= 32, "ZeroRanges holds two ranges per tree");
+            ZeroRanges Z{};
+            uint32_t nz = 0;
             uint64_t M = 0;
             for (size_t q = 0; q < g.size(); ++q) {
                 mkv_tree *t = ts[g[q]];
@@ -1584,11 +1625,13 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
                 const uint64_t words = (nn + 63) / 32 + 2;
                 uint32_t *bm = ens<uint32_t>(t->u_bm, words);
                 if (t->bm_bits < nn || t->bm_dirty) {
-                    MKV_HIP(hipMemsetAsync(bm, 0, words * 4, st));
+                    Z.p[nz] = reinterpret_cast<uint8_t *>(bm);
+                    Z.bytes[nz++] = words * 4;
                     t->bm_bits = words * 32 - 64;
                 }
                 uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);
-                MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, st));
+                Z.p[nz] = reinterpret_cast<uint8_t *>(cnt);
+                Z.bytes[nz++] = (L + 2) * 4;
                 uint32_t *l0 = ens<uint32_t>(t->u_l0, b.m + 1), *l1 = ens<uint32_t>(t->u_l1, b.m + 1);
                 T.t[q] = DirtyTree{t->nodes.as<uint8_t>(), bm, l0, l1, cnt, cnt + L + 1};
                 LM.T[q] = side_of(t);
@@ -1596,6 +1639,8 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
                 LM.missing[q] = cnt + L + 1;
                 t->bm_dirty = true;
             }
+            launch_zero_many(Z, nz, st);
+            HTRACE("setup-queued");
             const int pbits = bits_for(t0->n);
             uint64_t *pos = ens<uint64_t>(t0->u_pos, M + 1), *pos2 = ens<uint64_t>(t0->u_pos2, M + 1);
             uint32_t *idx = ens<uint32_t>(t0->u_idx, M + 1), *idx2 = ens<uint32_t>(t0->u_idx2, M + 1);
@@ -1615,6 +1660,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             for (size_t q = 0; q < g.size(); ++q)
                 launch_dirty_leaves(ps + B.base[q], is + B.base[q], B.m[q], bdig, T.t[q].nodes, T.t[q].bm, T.t[q].l0,
                                     T.t[q].cnt, T.t[q].missing, st, pmask);
+            HTRACE("phase1-queued");
         }
         // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest
         // of the climb in one fused launch (the dirty count never exceeds min(m, level size))
@@ -1694,12 +1740,15 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         }
         hipLaunchKernelGGL(k_copy_small_many, dim3(nc), dim3(64), 0, st, SC);
         MKV_LAUNCH_CHECK();
+        HTRACE("climb-queued");
         for (size_t q = 0; q < g.size(); ++q) prof_end(ts[g[q]], prof[q]);
-        MKV_HIP(hipEventRecord(t0->ev_join, st));
-        for (size_t q = 1; q < g.size(); ++q) MKV_HIP(hipStreamWaitEvent(ts[g[q]]->st, t0->ev_join, 0));
         for (size_t q = 0; q < g.size(); ++q) {
             mkv_tree *t = ts[g[q]];
-            sync(t);
+            // all of the group's work ran on t0's streams: one host wait orders it before anything later
+            // queued on the other trees' streams (no event wait left on them: a pending one costs every
+            // later query of that stream ~15 µs), and their profiling pairs were recorded on st
+            if (q == 0) sync(t);
+            else prof_collect(t);
             t->bm_dirty = keep_bits;
             ok[g[q]] = reinterpret_cast<volatile uint32_t *>(t->h_small)[0] == 0;
             if (ok[g[q]] && !t->sharded) std::memcpy(t->root, t->h_small + 16, 32);
@@ -1708,6 +1757,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
                 t->combine_pending = had_pending[q];
             }
         }
+        HTRACE("synced");
     }
 }
 
@@ -1874,6 +1924,7 @@ mkv_status mkv_tree_upsert_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
 
 mkv_status mkv_tree_upsert_device_many(mkv_tree *const *trees, const mkv_blob *keys, const mkv_blob *values,
                                        uint32_t k) {
+    g_trace.reset();
     MKV_TRY({
         NEED(trees || k == 0, "null trees");
         NEED((keys && values) || k == 0, "null batches");
@@ -1888,6 +1939,7 @@ mkv_status mkv_tree_upsert_device_many(mkv_tree *const *trees, const mkv_blob *k
             for (uint32_t j = 0; j < i; ++j) NEED(trees[j] != trees[i], "a tree appears twice");
         }
         if (k == 0) return MKV_OK;
+        HTRACE("checked");
         std::vector<DirtyBatch> bs(k);
         for (uint32_t i = 0; i < k; ++i)
             bs[i] = DirtyBatch{keys[i].bytes, keys[i].offsets, values[i].bytes, values[i].offsets, keys[i].n};
@@ -2150,7 +2202,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
             pos = sw ? k2 : k1;
         }
         // mismatching keys (nbad != 0) are read back with the key list's byte count (keylist_from_refs)
-        launch_topdown_leaves(pos, m, A, B, refs, cnt + L + 1, t->st);
+        launch_topdown_leaves(pos, m, A, B, a->keyset != b->keyset, refs, cnt + L + 1, t->st);
     }
     *m_out = m;
     return true;
@@ -2293,7 +2345,11 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     }
     const uint64_t m = d2h_u32(t, cnt);
     uint32_t *nbad = cnt + L + 2, *vcount = nbad + k;
-    std::vector<uint32_t> hb(2 * k, 0);
+    // per-variant key-check failures and segment starts come back through pinned memory with the
+    // key list's own wait (a pageable readback here would hold the host until the sort finishes)
+    static_assert(2 * TD_MAX_VARIANTS * 4 <= 512, "h_small holds the batched-walk counters");
+    uint32_t *hb = reinterpret_cast<uint32_t *>(t->h_small + 64);
+    for (uint32_t i = 0; i < k; ++i) hb[i] = 0;
     uint64_t *refs = ens<uint64_t>(t->d_refs, m + 1);
     const DiffSide A = side_of(a);
     if (m) {
@@ -2309,8 +2365,11 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         DiffSide *ds = reinterpret_cast<DiffSide *>(t->tb_sides.ensure(k * sizeof(DiffSide)));
         MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
         MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
-        launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, refs, nbad, vcount, t->st);
-        MKV_HIP(hipMemcpyAsync(hb.data(), nbad, 2 * k * 4, hipMemcpyDeviceToHost, t->st));
+        uint64_t check = 0;  // variants whose key set may differ from the base's
+        for (uint32_t i = 0; i < k; ++i)
+            if (vs[i]->keyset != a->keyset) check |= 1ull << i;
+        launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
+        small_d2h(t, hb, nbad, 2 * k * 4, t->st);
     }
     mkv_keylist *all = keylist_from_refs(t, refs, m, A, A);  // syncs: hb is valid after this
     // segment starts -> per-variant counts (variants appear in ascending order)
@@ -2355,6 +2414,7 @@ mkv_status mkv_tree_diff(const mkv_tree *a, const mkv_tree *b, mkv_keylist **out
 }
 
 mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, uint32_t k, mkv_keylist **outs) {
+    g_trace.reset();
     MKV_TRY({
         NEED(a && (others || k == 0) && (outs || k == 0), "null argument");
         for (uint32_t i = 0; i < k; ++i) {
@@ -2377,6 +2437,17 @@ mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, 
             }
             const bool roots_a = !a->combine_pending && a->has_root;
             std::vector<uint32_t> walk;
+            // a variant with the base's key-set id holds the same key sequence: no sampled screen
+            std::vector<uint32_t> same_ks, other_ks;
+            for (uint32_t c : cand) (others[c]->keyset == a->keyset ? same_ks : other_ks).push_back(c);
+            for (uint32_t c : same_ks) {
+                const mkv_tree *o = others[c];
+                if (roots_a && !o->combine_pending && o->has_root && std::memcmp(a->root, o->root, 32) == 0)
+                    res[c] = new mkv_keylist();  // equal roots: identical leaves
+                else
+                    walk.push_back(c);
+            }
+            cand.swap(other_ks);
             if (!cand.empty()) {
                 uint32_t *scr = ens<uint32_t>(t->tb_screen, cand.size() + 1);
                 MKV_HIP(hipMemsetAsync(scr, 0, cand.size() * 4, t->st));
@@ -2401,6 +2472,7 @@ mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, 
                 std::vector<const mkv_tree *> vs;
                 for (size_t i = s0; i < s1; ++i) vs.push_back(others[walk[i]]);
                 std::vector<mkv_keylist *> part(vs.size(), nullptr);
+                HTRACE("screened");
                 size_t pd = prof_begin(t, "diff");
                 const bool ok = topdown_batch(t, a, vs, part);
                 prof_end(t, pd);

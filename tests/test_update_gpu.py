@@ -305,6 +305,40 @@ def test_diff_many_matches_pairwise_and_oracle():
         assert lst == obase.diff(o), i
 
 
+def test_keyset_identity_follows_clones_and_key_changes():
+    """Diffs between trees sharing a key-set id (a clone plus value-only updates) skip the leaf-key
+    check; any build or key insert/remove on either side must bring the check back."""
+    n = 6007
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED + 3, 0, n)
+    keys = split_blob(kb, ko)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    obase = coracle.OracleTree.build(kb, ko, vb, vo)
+    c = base.clone()
+    c.upsert([keys[11], keys[3000]], [b"c1", b"c2"])           # value-only: key set kept
+    oc = obase.upsert(*pack([keys[11], keys[3000]]), *pack([b"c1", b"c2"]))
+    assert base.diff_keys_bytes(c) == obase.diff(oc)
+    # the base swaps one key for another (same count, same level plan): positions shift
+    base.remove_many([keys[5]])
+    base.upsert([b"~~late-key"], [b"x"])
+    obase = obase.remove(*pack([keys[5]])).upsert(*pack([b"~~late-key"]), *pack([b"x"]))
+    assert len(base) == len(c)
+    assert base.diff_keys_bytes(c) == obase.diff(oc)
+    assert c.diff_keys_bytes(base) == oc.diff(obase)
+    got = base.diff_keys_many_packed([c, c.clone()])
+    for raw, offs in got:
+        b, oo = raw.tobytes(), offs.tolist()
+        assert [b[oo[j]:oo[j + 1]] for j in range(len(oo) - 1)] == obase.diff(oc)
+    # a clone rebuilt from different keys of the same count
+    d = c.clone()
+    keys2 = list(keys)
+    keys2[100] = b"!" + keys2[100][1:]
+    vals = split_blob(vb, vo)
+    d.build(keys2, vals)
+    od = coracle.OracleTree.from_pairs(list(zip(keys2, vals)))
+    assert c.diff_keys_bytes(d) == oc.diff(od)
+
+
 def test_antientropy_exchange_matches_diff_and_moves_little():
     """Top-down exchange (README.md:310-347): same result as diff_keys; for a sparse value-only
     divergence only a small fraction of the tree's digests cross the wire; key-set changes fall back."""

@@ -10,6 +10,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from merklekv_amd import MerkleTree  # noqa: E402
+from merklekv_amd.merkle import debug_trace  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 125_000_000
 m, R = 125_000, 8
@@ -41,11 +42,15 @@ for it in range(8):
     t0 = time.perf_counter()
     MerkleTree.upsert_device_many(variants, ptrs)
     t1 = time.perf_counter()
+    tr_u = debug_trace()
+    t1b = time.perf_counter()
     new = base.diff_keys_many_view(variants)
     t2 = time.perf_counter()
+    tr_d = debug_trace()
     diffs = new  # releases the previous step's views
     t3 = time.perf_counter()
     upd = variants[0].prof_read("update")[0]
     dif = base.prof_read("diff")[0]
-    print(f"step {it}: upsert {1e3 * (t1 - t0):.3f} ms (device {upd:.3f})  diff_many {1e3 * (t2 - t1):.3f} ms "
-          f"(device {dif:.3f})  release {1e3 * (t3 - t2):.3f} ms  total {1e3 * (t3 - t0):.3f}", flush=True)
+    print(f"step {it}: upsert {1e3 * (t1 - t0):.3f} ms (device {upd:.3f})  diff_many {1e3 * (t2 - t1b):.3f} ms "
+          f"(device {dif:.3f})  release {1e3 * (t3 - t2):.3f} ms  total {1e3 * (t3 - t0):.3f}\n"
+          f"   upsert trace: {tr_u}\n   diff trace: {tr_d}", flush=True)
