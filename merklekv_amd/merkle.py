@@ -87,12 +87,20 @@ class KeyList:
         check(lib().mkv_keylist_get(handle, C.byref(n), C.byref(bp), C.byref(op)))
         self.n = n.value
         if self.n == 0:
-            self.raw, self.offs = np.zeros(0, np.uint8), np.zeros(1, np.uint64)
+            self.raw, self._offs = np.zeros(0, np.uint8), np.zeros(1, np.uint64)
             return
         offs = np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_uint64)), shape=(self.n + 1,))
         o0, o1 = int(offs[0]), int(offs[-1])
         self.raw = np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(o1,))[o0:]
-        self.offs = offs if o0 == 0 else offs - np.uint64(o0)
+        self._offs_lib, self._o0 = offs, o0
+        self._offs = offs if o0 == 0 else None
+
+    @property
+    def offs(self) -> np.ndarray:
+        """Offsets rebased to 0 (a list sharing one block with other lists is rebased on first use)."""
+        if self._offs is None:
+            self._offs = self._offs_lib - np.uint64(self._o0)
+        return self._offs
 
     def __len__(self):
         return self.n
