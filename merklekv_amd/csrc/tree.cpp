@@ -2110,10 +2110,22 @@ static bool jumps_enabled() {
     return on;
 }
 
+static bool fine_jumps() {
+    static const bool on = [] {
+        const char *e = getenv("MKV_TD_FINE");  // A/B knob: 0 = 4-level jumps down to the leaves (batched walk)
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Levels the jumping walk lands on: the top level, then every multiple of 4 below it down to 0.
-static std::vector<size_t> jump_targets(size_t L) {
+// fine: below level 8 every multiple of 2 instead. A jump of k levels reads 2^k digests per frontier
+// node; near the leaves of a dense diff the frontier holds about one node per divergent leaf, so
+// two 2-level jumps read half the bytes of one 4-level jump (configs[4]: 7 replicas x 125K updates of
+// 125M leaves, levels 8 -> 0: ~26M -> ~13.5M digest pairs, ~380 -> ~200 us).
+static std::vector<size_t> jump_targets(size_t L, bool fine = false) {
     std::vector<size_t> T{L - 1};
-    for (int64_t x = (int64_t)((L - 2) / 4) * 4; x >= 0; x -= 4) T.push_back((size_t)x);
+    for (int64_t x = (int64_t)((L - 2) / 4) * 4; x >= 0; x -= (fine && x <= 8) ? 2 : 4) T.push_back((size_t)x);
     return T;
 }
 
@@ -2317,7 +2329,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
                                    fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
         std::swap(fin, fout);
-        const std::vector<size_t> T = jump_targets(L);
+        const std::vector<size_t> T = jump_targets(L, fine_jumps());
         for (size_t q = 1; q < T.size(); ++q) {
             const size_t l = T[q - 1], lt = T[q];
             const int kk = (int)(l - lt);
