@@ -133,14 +133,11 @@ __device__ __forceinline__ bool get_bit(const uint32_t *bm, uint64_t b) {
 
 // Level 0: sorted (position, batch index) pairs; the last entry of each equal-position run is the last
 // write of that key. nodes0: local leaf level; bm bit index of leaf p = p (level 0 starts the bitmap).
-__global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict__ pos,
-                                                      const uint32_t *__restrict__ bidx, uint64_t m,
-                                                      const uint8_t *__restrict__ bdig, uint8_t *__restrict__ nodes0,
-                                                      uint32_t *__restrict__ bm, uint32_t *__restrict__ list,
-                                                      uint32_t *__restrict__ count, const uint32_t *__restrict__ missing,
-                                                      uint64_t pmask) {
-    __shared__ uint32_t sapp[17];
-    if (*missing) return;  // some batch key is not a leaf: the caller takes the merge path, tree untouched
+__device__ __forceinline__ void dirty_leaves_block(const uint64_t *__restrict__ pos, const uint32_t *__restrict__ bidx,
+                                                   uint64_t m, const uint8_t *__restrict__ bdig,
+                                                   uint8_t *__restrict__ nodes0, uint32_t *__restrict__ bm,
+                                                   uint32_t *__restrict__ list, uint32_t *__restrict__ count,
+                                                   uint64_t pmask, uint32_t *sapp) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool act = false;
     uint32_t p = 0;
@@ -157,6 +154,30 @@ __global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict
         }
     }
     block_append<uint32_t>(act, p, list, count, sapp);
+}
+
+__global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict__ pos,
+                                                      const uint32_t *__restrict__ bidx, uint64_t m,
+                                                      const uint8_t *__restrict__ bdig, uint8_t *__restrict__ nodes0,
+                                                      uint32_t *__restrict__ bm, uint32_t *__restrict__ list,
+                                                      uint32_t *__restrict__ count, const uint32_t *__restrict__ missing,
+                                                      uint64_t pmask) {
+    __shared__ uint32_t sapp[17];
+    if (*missing) return;  // some batch key is not a leaf: the caller takes the merge path, tree untouched
+    dirty_leaves_block(pos, bidx, m, bdig, nodes0, bm, list, count, pmask, sapp);
+}
+
+// k trees' level-0 scatters in one launch (grid.y = tree): tree q's sorted entries are
+// pos[S.base[q], S.base[q] + S.m[q]).
+__global__ __launch_bounds__(256) void k_dirty_leaves_multi(const uint64_t *__restrict__ pos,
+                                                            const uint32_t *__restrict__ bidx, DirtySegs S,
+                                                            const uint8_t *__restrict__ bdig, DirtyTrees T,
+                                                            uint64_t pmask) {
+    __shared__ uint32_t sapp[17];
+    const DirtyTree &D = T.t[blockIdx.y];
+    const uint64_t m = S.m[blockIdx.y], b = S.base[blockIdx.y];
+    if (*D.missing || (uint64_t)blockIdx.x * blockDim.x >= m) return;  // workgroup-uniform exits
+    dirty_leaves_block(pos + b, bidx + b, m, bdig, D.nodes, D.bm, D.l0, D.cnt, pmask, sapp);
 }
 
 // One dirty entry x (local index at level l): clears its children's bits, and, when its parent is owned
@@ -426,6 +447,14 @@ void launch_locate_samples(const uint64_t *pfx, uint64_t n, uint64_t *ps, hipStr
     const uint64_t ns = locate_samples(n);
     if (!ns) return;
     hipLaunchKernelGGL(k_strided_u64, grid1d(ns), dim3(256), 0, st, pfx, ns, ps);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_dirty_leaves_multi(const uint64_t *pos, const uint32_t *bidx, const DirtySegs &S, uint64_t mmax,
+                               const uint8_t *bdig, const DirtyTrees &T, uint32_t k, hipStream_t st, uint64_t pmask) {
+    if (!mmax || !k) return;
+    hipLaunchKernelGGL(k_dirty_leaves_multi, dim3((uint32_t)ceil_div(mmax, 256), k), dim3(256), 0, st, pos, bidx, S,
+                       bdig, T, pmask);
     MKV_LAUNCH_CHECK();
 }
 

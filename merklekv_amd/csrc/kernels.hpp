@@ -255,6 +255,12 @@ constexpr int DIRTY_MAX_TREES = 16;
 struct DirtyTrees {
     DirtyTree t[DIRTY_MAX_TREES];
 };
+// Sorted (tree, position) entries of k trees: tree q's run starts at base[q] and holds m[q] entries.
+struct DirtySegs {
+    uint64_t base[DIRTY_MAX_TREES], m[DIRTY_MAX_TREES];
+};
+void launch_dirty_leaves_multi(const uint64_t *pos, const uint32_t *bidx, const DirtySegs &S, uint64_t mmax,
+                               const uint8_t *bdig, const DirtyTrees &T, uint32_t k, hipStream_t st, uint64_t pmask);
 // Level l of k trees sharing the level plan (grid.y = tree).
 void launch_dirty_level(const DirtyLevel &L, int l, uint64_t max_entries, const DirtyTrees &T, uint32_t k,
                         hipStream_t st);

@@ -1657,9 +1657,12 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             const uint64_t *ps = sw ? pos2 : pos;
             const uint32_t *is = sw ? idx2 : idx;
             const uint64_t pmask = (1ull << pbits) - 1ull;
-            for (size_t q = 0; q < g.size(); ++q)
-                launch_dirty_leaves(ps + B.base[q], is + B.base[q], B.m[q], bdig, T.t[q].nodes, T.t[q].bm, T.t[q].l0,
-                                    T.t[q].cnt, T.t[q].missing, st, pmask);
+            DirtySegs S{};
+            for (size_t q = 0; q < g.size(); ++q) {
+                S.base[q] = B.base[q];
+                S.m[q] = B.m[q];
+            }
+            launch_dirty_leaves_multi(ps, is, S, mmax, bdig, T, k2, st, pmask);
             HTRACE("phase1-queued");
         }
         // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest
