@@ -38,6 +38,10 @@ __device__ __forceinline__ const uint8_t *tree_key(const DiffSide &T, uint64_t i
     return T.kb + a;
 }
 
+__device__ __forceinline__ uint64_t locate_run(const uint8_t *k, uint64_t len, uint64_t c0, const DiffSide &T,
+                                               uint64_t lo);
+constexpr int LOCATE_ILP = 2;  // batch keys per lane in k_locate_multi
+
 // Sorted position of key k in tree T, UINT64_MAX when it is not a leaf. ps[j] = T.pfx[LOC_STRIDE * j]
 // (ns samples, a 1/64 copy that stays in the MALL / L2): the lower bound is first narrowed on the samples
 // to a window of LOC_STRIDE prefixes (one or two HBM lines) instead of ~log2(n / LOC_STRIDE) random
@@ -58,8 +62,81 @@ __device__ __forceinline__ uint64_t locate_one(const uint8_t *k, uint64_t len, c
         if (T.pfx[mid] < c0) lo = mid + 1;
         else hi = mid;
     }
+    return lo < T.n && T.pfx[lo] == c0 ? locate_run(k, len, c0, T, lo) : UINT64_MAX;
+}
+
+// K batch keys per thread (k_locate_multi): the same search as locate_one, with the sample and window
+// lower bounds in the branchless fixed-trip form so the K dependent load chains advance together
+// (K misses in flight per lane instead of one), and the common single-candidate tail (one leaf holds
+// the prefix) as straight-line loads; longer equal-prefix runs take locate_run.
+template <int K>
+__device__ __forceinline__ void locate_k(const uint8_t *const kp[K], const uint64_t len[K], const bool v[K],
+                                         const DiffSide &T, const uint64_t *__restrict__ ps, uint64_t ns,
+                                         uint64_t found[K]) {
+    uint64_t c0[K], lo[K], w[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        c0[j] = v[j] ? key_chunk(kp[j], len[j], 0) : 0;
+        lo[j] = 0;
+    }
+    if (ns) {  // first sample >= c0
+        uint64_t n = ns;
+        while (n > 1) {
+            const uint64_t half = n >> 1;
+#pragma unroll
+            for (int j = 0; j < K; ++j) lo[j] = ps[lo[j] + half] < c0[j] ? lo[j] + half : lo[j];
+            n -= half;
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) lo[j] += ps[lo[j]] < c0[j] ? 1 : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {  // window of at most LOC_STRIDE prefixes
+        const uint64_t j0 = lo[j];
+        const uint64_t a = j0 ? (j0 - 1) * LOC_STRIDE + 1 : 0;
+        const uint64_t b = j0 * LOC_STRIDE < T.n ? j0 * LOC_STRIDE : T.n;
+        lo[j] = a;
+        w[j] = b > a ? b - a : 0;
+    }
+    static_assert(LOC_STRIDE <= 64, "window search unrolled for <= 64 prefixes");
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if (w[j] > 1) {
+                const uint64_t half = w[j] >> 1;
+                lo[j] = T.pfx[lo[j] + half] < c0[j] ? lo[j] + half : lo[j];
+                w[j] -= half;
+            }
+    }
+    bool hit[K], run[K];
+    uint32_t o[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (w[j] == 1) lo[j] += T.pfx[lo[j]] < c0[j] ? 1 : 0;
+        hit[j] = v[j] && lo[j] < T.n && T.pfx[lo[j]] == c0[j];
+        run[j] = hit[j] && lo[j] + 1 < T.n && T.pfx[lo[j] + 1] == c0[j];
+        o[j] = hit[j] && !run[j] ? T.perm[lo[j]] : 0;
+    }
+    uint64_t ka[K], kl[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        ka[j] = hit[j] && !run[j] ? T.koff[o[j]] : 0;
+        kl[j] = hit[j] && !run[j] ? T.koff[o[j] + 1] - ka[j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        if (!hit[j]) found[j] = UINT64_MAX;
+        else if (run[j]) found[j] = locate_run(kp[j], len[j], c0[j], T, lo[j]);
+        else found[j] = key_cmp(kp[j], len[j], c0[j], T.kb + ka[j], kl[j], c0[j]) == 0 ? lo[j] : UINT64_MAX;
+    }
+}
+
+// Equal-prefix run starting at lo (T.pfx[lo] == c0): the sorted position of key k, UINT64_MAX if absent.
+__device__ __forceinline__ uint64_t locate_run(const uint8_t *k, uint64_t len, uint64_t c0, const DiffSide &T,
+                                               uint64_t lo) {
     uint64_t found = UINT64_MAX;
-    if (lo < T.n && T.pfx[lo] == c0) {
+    {
         // Equal-prefix run [lo, e): keys sharing >= 8 leading bytes ("tenant/0001/obj/...") can make
         // it the whole tree, so it is binary-searched on the full key (lower_bound with key_cmp),
         // never walked: O(log n) full-key compares per batch key.
@@ -111,18 +188,32 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
                                                       uint64_t *__restrict__ pos, uint32_t *__restrict__ idx) {
     const uint32_t t = blockIdx.y;
     const uint64_t m = B.m[t];
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool miss = false;
-    if (i < m) {
-        const uint64_t a = B.koff[t][i];
-        const uint64_t found = locate_one(B.kb[t] + a, B.koff[t][i + 1] - a, L.T[t], L.ps[t], L.ns[t]);
-        miss = found == UINT64_MAX;
-        const uint64_t g = B.base[t] + i;
-        pos[g] = ((uint64_t)t << pbits) | (miss ? (1ull << pbits) - 1ull : found);
-        idx[g] = (uint32_t)g;
+    const uint64_t i0 = (uint64_t)blockIdx.x * (LOCATE_ILP * blockDim.x) + threadIdx.x;
+    const uint8_t *kp[LOCATE_ILP];
+    uint64_t len[LOCATE_ILP], found[LOCATE_ILP];
+    bool v[LOCATE_ILP];
+#pragma unroll
+    for (int j = 0; j < LOCATE_ILP; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * blockDim.x;
+        v[j] = i < m;
+        const uint64_t a = v[j] ? B.koff[t][i] : 0;
+        kp[j] = B.kb[t] + a;
+        len[j] = v[j] ? B.koff[t][i + 1] - a : 0;
     }
-    const uint64_t b = __ballot(miss);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(L.missing[t], (uint32_t)__popcll(b));
+    locate_k<LOCATE_ILP>(kp, len, v, L.T[t], L.ps[t], L.ns[t], found);
+    uint32_t nmiss = 0;
+#pragma unroll
+    for (int j = 0; j < LOCATE_ILP; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * blockDim.x;
+        const bool miss = v[j] && found[j] == UINT64_MAX;
+        if (v[j]) {
+            const uint64_t g = B.base[t] + i;
+            pos[g] = ((uint64_t)t << pbits) | (miss ? (1ull << pbits) - 1ull : found[j]);
+            idx[g] = (uint32_t)g;
+        }
+        nmiss += (uint32_t)__popcll(__ballot(miss));
+    }
+    if ((threadIdx.x & 63) == 0 && nmiss) atomicAdd(L.missing[t], nmiss);
 }
 
 __device__ __forceinline__ void set_bit(uint32_t *bm, uint64_t b) { atomicOr(bm + (b >> 5), 1u << (b & 31)); }
@@ -470,7 +561,8 @@ void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, 
 void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
                          uint64_t *pos, uint32_t *idx, hipStream_t st) {
     if (!k || !mmax) return;
-    hipLaunchKernelGGL(k_locate_multi, dim3((uint32_t)ceil_div(mmax, 256), k), dim3(256), 0, st, B, L, pbits, pos, idx);
+    hipLaunchKernelGGL(k_locate_multi, dim3((uint32_t)ceil_div(mmax, 256 * LOCATE_ILP), k), dim3(256), 0, st, B, L, pbits,
+                       pos, idx);
     MKV_LAUNCH_CHECK();
 }
 
