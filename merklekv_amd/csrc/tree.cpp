@@ -1634,8 +1634,12 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
                 Z.bytes[nz++] = (L + 2) * 4;
                 uint32_t *l0 = ens<uint32_t>(t->u_l0, b.m + 1), *l1 = ens<uint32_t>(t->u_l1, b.m + 1);
                 T.t[q] = DirtyTree{t->nodes.as<uint8_t>(), bm, l0, l1, cnt, cnt + L + 1};
-                LM.T[q] = side_of(t);
-                LM.ps[q] = locate_samples_of(t, st, &LM.ns[q]);
+                // replicas sharing t0's key-set id hold the same sorted keys, so their batches are located
+                // in t0: one tree's prefix / permutation / key arrays serve all lookups (a 1/k working set
+                // for the caches and the TLB instead of k copies of the same data)
+                mkv_tree *lt = t->keyset == t0->keyset ? t0 : t;
+                LM.T[q] = side_of(lt);
+                LM.ps[q] = locate_samples_of(lt, st, &LM.ns[q]);
                 LM.missing[q] = cnt + L + 1;
                 t->bm_dirty = true;
             }
