@@ -40,35 +40,15 @@ __device__ __forceinline__ const uint8_t *tree_key(const DiffSide &T, uint64_t i
 
 __device__ __forceinline__ uint64_t locate_run(const uint8_t *k, uint64_t len, uint64_t c0, const DiffSide &T,
                                                uint64_t lo);
-constexpr int LOCATE_ILP = 2;  // batch keys per lane in k_locate_multi
+constexpr int LOCATE_ILP = 2;  // batch keys per lane in k_locate / k_locate_multi
 
-// Sorted position of key k in tree T, UINT64_MAX when it is not a leaf. ps[j] = T.pfx[LOC_STRIDE * j]
-// (ns samples, a 1/64 copy that stays in the MALL / L2): the lower bound is first narrowed on the samples
-// to a window of LOC_STRIDE prefixes (one or two HBM lines) instead of ~log2(n / LOC_STRIDE) random
-// HBM reads into the full prefix array.
-__device__ __forceinline__ uint64_t locate_one(const uint8_t *k, uint64_t len, const DiffSide &T,
-                                               const uint64_t *__restrict__ ps, uint64_t ns) {
-    const uint64_t c0 = key_chunk(k, len, 0);
-    uint64_t j0 = 0, j1 = ns;  // first sample >= c0
-    while (j0 < j1) {
-        const uint64_t mid = (j0 + j1) >> 1;
-        if (ps[mid] < c0) j0 = mid + 1;
-        else j1 = mid;
-    }
-    uint64_t lo = j0 ? (j0 - 1) * LOC_STRIDE + 1 : 0;
-    uint64_t hi = j0 * LOC_STRIDE < T.n ? j0 * LOC_STRIDE : T.n;  // first position with pfx >= c0
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (T.pfx[mid] < c0) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo < T.n && T.pfx[lo] == c0 ? locate_run(k, len, c0, T, lo) : UINT64_MAX;
-}
-
-// K batch keys per thread (k_locate_multi): the same search as locate_one, with the sample and window
-// lower bounds in the branchless fixed-trip form so the K dependent load chains advance together
-// (K misses in flight per lane instead of one), and the common single-candidate tail (one leaf holds
-// the prefix) as straight-line loads; longer equal-prefix runs take locate_run.
+// Sorted positions of K batch keys in tree T (found[j] = UINT64_MAX when key j is not a leaf), K keys per
+// lane. ps[j] = T.pfx[LOC_STRIDE * j] (ns samples, a 1/64 copy that stays in the MALL / L2): the lower
+// bound is first narrowed on the samples to a window of LOC_STRIDE prefixes (one or two HBM lines)
+// instead of ~log2(n / LOC_STRIDE) random HBM reads into the full prefix array. Both lower bounds take
+// the branchless fixed-trip form, so the K dependent load chains advance together (K misses in flight
+// per lane instead of one), and the common single-candidate tail (one leaf holds the prefix) is
+// straight-line loads; longer equal-prefix runs take locate_run.
 template <int K>
 __device__ __forceinline__ void locate_k(const uint8_t *const kp[K], const uint64_t len[K], const bool v[K],
                                          const DiffSide &T, const uint64_t *__restrict__ ps, uint64_t ns,
@@ -171,17 +151,31 @@ __global__ __launch_bounds__(256) void k_locate(const uint8_t *__restrict__ kb, 
                                                 uint64_t m, DiffSide T, const uint64_t *__restrict__ ps, uint64_t ns,
                                                 uint64_t *__restrict__ pos, uint32_t *__restrict__ idx,
                                                 uint32_t *__restrict__ missing) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool miss = false;
-    if (i < m) {
-        const uint64_t a = koff[i];
-        const uint64_t found = locate_one(kb + a, koff[i + 1] - a, T, ps, ns);
-        miss = found == UINT64_MAX;
-        pos[i] = found;
-        idx[i] = (uint32_t)i;
+    const uint64_t i0 = (uint64_t)blockIdx.x * (LOCATE_ILP * blockDim.x) + threadIdx.x;
+    const uint8_t *kp[LOCATE_ILP];
+    uint64_t len[LOCATE_ILP], found[LOCATE_ILP];
+    bool v[LOCATE_ILP];
+#pragma unroll
+    for (int j = 0; j < LOCATE_ILP; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * blockDim.x;
+        v[j] = i < m;
+        const uint64_t a = v[j] ? koff[i] : 0;
+        kp[j] = kb + a;
+        len[j] = v[j] ? koff[i + 1] - a : 0;
     }
-    const uint64_t b = __ballot(miss);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(missing, (uint32_t)__popcll(b));
+    locate_k<LOCATE_ILP>(kp, len, v, T, ps, ns, found);
+    uint32_t nmiss = 0;
+#pragma unroll
+    for (int j = 0; j < LOCATE_ILP; ++j) {
+        const uint64_t i = i0 + (uint64_t)j * blockDim.x;
+        const bool miss = v[j] && found[j] == UINT64_MAX;
+        if (v[j]) {
+            pos[i] = found[j];
+            idx[i] = (uint32_t)i;
+        }
+        nmiss += (uint32_t)__popcll(__ballot(miss));
+    }
+    if ((threadIdx.x & 63) == 0 && nmiss) atomicAdd(missing, nmiss);
 }
 
 __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti L, int pbits,
@@ -526,7 +520,8 @@ inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_d
 void launch_locate(const uint8_t *kb, const uint64_t *koff, uint64_t m, const DiffSide &T, const uint64_t *ps,
                    uint64_t ns, uint64_t *pos, uint32_t *idx, uint32_t *missing, hipStream_t st) {
     if (!m) return;
-    hipLaunchKernelGGL(k_locate, grid1d(m), dim3(256), 0, st, kb, koff, m, T, ps, ns, pos, idx, missing);
+    hipLaunchKernelGGL(k_locate, dim3((uint32_t)ceil_div(m, 256 * LOCATE_ILP)), dim3(256), 0, st, kb, koff, m, T, ps, ns,
+                       pos, idx, missing);
     MKV_LAUNCH_CHECK();
 }
 
