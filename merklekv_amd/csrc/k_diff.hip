@@ -539,7 +539,18 @@ __global__ void k_diff_keys(const uint64_t *__restrict__ refs, uint64_t m, DiffS
     uint64_t len;
     const uint8_t *s = key_at(S, i, &len);
     uint8_t *d = out + off[k];
-    for (uint64_t x = 0; x < len; ++x) d[x] = s[x];
+    // widest copy the alignments allow: fixed 16-B-multiple keys (configs' 32-B keys) move as 16-B words,
+    // so a wave's stores cover one contiguous span (the destination may be mapped host memory)
+    const uintptr_t al = reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d) | (uintptr_t)len;
+    if ((al & 15) == 0) {
+        for (uint64_t x = 0; x < len; x += 16)
+            *reinterpret_cast<uint4 *>(d + x) = *reinterpret_cast<const uint4 *>(s + x);
+    } else if ((al & 3) == 0) {
+        for (uint64_t x = 0; x < len; x += 4)
+            *reinterpret_cast<uint32_t *>(d + x) = *reinterpret_cast<const uint32_t *>(s + x);
+    } else {
+        for (uint64_t x = 0; x < len; ++x) d[x] = s[x];
+    }
 }
 
 // lohi[0] = lower_bound(prefix), lohi[1] = first index >= lo whose key does not start with prefix.
