@@ -347,7 +347,10 @@ def route_block(ctx, n, reps=2):
     torch.cuda.synchronize()
     t = MerkleTree(ctx.local)
     times = []
-    for _ in range(reps + 1):
+    from merklekv_amd.shard import coll_stats, coll_stats_reset
+    for i in range(reps + 1):
+        if i == 1:
+            coll_stats_reset()  # collective timings of the timed redistributions only
         ctx.barrier()
         t0 = time.perf_counter()
         routed = redistribute(t, kb, ko, vb, vo, n, ctx.dist, ctx.coll)
@@ -363,10 +366,12 @@ def route_block(ctx, n, reps=2):
     moved = int(routed.sent[:, 1].sum() + routed.sent[:, 2].sum() - routed.sent[me, 1] - routed.sent[me, 2])
     moved_max = ctx.max_over_ranks(float(moved))
     red = sorted(times[1:])[len(times[1:]) // 2]
+    coll = {k: {"ms_per_call": v[0] / max(v[1], 1) * 1e3, "calls": v[1],
+                "bytes_per_rank_per_call": v[2] / max(v[1], 1)} for k, v in coll_stats.items()}
     out = {"records_per_rank": n, "global_keys": sum(counts), "redistribute_ms": red * 1e3,
            "build_after_ms": build_s * 1e3, "bytes_to_other_ranks_max": moved_max,
            "gb_per_s_per_rank": moved_max / red / 1e9, "shard_min": min(counts), "shard_max": max(counts),
-           "root": root.hex() if root else None,
+           "root": root.hex() if root else None, "collectives": coll,
            "note": "median of %d redistributions after one warm-up; gb_per_s_per_rank = key+value bytes a "
                    "rank sends to other ranks / time (xGMI all-to-all incl. sampling, plan and pack)" % reps}
     del t, routed, kb, vb, ko, vo
@@ -482,6 +487,9 @@ def wl_build(ctx, args):
         first = False
     if first:  # no warmup: validate the shard ranges outside the timed region anyway
         ctx.build(tree, kb, ko, vb, vo, n, validate=True)
+    if ctx.dist is not None:
+        from merklekv_amd.shard import coll_stats_reset
+        coll_stats_reset()  # per-collective timings of the timed steps only
     tree.prof_enable(True)
     tree.prof_reset()
     ctx.barrier()
@@ -501,13 +509,23 @@ def wl_build(ctx, args):
     leaf_avg_ms = leaf_ms / max(leaf_cnt, 1)
     roofline = leaf_roofline(n, leaf_avg_ms, leaf_cnt)
 
+    coll = None
+    if ctx.dist is not None:
+        from merklekv_amd.shard import coll_stats
+        coll = {k: {"ms_per_call": v[0] / max(v[1], 1) * 1e3, "calls": v[1], "bytes_per_rank_per_call":
+                    v[2] / max(v[1], 1)} for k, v in coll_stats.items()}
+
     # ---------------- secondary, 1 GPU only ----------------
-    diff_info = upd_info = d100 = anchor = c0 = shared = None
+    diff_info = upd_info = d100 = anchor = c0 = shared = dN = None
     if not args.no_diff and ctx.world == 1:
         diff_info = diff_secondary(ctx, tree, kb, ko, vb, vo, n)
         upd_info = incremental_secondary(ctx, tree, kb, ko, vb, vo, n)
     del tree, kb, vb, ko, vo
     torch.cuda.empty_cache()
+    if not args.no_diff and ctx.dist is not None:
+        # N>1: configs[2]-style diff of two replicas of this rank's key range (both divergence modes),
+        # exact vs construction on every rank, plus the global sorted list (all-gather-v) once
+        dN = diff_modes(ctx, n, steps=5, warmup=2, gather=True)
     if not args.no_diff and ctx.world == 1:
         c0 = configs0_block(ctx)
         shared = shared_prefix_block(ctx, n)
@@ -540,6 +558,9 @@ def wl_build(ctx, args):
         out["anchor_125m"] = anchor
         out["configs0_gpu"] = c0
         out["shared_prefix_10m"] = shared
+        if ctx.dist is not None:
+            out["diff_sharded"] = dN
+            out["collectives_build"] = coll
         if route is not None:
             out["route"] = route
         out["cpu_baseline"] = cpu
@@ -547,10 +568,24 @@ def wl_build(ctx, args):
 
 
 # ============================================================================================= diff
-def diff_modes(ctx, n, steps, warmup):
+def _all_counts(ctx, x: int) -> list:
+    """All-gather of one int per rank (host list)."""
+    if ctx.dist is None:
+        return [x]
+    torch = ctx.torch
+    t = torch.tensor([x], dtype=torch.int64, device=ctx.coll)
+    out = torch.empty(ctx.world, dtype=torch.int64, device=ctx.coll)
+    if ctx.coll.type == "cuda":
+        ctx.dist.all_gather_into_tensor(out, t)
+    else:
+        ctx.dist.all_gather(list(out.chunk(ctx.world)), t)
+    return [int(v) for v in out.tolist()]
+
+
+def diff_modes(ctx, n, steps, warmup, gather=False):
     """configs[2]: two n-key replicas per rank, 0.1 % divergence, (a) value-only -> top-down walk,
     (b) mixed 80/10/10 change/delete/insert -> merge-join. Each output is checked against the constructed
-    divergent set (exact_vs_construction)."""
+    divergent set (exact_vs_construction). gather (N>1): also the global sorted list on every rank."""
     torch = ctx.torch
     import numpy as np
     from merklekv_amd import MerkleTree
@@ -608,10 +643,31 @@ def diff_modes(ctx, n, steps, warmup):
         union = ctx.sum_over_ranks(n + new)
         res[mode] = {"union_keys": union, "union_keys_per_rank": n + new, "divergent": ctx.sum_over_ranks(len(d)),
                      "expected_divergent": ctx.sum_over_ranks(int(exp_sorted.shape[0])),
-                     "exact_vs_construction": exact, "ms": el / steps * 1e3,
-                     "device_ms": dms / max(steps, 1),
+                     "exact_vs_construction": ctx.sum_over_ranks(int(exact)) == ctx.world,
+                     "ms": el / steps * 1e3, "device_ms": dms / max(steps, 1),
                      "keys_per_s": union * steps / el,
                      "path": "top-down" if mode == "value_only" else "merge-join"}
+        if gather and ctx.dist is not None:
+            # the global sorted list on every rank (sync.rs:67-83 consumes it whole): local diff +
+            # all-gather-v of key lengths and bytes; this rank's slice must sit at its global offset
+            from merklekv_amd.shard import coll_stats, sharded_diff_gather
+            ctx.barrier()
+            t0 = time.perf_counter()
+            graw, goffs = sharded_diff_gather(A, B, ctx.dist, ctx.coll)
+            ctx.barrier()
+            gel = ctx.max_over_ranks(time.perf_counter() - t0)
+            gk = graw.reshape(-1, KLEN)
+            before = int(sum(_all_counts(ctx, len(d))[:ctx.rank]))
+            mine_ok = bool((gk[before:before + len(d)] == got).all()) and len(goffs) - 1 == res[mode]["divergent"]
+            sorted_ok = bool((np.lexsort(gk.T[::-1]) == np.arange(gk.shape[0])).all()) if gk.shape[0] else True
+            res[mode]["global_list"] = {
+                "ms": gel * 1e3, "keys": len(goffs) - 1, "bytes": int(goffs[-1]),
+                "rank_slice_at_global_offset": ctx.sum_over_ranks(int(mine_ok)) == ctx.world,
+                "sorted": sorted_ok,
+                "all_gather_v_ms": coll_stats.get("diff_all_gather_v", [0, 1])[0]
+                / max(coll_stats.get("diff_all_gather_v", [0, 1])[1], 1) * 1e3,
+                "note": "local diff + one (count, bytes) all-gather + one all-gather of padded [u32 lengths | "
+                        "key bytes] blocks; wall time max over ranks"}
         del d, B, kBf, vBf
         torch.cuda.empty_cache()
     del A, kb, vb
@@ -868,6 +924,50 @@ def emit(out):
     f.flush()
 
 
+def launch_ranks(n: int) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes (one per GPU) through
+    torch.distributed.run as a child process — this parent never touches the GPU — forward rank 0's
+    JSON line and fail unless every rank succeeded and the line reports n_gpus == N."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    log(f"bench: launching {n} ranks: {' '.join(cmd)}")
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)  # stderr streams through
+    lines = []
+    for line in p.stdout.splitlines():
+        line = line.strip()
+        if not line.startswith("{"):
+            if line:
+                log(line)
+            continue
+        try:
+            d = json.loads(line)
+        except ValueError:
+            log(line)
+            continue
+        if isinstance(d, dict) and "metric" in d:
+            lines.append(line)
+    if p.returncode != 0:
+        log(f"bench: rank launcher exited with {p.returncode}")
+        return p.returncode or 1
+    if len(lines) != 1:
+        log(f"bench: expected one result line from rank 0, got {len(lines)}")
+        return 1
+    if json.loads(lines[0]).get("n_gpus") != n:
+        log("bench: result line does not report n_gpus == --gpus")
+        return 1
+    sys.stdout.write(lines[0] + "\n")
+    sys.stdout.flush()
+    return 0
+
+
 def main():
     global _RESULT_OUT
     # The result line is the only thing on stdout: fd 1 is pointed at stderr for the rest of the process,
@@ -887,13 +987,19 @@ def main():
     ap.add_argument("--diff-records", type=int, default=100_000_000, help="build workload: diff_100m keys")
     ap.add_argument("--anchor-records", type=int, default=125_000_000,
                     help="build workload at N=1: anchor build size (0 = skip)")
-    ap.add_argument("--route-records", type=int, default=0,
+    ap.add_argument("--route-records", type=int, default=None,
                     help="build workload with a process group: also time the all-to-all redistribution of "
-                         "this many unpartitioned records per rank (SURVEY 8f-3; 0 = skip)")
+                         "this many unpartitioned records per rank (SURVEY 8f-3; default 10M at N>1; 0 = skip)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))  # before anything touches the GPU
     sys.stdout.flush()
     _RESULT_OUT = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')}")
+    if args.route_records is None:
+        args.route_records = 10_000_000 if int(os.environ.get("WORLD_SIZE", "1")) > 1 else 0
     if args.n is None:
         multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
         args.n = {"build": 125_000_000 if multi else 10_000_000, "diff": 100_000_000,

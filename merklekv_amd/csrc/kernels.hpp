@@ -58,8 +58,9 @@ void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *c
 void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t st);
 // Fused form for builds: pfx[i] = the 8 key bytes at byte offset `off` (0 = the prefix) AND all eight
 // digit histograms, one read of the keys. Control words the onesweep passes never touch (they use
-// 8 * 256 + 0..31): PH_MAXLEN_WORD = longest key length; with off == 0 also PH_NLCP_WORD = ~(shortest
-// zero-padded common prefix of any key with key 0) and PH_K0_WORD/+1 = key 0's first 8 bytes (hi, lo).
+// 8 * 256 + 0..31): PH_MAXLEN_WORD = longest key length; with lcp = true (whatever `off` is) also
+// PH_NLCP_WORD = ~(shortest zero-padded common prefix of any key with key 0, measured from byte 0) and
+// PH_K0_WORD/+1 = key 0's first 8 bytes (hi, lo).
 constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
 constexpr uint32_t PH_NLCP_WORD = 8 * 256 + 62;
 constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;

@@ -234,11 +234,13 @@ struct mkv_tree {
     DevBuf w_scan, w_gets, w_nl1, w_nl2, w_scr, w_ks, w_kl, w_vs, w_vl, w_found, w_rank;  // wire ingestion
     DevBuf d_seam, d_S, d_fr;
     // redistribution (mkv_route_*): splitters, per-destination counts, the destination-grouped permutation
-    DevBuf rt_spl, rt_cnt;
+    // (the permutation lives in a route-owned buffer: the sort scratch it comes from is reused by every
+    // other entry point; the plan's blobs are recorded so a pack of different records is refused)
+    DevBuf rt_spl, rt_cnt, rt_pbuf;
     const uint32_t *rt_perm = nullptr;
     uint64_t rt_n = 0;
-    const uint8_t *rt_kb = nullptr;
-    const uint64_t *rt_koff = nullptr;
+    const uint8_t *rt_kb = nullptr, *rt_vb = nullptr;
+    const uint64_t *rt_koff = nullptr, *rt_voff = nullptr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
     // batch merge (key-set changes): batch tombstones, merged prefixes / permutation / levels, count
@@ -264,6 +266,16 @@ struct mkv_tree {
     const uint8_t *in_tomb = nullptr;
     bool counted = false;  // counted in g_live_trees
 };
+
+// Same key-set id => same sorted keys. The id is a correctness input (the batched dirty path locates a
+// replica's batch in another tree, the walks skip the leaf-key check), so the cheap host-side facts that
+// must agree are checked every time: a mismatch means some key-changing path kept a stale id.
+static bool same_keyset(const mkv_tree *a, const mkv_tree *b) {
+    if (a->keyset != b->keyset) return false;
+    if (a->n != b->n || a->nstore != b->nstore || a->kbytes != b->kbytes)
+        throw Error(ST_ESTATE, "internal: trees share a key-set id but hold different keys");
+    return true;
+}
 
 namespace {
 
@@ -1637,7 +1649,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
                 // replicas sharing t0's key-set id hold the same sorted keys, so their batches are located
                 // in t0: one tree's prefix / permutation / key arrays serve all lookups (a 1/k working set
                 // for the caches and the TLB instead of k copies of the same data)
-                mkv_tree *lt = t->keyset == t0->keyset ? t0 : t;
+                mkv_tree *lt = same_keyset(t, t0) ? t0 : t;
                 LM.T[q] = side_of(lt);
                 LM.ps[q] = locate_samples_of(lt, st, &LM.ns[q]);
                 LM.missing[q] = cnt + L + 1;
@@ -2221,7 +2233,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
             pos = sw ? k2 : k1;
         }
         // mismatching keys (nbad != 0) are read back with the key list's byte count (keylist_from_refs)
-        launch_topdown_leaves(pos, m, A, B, a->keyset != b->keyset, refs, cnt + L + 1, t->st);
+        launch_topdown_leaves(pos, m, A, B, !same_keyset(a, b), refs, cnt + L + 1, t->st);
     }
     *m_out = m;
     return true;
@@ -2386,7 +2398,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
         uint64_t check = 0;  // variants whose key set may differ from the base's
         for (uint32_t i = 0; i < k; ++i)
-            if (vs[i]->keyset != a->keyset) check |= 1ull << i;
+            if (!same_keyset(vs[i], a)) check |= 1ull << i;
         launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
         small_d2h(t, hb, nbad, 2 * k * 4, t->st);
     }
@@ -2458,7 +2470,7 @@ mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, 
             std::vector<uint32_t> walk;
             // a variant with the base's key-set id holds the same key sequence: no sampled screen
             std::vector<uint32_t> same_ks, other_ks;
-            for (uint32_t c : cand) (others[c]->keyset == a->keyset ? same_ks : other_ks).push_back(c);
+            for (uint32_t c : cand) (same_keyset(others[c], a) ? same_ks : other_ks).push_back(c);
             for (uint32_t c : same_ks) {
                 const mkv_tree *o = others[c];
                 if (roots_a && !o->combine_pending && o->has_root && std::memcmp(a->root, o->root, 32) == 0)
@@ -2964,10 +2976,15 @@ mkv_status mkv_route_plan(mkv_tree *t, mkv_blob keys, mkv_blob values, uint32_t 
             counts[3 * r + 1] = hc[world + r];
             counts[3 * r + 2] = hc[2 * world + r];
         }
-        t->rt_perm = sw ? v2 : v1;
+        uint32_t *perm = ens<uint32_t>(t->rt_pbuf, n + 1);
+        if (n) MKV_HIP(hipMemcpyAsync(perm, sw ? v2 : v1, 4 * n, hipMemcpyDeviceToDevice, t->st));
+        wait_stream(t, t->st);
+        t->rt_perm = perm;
         t->rt_n = n;
         t->rt_kb = keys.bytes;
         t->rt_koff = keys.offsets;
+        t->rt_vb = values.bytes;
+        t->rt_voff = values.offsets;
     });
 }
 
@@ -2977,7 +2994,8 @@ mkv_status mkv_route_pack(mkv_tree *t, mkv_blob keys, mkv_blob values, uint8_t *
         NEED(t, "tree is null");
         NEED(keys.n == values.n, "keys.n != values.n");
         NEED(t->rt_perm || keys.n == 0, "mkv_route_plan first");
-        NEED(keys.n == t->rt_n && keys.bytes == t->rt_kb && keys.offsets == t->rt_koff,
+        NEED(keys.n == t->rt_n && keys.bytes == t->rt_kb && keys.offsets == t->rt_koff &&
+                 values.bytes == t->rt_vb && values.offsets == t->rt_voff,
              "mkv_route_pack: not the blobs of the last mkv_route_plan");
         const uint64_t n = keys.n;
         if (n == 0) return MKV_OK;

@@ -32,6 +32,21 @@ from ._lib import FRINGE_BYTES
 
 _bufs: dict = {}
 
+# Wall time of each collective kind (host clock around the collective and the wait for its result):
+# name -> [seconds, calls, payload bytes per rank]. Read by bench.py (per-collective timings).
+coll_stats: dict = {}
+
+
+def _coll_add(name: str, secs: float, nbytes: int) -> None:
+    s = coll_stats.setdefault(name, [0.0, 0, 0])
+    s[0] += secs
+    s[1] += 1
+    s[2] += int(nbytes)
+
+
+def coll_stats_reset() -> None:
+    coll_stats.clear()
+
 
 def _is_gpu(device) -> bool:
     import torch
@@ -66,15 +81,21 @@ def _all_gather_bytes(dist, payload: bytes, device, group=None) -> list[bytes]:
 
 def shard_counts(dist, n_local: int, device, group=None) -> list[int]:
     """All-gather of the 8-byte leaf counts; the host needs them (offsets plan the levels)."""
+    import time
+
     import torch
+    t0 = time.perf_counter()
     if _is_gpu(device):
         world = dist.get_world_size(group)
         src = torch.full((1,), int(n_local), dtype=torch.int64, device=device)
         out = torch.empty(world, dtype=torch.int64, device=device)
         dist.all_gather_into_tensor(out, src, group=group)
-        return [int(x) for x in out.tolist()]
-    raw = _all_gather_bytes(dist, np.array([n_local], dtype=np.uint64).tobytes(), device, group)
-    return [int(np.frombuffer(r, dtype=np.uint64)[0]) for r in raw]
+        res = [int(x) for x in out.tolist()]
+    else:
+        raw = _all_gather_bytes(dist, np.array([n_local], dtype=np.uint64).tobytes(), device, group)
+        res = [int(np.frombuffer(r, dtype=np.uint64)[0]) for r in raw]
+    _coll_add("counts_all_gather", time.perf_counter() - t0, 8)
+    return res
 
 
 def check_ranges(tree, counts: list[int], dist, device, group=None) -> None:
@@ -129,8 +150,11 @@ def shard_recombine_many(trees, dist, total: int, device="cpu", group=None) -> l
         base = src.data_ptr()
         for i, t in enumerate(trees):
             t.shard_fringe_device(base + i * FRINGE_BYTES)  # complete on return
+        import time
+        t0 = time.perf_counter()
         dist.all_gather_into_tensor(dst[:world * k * FRINGE_BYTES], src[:k * FRINGE_BYTES], group=group)
         torch.cuda.current_stream(device).synchronize()  # the library runs on its own streams
+        _coll_add("fringe_all_gather", time.perf_counter() - t0, k * FRINGE_BYTES)
         out = dst.data_ptr()
         return [t.shard_combine_device(out + i * FRINGE_BYTES, world, k * FRINGE_BYTES, total)
                 for i, t in enumerate(trees)]
@@ -154,6 +178,43 @@ def sharded_diff(a, b, dist, device="cpu", group=None):
     raw, offs = a.diff_keys_packed(b)
     counts = shard_counts(dist, len(offs) - 1, device, group)
     return (raw, offs), sum(counts[:rank]), sum(counts)
+
+
+def sharded_diff_gather(a, b, dist, device="cpu", group=None):
+    """diff_keys (merkle.rs:171-196) of two sharded trees as ONE sorted list on every rank — what
+    SyncManager::sync_once consumes whole (sync.rs:67-83). Each rank diffs its own key range on the
+    device, then an all-gather-v of the divergent keys: one all-gather of (count, bytes) per rank, one
+    all-gather of [u32 key lengths | key bytes] blocks padded to the largest rank's (RCCL over xGMI on a
+    GPU group). Ranges are ordered by rank, so the rank-order concatenation is already sorted and unique.
+    Returns (key bytes uint8, offsets uint64[n+1])."""
+    import time
+
+    import torch
+    world = dist.get_world_size(group)
+    raw, offs = a.diff_keys_packed(b)
+    n, nb = len(offs) - 1, int(offs[-1])
+    gpu = _is_gpu(device)
+    t0 = time.perf_counter()
+    meta = _all_gather_tensor(dist, torch.tensor([n, nb], dtype=torch.int64, device=device), group)
+    meta = meta.cpu().numpy().reshape(world, 2)
+    mn, mb = int(meta[:, 0].max()), int(meta[:, 1].max())
+    blk = 4 * mn + mb
+    if blk == 0:
+        _coll_add("diff_all_gather_v", time.perf_counter() - t0, 16)
+        return np.zeros(0, np.uint8), np.zeros(1, np.uint64)
+    pay = np.zeros(blk, np.uint8)
+    pay[:4 * n].view(np.uint32)[:] = np.diff(offs).astype(np.uint32)
+    pay[4 * mn:4 * mn + nb] = raw[:nb]
+    src = torch.from_numpy(pay)
+    if gpu:
+        src = src.to(device, non_blocking=False)
+    allp = _all_gather_tensor(dist, src, group).cpu().numpy().reshape(world, blk)
+    _coll_add("diff_all_gather_v", time.perf_counter() - t0, 16 + blk)
+    lens = np.concatenate([allp[r, :4 * int(meta[r, 0])].view(np.uint32) for r in range(world)])
+    out = np.concatenate([allp[r, 4 * mn:4 * mn + int(meta[r, 1])] for r in range(world)])
+    o = np.zeros(len(lens) + 1, np.uint64)
+    np.cumsum(lens, dtype=np.uint64, out=o[1:])
+    return out, o
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -182,15 +243,20 @@ def _all_gather_tensor(dist, t, group=None):
 
 def _all_to_all(dist, out, inp, out_splits, in_splits, group=None) -> None:
     """all_to_all_single over RCCL for device tensors; staged through host memory for gloo."""
+    import time
     outs = [int(x) for x in out_splits]
     ins = [int(x) for x in in_splits]
+    t0 = time.perf_counter()
     if _is_gpu(out.device) and _backend(dist, group) == "nccl":
         dist.all_to_all_single(out, inp, outs, ins, group=group)
-        return
-    o = out.cpu() if _is_gpu(out.device) else out
-    dist.all_to_all_single(o, inp.cpu(), outs, ins, group=group)
-    if o is not out:
-        out.copy_(o)
+        import torch
+        torch.cuda.current_stream(out.device).synchronize()
+    else:
+        o = out.cpu() if _is_gpu(out.device) else out
+        dist.all_to_all_single(o, inp.cpu(), outs, ins, group=group)
+        if o is not out:
+            out.copy_(o)
+    _coll_add("all_to_all", time.perf_counter() - t0, inp.numel() * inp.element_size())
 
 
 @dataclass
@@ -231,7 +297,9 @@ def redistribute(tree, kb, koff, vb, voff, n: int, dist, device, group=None, sam
     counts = shard_counts(dist, n, device, group)
     N = sum(counts)
     m = [min(c, -(-samples * c // N)) if N else 0 for c in counts]
-    loc = torch.zeros(max(max(m), 1), dtype=torch.int64, device=dev)
+    # torch.empty: no fill kernel on torch's stream racing the library's sample writes (the padding
+    # beyond m[rank] is never read)
+    loc = torch.empty(max(max(m), 1), dtype=torch.int64, device=dev)
     if m[rank]:
         tree.route_sample(kb, koff, n, m[rank], loc)
     gathered = _all_gather_tensor(dist, loc, group).cpu().numpy().view(np.uint64)

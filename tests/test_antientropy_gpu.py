@@ -33,12 +33,14 @@ def test_build_digests_equals_build(n):
     keys, vals = split_blob(kb, ko), split_blob(vb, vo)
     dig = b"".join(leaf_hash(k, v) for k, v in zip(keys, vals))
     b = MerkleTree.from_digests((kb, ko), np.frombuffer(dig, np.uint8) if dig else np.zeros(0, np.uint8))
-    assert b.get_root_hash() == a.get_root_hash()
-    assert len(b) == len(a)
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    assert b.get_root_hash() == a.get_root_hash() == o.root()  # both against the oracle, not each other
+    assert len(b) == len(a) == len(o)
     if n:
         raw, offs, d = a.leaves_packed()
         raw2, offs2, d2 = b.leaves_packed()
         assert np.array_equal(raw, raw2) and np.array_equal(offs, offs2) and np.array_equal(d, d2)
+        assert np.array_equal(d, o.level(0))
         assert a.diff_keys_bytes(b) == []
 
 

@@ -357,3 +357,64 @@ def test_route_splitters_host():
     assert list(route_splitters(np.zeros(0, np.uint64), 3)) == [2 ** 64 - 1] * 2
     dup = np.array([5] * 10 + [9] * 2, np.uint64)
     assert list(route_splitters(dup, 3)) == [5, 5]
+
+
+def _fn_diff_gather(rank, dist, shards_a, shards_b, values_a, values_b):
+    from merklekv_amd.shard import coll_stats, sharded_diff_gather, sharded_root
+    a, b = ModelShardTree(), ModelShardTree()
+    sharded_root(a, shards_a[rank], [values_a[k] for k in shards_a[rank]], dist, device="cpu")
+    sharded_root(b, shards_b[rank], [values_b[k] for k in shards_b[rank]], dist, device="cpu")
+    raw, offs = sharded_diff_gather(a, b, dist, device="cpu")
+    b_ = raw.tobytes()
+    return [b_[int(offs[i]):int(offs[i + 1])] for i in range(len(offs) - 1)], dict(coll_stats)
+
+
+@pytest.mark.parametrize("world,empty_b_rank", [(2, None), (3, None), (3, 1)])
+def test_sharded_diff_gather_gloo(world, empty_b_rank):
+    """the sharded diff assembled into ONE sorted list on every rank (all-gather-v of key
+    lengths + bytes) equals diff_keys over the union (merkle.rs:171-196, consumed by sync.rs:67-83),
+    including key-set changes at the shard seams (keys inserted right after a splitter, the first key of
+    a range deleted) and a rank whose B range is empty."""
+    n = 900
+    keys = [b"key%05d" % i for i in range(n)]
+    va = {k: b"a" + k for k in keys}
+    vb = dict(va)
+    cuts = [keys[n * (r + 1) // world] for r in range(world - 1)]
+    for i in range(0, n, 41):
+        vb[keys[i]] = b"changed"
+    for c in cuts:
+        vb.pop(c)                      # first key of the next range deleted on B
+        vb[c + b"\x00"] = b"seam-new"  # new key right after the deleted one, same range
+    vb[b"key"] = b"before-everything"  # new smallest key (rank 0)
+    vb[b"zzz"] = b"after-everything"   # new largest key (last rank)
+    bounds = [b""] + cuts + [None]
+
+    def part(ks):
+        ks = sorted(ks)
+        return [[k for k in ks if bounds[r] <= k and (bounds[r + 1] is None or k < bounds[r + 1])]
+                for r in range(world)]
+
+    pa, pb = part(va), part(vb)
+    if empty_b_rank is not None:
+        for k in pb[empty_b_rank]:
+            vb.pop(k)
+        pb[empty_b_rank] = []
+    ra, rb = PyMerkleTree(), PyMerkleTree()
+    for k, v in va.items():
+        ra.insert(k, v)
+    for k, v in vb.items():
+        rb.insert(k, v)
+    want = ra.diff_keys(rb)
+    res = _run_fn(world, _fn_diff_gather, pa, pb, va, vb)
+    for got, stats in res:
+        assert got == want
+        assert stats["diff_all_gather_v"][1] == 1
+
+
+def test_sharded_diff_gather_identical_gloo():
+    """Identical replicas: every rank gets the empty list (no key bytes to gather)."""
+    keys = [b"k%04d" % i for i in range(300)]
+    v = {k: k for k in keys}
+    parts = [keys[:100], keys[100:]]
+    res = _run_fn(2, _fn_diff_gather, parts, parts, v, v)
+    assert [g for g, _ in res] == [[], []]

@@ -1,5 +1,5 @@
-"""Sharded build on the device: mkv_shard_prepare/_reduce/_fringe/_combine must give the unsharded
-root bit-exactly (seam nodes across unaligned shard boundaries, empty / one-leaf shards, R5 promotion
+"""Sharded build on the device: mkv_shard_prepare/_reduce/_fringe/_combine must give the oracle's
+root of the union bit-exactly (seam nodes across unaligned shard boundaries, empty / one-leaf shards, R5 promotion
 at the global end only)."""
 import itertools
 import os
@@ -36,12 +36,20 @@ def _sharded(shards):
     return roots
 
 
+def _oracle_root(keys, vals):
+    from oracle import coracle
+    from oracle.merkle_oracle import pack
+    return coracle.OracleTree.build(*pack(keys), *pack(vals)).root()
+
+
 def test_sharded_small_exhaustive():
+    from oracle.merkle_oracle import PyMerkleTree
     for n in (1, 2, 3, 5, 8, 13, 33):
         keys = [b"k%04d" % i for i in range(n)]
-        t = MerkleTree()
-        t.build(keys, keys)
-        want = t.get_root_hash()
+        ref = PyMerkleTree()
+        for k in keys:
+            ref.insert(k, k)
+        want = ref.get_root_hash()
         for cuts in itertools.combinations(range(n + 1), 2):
             roots = _sharded(_shards(keys, keys, cuts))
             assert all(r == want for r in roots), (n, cuts)
@@ -52,9 +60,8 @@ def test_sharded_synthetic_uneven(world):
     n = 200_003
     kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, n)
     keys, vals = split_blob(kb, ko), split_blob(vb, vo)
-    t = MerkleTree()
-    t.build((kb, ko), (vb, vo))
-    want = t.get_root_hash()
+    from oracle import coracle
+    want = coracle.OracleTree.build(kb, ko, vb, vo).root()
     step = n // world
     cuts = [step * i + (i * 7919) % 1000 for i in range(1, world)]
     roots = _sharded(_shards(keys, vals, cuts))
@@ -71,10 +78,9 @@ def test_sharded_generator_ranges():
         shards.append((k, v))
         allk += k
         allv += v
-    t = MerkleTree()
-    t.build(allk, allv)
+    want = _oracle_root(allk, allv)
     roots = _sharded(shards)
-    assert all(r == t.get_root_hash() for r in roots)
+    assert all(r == want for r in roots)
 
 
 def _free_port():
@@ -119,9 +125,7 @@ def test_sharded_two_processes_gloo_same_gpu():
         kb, ko, vb, vo = gen_records(DEFAULT_SEED, g * 30_000, 30_000, shard=g, nshards=world)
         allk += split_blob(kb, ko)
         allv += split_blob(vb, vo)
-    t = MerkleTree()
-    t.build(allk, allv)
-    assert [r for _, r in res] == [t.get_root_hash()] * world
+    assert [r for _, r in res] == [_oracle_root(allk, allv)] * world
 
 
 def test_fringe_device_combine_matches_host():
@@ -131,12 +135,11 @@ def test_fringe_device_combine_matches_host():
     import torch
 
     from merklekv_amd._lib import FRINGE_BYTES
+    from oracle import coracle
     n = 100_003
     kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, n)
     keys, vals = split_blob(kb, ko), split_blob(vb, vo)
-    t = MerkleTree()
-    t.build((kb, ko), (vb, vo))
-    want = t.get_root_hash()
+    want = coracle.OracleTree.build(kb, ko, vb, vo).root()
     for world in (1, 3, 8):
         step = n // world
         shards = _shards(keys, vals, [step * i + 17 * i for i in range(1, world)])
@@ -273,11 +276,11 @@ def test_rccl_single_rank_device_fringe_path():
     roots, again, routed_root, routed_n = q.get(timeout=300)
     p.join(timeout=60)
     assert p.exitcode == 0
+    from oracle import coracle
     kb, ko, vb, vo = gen_records(DEFAULT_SEED, 0, 50_000)
-    t = MerkleTree()
-    t.build((kb, ko), (vb, vo))
-    assert roots == [t.get_root_hash()] * 3 and again == roots
-    assert routed_root == t.get_root_hash() and routed_n == 50_000
+    want = coracle.OracleTree.build(kb, ko, vb, vo).root()
+    assert roots == [want] * 3 and again == roots
+    assert routed_root == want and routed_n == 50_000
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -425,6 +428,4 @@ def test_device_entry_points_refuse_host_pointers():
     with pytest.raises(MerkleError, match="not device-accessible"):
         t.build_device(dkb.data_ptr(), hko.data_ptr(), dvb.data_ptr(), dvo.data_ptr(), n)
     t.build_device(dkb.data_ptr(), dko.data_ptr(), dvb.data_ptr(), dvo.data_ptr(), n)  # still usable
-    ref = MerkleTree()
-    ref.build(keys, vals)
-    assert t.get_root_hash() == ref.get_root_hash()
+    assert t.get_root_hash() == _oracle_root(keys, vals)

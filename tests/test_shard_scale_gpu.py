@@ -1,0 +1,206 @@
+"""configs[3] on one GPU: 1B keys sharded by key range over 8 GPUs, rehearsed as 8
+in-process shards on one device with the exact per-rank protocol (shard_prepare -> counts -> shard_reduce
+-> fringe -> combine; diffs per shard, rank order = global order).
+
+  * 10M keys in 8 generator key ranges (shard=g, nshards=8): the global root of the sharded build and the
+    concatenated per-shard value-only (top-down) and mixed (merge-join) diffs equal the C oracle on the
+    union (/root/reference/src/store/merkle.rs:73-121, :171-196);
+  * 125M keys (one configs[3] GPU's worth, split 8 ways) through the device fringe path
+    (shard_fringe_device / shard_combine_device, stride = k x MKV_FRINGE_BYTES, two replicas per gathered
+    block): root == the unsharded device build of the same records, and the sharded diffs equal the
+    constructed divergent set with global offsets from the counts.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from merklekv_amd import MerkleTree  # noqa: E402
+from oracle import coracle  # noqa: E402
+from oracle.merkle_oracle import DEFAULT_SEED  # noqa: E402
+
+K, V = 32, 100
+W = 8
+
+
+@pytest.fixture(autouse=True)
+def _free_torch_cache():
+    yield
+    import gc
+
+    import torch
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def _concat(parts):
+    """Union blob of fixed-shape shard blobs (kb, ko, vb, vo) in rank order."""
+    kb = np.concatenate([p[0] for p in parts])
+    vb = np.concatenate([p[2] for p in parts])
+    n = sum(len(p[1]) - 1 for p in parts)
+    return kb, np.arange(n + 1, dtype=np.uint64) * K, vb, np.arange(n + 1, dtype=np.uint64) * V
+
+
+def _fixed(kb, vb):
+    n = len(kb) // K
+    return kb, np.arange(n + 1, dtype=np.uint64) * K, vb, np.arange(n + 1, dtype=np.uint64) * V
+
+
+def _sharded_host(parts):
+    """The per-rank protocol with host fringes; returns (trees, roots, counts)."""
+    trees = [MerkleTree() for _ in parts]
+    counts = [t.shard_prepare((kb, ko), (vb, vo)) for t, (kb, ko, vb, vo) in zip(trees, parts)]
+    N = sum(counts)
+    for r, t in enumerate(trees):
+        t.shard_reduce(sum(counts[:r]), N)
+    fr = b"".join(t.shard_fringe() for t in trees)
+    return trees, [t.shard_combine(fr, len(trees), N) for t in trees], counts
+
+
+def _replica_b(g, kb, vb, mixed):
+    """Shard g's B records: every 1000th value changed; mixed also deletes every 1201st record and
+    inserts 1/1000 new keys of the same key range."""
+    k2, v2 = kb.reshape(-1, K), vb.reshape(-1, V).copy()
+    n = len(k2)
+    v2[np.arange(3 + g, n, 1000), 5] ^= 0x10
+    if not mixed:
+        return k2.reshape(-1), v2.reshape(-1)
+    keep = np.ones(n, bool)
+    keep[np.arange(11 + g, n, 1201)] = False
+    m = n // 1000
+    nk, _, nv, _ = coracle.gen_records(DEFAULT_SEED, 10**12 + g * m, m, shard=g, nshards=W)
+    return (np.concatenate([k2[keep].reshape(-1), nk]), np.concatenate([v2[keep].reshape(-1), nv]))
+
+
+def test_sharded_8way_10m_vs_oracle():
+    ng = 1_250_000
+    parts = [coracle.gen_records(DEFAULT_SEED, g * ng, ng, shard=g, nshards=W) for g in range(W)]
+    shani = coracle.set_backend(1)  # SHA-NI oracle backend (cross-checked vs portable in test_oracle)
+    try:
+        oa = coracle.OracleTree.build(*_concat(parts))
+        trees_a, roots_a, counts_a = _sharded_host(parts)
+        assert counts_a == [ng] * W
+        assert roots_a == [oa.root()] * W
+        for mixed in (False, True):
+            bparts = [_fixed(*_replica_b(g, p[0], p[2], mixed)) for g, p in enumerate(parts)]
+            ob = coracle.OracleTree.build(*_concat(bparts))
+            trees_b, roots_b, counts_b = _sharded_host(bparts)
+            assert roots_b == [ob.root()] * W, mixed
+            want = oa.diff(ob)
+            got, offs = [], []
+            for ta, tb in zip(trees_a, trees_b):
+                offs.append(len(got))
+                got += ta.diff_keys_bytes(tb)
+            assert got == want, mixed
+            assert len(want) >= W * ng // 1000
+            del trees_b
+    finally:
+        coracle.set_backend(0)
+    assert shani in (0, 1)
+
+
+def _dev_shard(torch, g, ng, kall, vall):
+    """Generate shard g's records into its slice of the union buffers; returns device offsets."""
+    from merklekv_amd.merkle import gen_records_device
+    ko = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    vo = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    kv = kall[g * ng * K:(g + 1) * ng * K]
+    vv = vall[g * ng * V:(g + 1) * ng * V]
+    gen_records_device(0, DEFAULT_SEED, g * ng, ng, K, V, kv.data_ptr(), ko.data_ptr(), vv.data_ptr(),
+                       vo.data_ptr(), shard=g, nshards=W)
+    return kv, ko, vv, vo
+
+
+def _sharded_device(torch, blobs):
+    """The RCCL path's device-resident fringe buffers: every shard writes its fringe into a (world x 2 x
+    FRINGE_BYTES) buffer (two replica slots per rank, like shard_recombine_many), combined from there."""
+    from merklekv_amd._lib import FRINGE_BYTES
+    trees = [MerkleTree() for _ in blobs]
+    counts = [t.shard_prepare(b, None, on_device=True) for t, b in zip(trees, blobs)]
+    N = sum(counts)
+    for r, t in enumerate(trees):
+        t.shard_reduce(sum(counts[:r]), N)
+    buf = torch.zeros(len(trees) * 2 * FRINGE_BYTES, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    for r, t in enumerate(trees):
+        t.shard_fringe_device(buf.data_ptr() + (2 * r + 1) * FRINGE_BYTES)  # slot 1 of rank r
+    roots = [t.shard_combine_device(buf.data_ptr() + FRINGE_BYTES, len(trees), 2 * FRINGE_BYTES, N)
+             for t in trees]
+    return trees, roots, counts
+
+
+def test_sharded_8way_125m_device_fringe():
+    import torch
+    ng = 125_000_000 // W
+    n = ng * W
+    kall = torch.empty(n * K + 64, dtype=torch.uint8, device="cuda")
+    vall = torch.empty(n * V + 64, dtype=torch.uint8, device="cuda")
+    shards = [_dev_shard(torch, g, ng, kall, vall) for g in range(W)]
+    torch.cuda.synchronize()
+    blobs = [(kv, ko, vv, vo, ng) for kv, ko, vv, vo in shards]
+    trees_a, roots_a, counts = _sharded_device(torch, blobs)
+    assert counts == [ng] * W
+    # the unsharded device build of the same records (the 10M sharded test pins both to the oracle)
+    uko = torch.arange(0, n + 1, device="cuda", dtype=torch.int64) * K
+    uvo = torch.arange(0, n + 1, device="cuda", dtype=torch.int64) * V
+    torch.cuda.synchronize()
+    whole = MerkleTree()
+    whole.build_device(kall.data_ptr(), uko.data_ptr(), vall.data_ptr(), uvo.data_ptr(), n)
+    want_root = whole.get_root_hash()
+    del whole, uko, uvo
+    torch.cuda.empty_cache()
+    assert roots_a == [want_root] * W
+    # replicas: value-only (top-down per shard) and mixed (merge-join per shard), 0.1 % per shard
+    g_ = torch.Generator(device="cuda")
+    g_.manual_seed(31)
+    for mode in ("value_only", "mixed"):
+        bl, exp = [], []
+        for g, (kv, ko, vv, vo) in enumerate(shards):
+            k2, v2 = kv.view(ng, K), vv.view(ng, V).clone()
+            perm = torch.randperm(ng, device="cuda", generator=g_)
+            nd = ng // 1000
+            if mode == "value_only":
+                chg, rm, new = perm[:nd], perm[:0], 0
+            else:
+                c, r = nd * 8 // 10, nd // 10
+                chg, rm, new = perm[:c], perm[c:c + r], nd - c - r
+            v2[chg, 9] ^= 4
+            keep = torch.ones(ng, dtype=torch.bool, device="cuda")
+            keep[rm] = False
+            kB, vB = k2[keep], v2[keep]
+            e = [k2[chg], k2[rm]]
+            if new:
+                from merklekv_amd.merkle import gen_records_device
+                nkb = torch.empty(new * K + 64, dtype=torch.uint8, device="cuda")
+                nvb = torch.empty(new * V + 64, dtype=torch.uint8, device="cuda")
+                nko = torch.empty(new + 1, dtype=torch.int64, device="cuda")
+                nvo = torch.empty(new + 1, dtype=torch.int64, device="cuda")
+                gen_records_device(0, DEFAULT_SEED, 10**12 + g * new, new, K, V, nkb.data_ptr(), nko.data_ptr(),
+                                   nvb.data_ptr(), nvo.data_ptr(), shard=g, nshards=W)
+                torch.cuda.synchronize()
+                kB = torch.cat([kB, nkb[: new * K].view(new, K)])
+                vB = torch.cat([vB, nvb[: new * V].view(new, V)])
+                e.append(nkb[: new * K].view(new, K))
+            nb = kB.shape[0]
+            kBf, vBf = kB.contiguous().view(-1), vB.contiguous().view(-1)
+            bl.append((kBf, torch.arange(0, nb + 1, device="cuda", dtype=torch.int64) * K, vBf,
+                       torch.arange(0, nb + 1, device="cuda", dtype=torch.int64) * V, nb))
+            ex = torch.cat(e).cpu().numpy()
+            exp.append(ex[np.lexsort(ex.T[::-1])])
+            del v2, kB, vB
+        torch.cuda.synchronize()
+        trees_b, roots_b, counts_b = _sharded_device(torch, bl)
+        assert len(set(roots_b)) == 1 and roots_b[0] != want_root
+        want = np.concatenate(exp)  # ranges are ordered by rank: the concatenation is the global order
+        got, offs = [], []
+        for ta, tb in zip(trees_a, trees_b):
+            raw, o = ta.diff_keys_packed(tb)
+            offs.append(sum(len(x) for x in got))
+            got.append(raw.reshape(-1, K))
+        cnt = [len(x) for x in got]
+        assert offs == [sum(cnt[:r]) for r in range(W)]  # global offsets from the counts
+        g_all = np.concatenate(got)
+        assert np.array_equal(g_all, want), mode
+        assert (np.lexsort(g_all.T[::-1]) == np.arange(len(g_all))).all()  # globally sorted
+        del trees_b, bl
+        torch.cuda.empty_cache()

@@ -391,3 +391,48 @@ def test_keylist_views_zero_copy_and_shared_blocks():
     one = base.diff_keys_view(vs[2])
     b, o = one.raw.tobytes(), one.offs.tolist()
     assert [b[o[i]:o[i + 1]] for i in range(len(one))] == want[2]
+
+
+def test_clone_keyset_change_then_batched_update_and_diff_vs_oracle():
+    """the key-set id is a correctness input of the batched dirty path (a replica's batch is
+    located in the first tree of its group) and of the batched walk (leaf-key check skipped). A clone
+    that swaps keys through apply() (same count, same level plan) must leave the group: a batched
+    upsert over [orig, clone] and diff_many against the original must still equal the oracle."""
+    import torch
+    n = 9001
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED + 17, 0, n)
+    keys = split_blob(kb, ko)
+    orig = MerkleTree()
+    orig.build((kb, ko), (vb, vo))
+    o_orig = coracle.OracleTree.build(kb, ko, vb, vo)
+    clone = orig.clone()
+    # apply(): remove two keys, insert two new ones (count and level plan unchanged, positions shift)
+    new_keys = [b"!!first-new", b"~~last-new"]
+    clone.apply([keys[10], keys[4000]] + new_keys, [b"", b""] + [b"n1", b"n2"], [1, 1, 0, 0])
+    o_clone = o_orig.remove(*pack([keys[10], keys[4000]])).upsert(*pack(new_keys), *pack([b"n1", b"n2"]))
+    assert len(clone) == len(orig) == n
+    assert clone.get_root_hash() == o_clone.root()
+    rng = np.random.default_rng(3)
+    live = [k for k in keys if k not in (keys[10], keys[4000])]
+    batches, keep, oracles = [], [], []
+    for r, (t, o, pool) in enumerate(((orig, o_orig, keys), (clone, o_clone, live + new_keys))):
+        idx = [int(i) for i in rng.integers(0, len(pool), size=257)]
+        ks = [pool[i] for i in idx] + ([new_keys[1]] if r else [keys[10]])  # keys only this tree holds
+        vs = [b"b%d-%d" % (r, j) for j in range(len(ks))]
+        bk, bo = pack(ks)
+        bv, bvo = pack(vs)
+        d = [torch.from_numpy(bk.copy()).cuda(), torch.from_numpy(bo.astype(np.int64)).cuda(),
+             torch.from_numpy(bv.copy()).cuda(), torch.from_numpy(bvo.astype(np.int64)).cuda()]
+        keep.append(d)
+        batches.append((d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), len(ks)))
+        oracles.append(o.upsert(bk, bo, bv, bvo))
+    torch.cuda.synchronize()
+    base = orig.clone()  # the pre-update original, for the batched diff
+    MerkleTree.upsert_device_many([orig, clone], batches)
+    assert orig.get_root_hash() == oracles[0].root()
+    assert clone.get_root_hash() == oracles[1].root()
+    assert _levels(clone) == _oracle_levels(oracles[1])
+    got = base.diff_keys_many_packed([orig, clone])
+    for (raw, offs), o in zip(got, oracles):
+        b, oo = raw.tobytes(), offs.tolist()
+        assert [b[oo[j]:oo[j + 1]] for j in range(len(oo) - 1)] == o_orig.diff(o)
