@@ -415,6 +415,54 @@ def shared_prefix_block(ctx, n, steps=5, warmup=2, prefix=b"tenant/0001/object/"
     return out
 
 
+def ragged_block(ctx, n, fixed_leaf_ms, steps=5, warmup=2, klen=64, vlen=256):
+    """Store-like ragged records: keys 8-64 B, values 16-256 B, packed back to back (every
+    record at an arbitrary byte offset), the oracle's gen_records(ragged=2). The default build over them;
+    the leaf-hash stage (k_leaf_direct's listing pass + bucketing + k_leaf_ragged) in SHA compressions/s
+    next to the fixed 32/100-B shape's (3 compressions per leaf, same build, same co-running sort)."""
+    torch = ctx.torch
+    import numpy as np
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.merkle import gen_records_ragged_device
+    kb = torch.empty(n * klen + 64, dtype=torch.uint8, device=ctx.dev)
+    vb = torch.empty(n * vlen + 64, dtype=torch.uint8, device=ctx.dev)
+    ko = torch.empty(n + 1, dtype=torch.int64, device=ctx.dev)
+    vo = torch.empty(n + 1, dtype=torch.int64, device=ctx.dev)
+    gen_records_ragged_device(ctx.local, SEED, 0, n, klen, vlen, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
+                              vo.data_ptr())
+    torch.cuda.synchronize()
+    L = 8 + (ko[1:] - ko[:-1]) + (vo[1:] - vo[:-1])
+    comp = int(((L + 9 + 63) // 64).sum().item())
+    lsum = int(L.sum().item())
+    t = MerkleTree(ctx.local)
+    for _ in range(warmup):
+        t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+    t.prof_enable(True)
+    t.prof_reset()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+        root = t.get_root_hash()
+    el = time.perf_counter() - t0
+    lm, lc = t.prof_read("leaf_hash")
+    leaf_ms = lm / max(lc, 1)
+    t.prof_enable(False)
+    fixed_cps = 3 * 10_000_000 / (fixed_leaf_ms * 1e-3) if fixed_leaf_ms else None
+    cps = comp / (leaf_ms * 1e-3)
+    out = {"keys": n, "key_bytes": f"{klen // 8}-{klen}", "value_bytes": f"{vlen // 16}-{vlen}",
+           "mean_record_bytes": lsum / n - 8, "compressions": comp, "ms_per_step": el / steps * 1e3,
+           "leaves_per_s": n * steps / el, "leaf_hash_ms": leaf_ms, "compressions_per_s": cps,
+           "gb_per_s_hashed": lsum / (leaf_ms * 1e-3) / 1e9,
+           "fixed_shape_compressions_per_s": fixed_cps,
+           "ratio_vs_fixed": cps / fixed_cps if fixed_cps else None, "root": root.hex(),
+           "note": "leaf_hash_ms = the whole leaf stage of the build (listing pass, bucketing by block count, "
+                   "k_leaf_ragged) while the ordering kernels co-run, HIP events on the tree's stream"}
+    del t, kb, vb, ko, vo
+    torch.cuda.empty_cache()
+    return out
+
+
 def configs0_block(ctx, reps=5):
     """BASELINE configs[0] on the GPU: 100K-key tree A, replica B with 1 % 80/10/10 events, host blobs
     (what a server snapshot hands over): build A, build B, diff."""
@@ -516,7 +564,7 @@ def wl_build(ctx, args):
                     v[2] / max(v[1], 1)} for k, v in coll_stats.items()}
 
     # ---------------- secondary, 1 GPU only ----------------
-    diff_info = upd_info = d100 = anchor = c0 = shared = dN = None
+    diff_info = upd_info = d100 = anchor = c0 = shared = dN = ragged = None
     if not args.no_diff and ctx.world == 1:
         diff_info = diff_secondary(ctx, tree, kb, ko, vb, vo, n)
         upd_info = incremental_secondary(ctx, tree, kb, ko, vb, vo, n)
@@ -529,6 +577,7 @@ def wl_build(ctx, args):
     if not args.no_diff and ctx.world == 1:
         c0 = configs0_block(ctx)
         shared = shared_prefix_block(ctx, n)
+        ragged = ragged_block(ctx, n, leaf_avg_ms if n == 10_000_000 else None)
         d100 = diff_modes(ctx, args.diff_records, steps=5, warmup=2)
         torch.cuda.empty_cache()
         if args.anchor_records:
@@ -558,6 +607,7 @@ def wl_build(ctx, args):
         out["anchor_125m"] = anchor
         out["configs0_gpu"] = c0
         out["shared_prefix_10m"] = shared
+        out["ragged_10m"] = ragged
         if ctx.dist is not None:
             out["diff_sharded"] = dN
             out["collectives_build"] = coll

@@ -214,6 +214,12 @@ mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms,
 mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,
                                   uint32_t vlen, uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb,
                                   uint64_t *koff, uint8_t *vb, uint64_t *voff);
+/* Ragged ("store-like") synthetic records for benches / tests: keys of [max(1, klen/8), klen] bytes and
+ * values of [vlen/16, vlen] bytes, packed back to back (records start at arbitrary byte offsets); the same
+ * definition as the oracle's orc_gen_records(ragged = 2). kb >= n*klen, vb >= n*vlen bytes. */
+mkv_status mkv_gen_records_ragged_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,
+                                         uint32_t vlen, uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb,
+                                         uint64_t *koff, uint8_t *vb, uint64_t *voff);
 /* Leaf digests only (Kernel A) over host records; out = n*32 bytes. */
 mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint8_t *out);
 /* Pinned key-list pool (results of diff / leaves / keys_at live in pinned host blocks recycled through

@@ -57,7 +57,45 @@ __global__ void k_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t
     gen_field(seed, idx0 + i, vfield, vlen, 0, 1, vb + i * vlen);
 }
 
+// Ragged mode 2 of orc_gen_records ("store-like"): keys of [max(1, klen/8), klen] bytes, values of
+// [vlen/16, vlen] bytes, packed back to back (so every record starts at an arbitrary byte offset).
+// Pass 1 writes the lengths into koff[i] / voff[i] (scanned in place by the host side), pass 2 fills.
+__global__ void k_gen_ragged_lens(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen,
+                                  uint64_t *koff, uint64_t *voff) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t kmin = klen / 8 ? klen / 8 : 1, vmin = vlen / 16;
+    koff[i] = kmin + gen_word(seed, idx0 + i, 62, 0) % (klen - kmin + 1);
+    voff[i] = vmin + gen_word(seed, idx0 + i, 62, 1) % (vlen - vmin + 1);
+}
+
+__global__ void k_gen_ragged_fill(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t shard, uint32_t nshards,
+                                  uint32_t vfield, uint8_t *kb, const uint64_t *koff, uint8_t *vb,
+                                  const uint64_t *voff) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    gen_field(seed, idx0 + i, 0, (uint32_t)(koff[i + 1] - koff[i]), shard, nshards, kb + koff[i]);
+    gen_field(seed, idx0 + i, vfield, (uint32_t)(voff[i + 1] - voff[i]), 0, 1, vb + voff[i]);
+}
+
 }  // namespace
+
+void launch_gen_records_ragged(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
+                               uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb,
+                               uint64_t *voff, void *scan_scratch, hipStream_t st) {
+    if (n) {
+        hipLaunchKernelGGL(k_gen_ragged_lens, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, seed, idx0, n, klen,
+                           vlen, koff, voff);
+        MKV_LAUNCH_CHECK();
+    }
+    exclusive_scan_u64(koff, koff, n, koff + n, scan_scratch, st);
+    exclusive_scan_u64(voff, voff, n, voff + n, scan_scratch, st);
+    if (n) {
+        hipLaunchKernelGGL(k_gen_ragged_fill, dim3((uint32_t)ceil_div(n, 256)), dim3(256), 0, st, seed, idx0, n, shard,
+                           nshards, vfield, kb, koff, vb, voff);
+        MKV_LAUNCH_CHECK();
+    }
+}
 
 void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
                         uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb, uint64_t *voff,

@@ -745,6 +745,215 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ragged records (round 3): the chunks k_leaf_direct lists (any key / value lengths, any byte
+// alignment) — the shape of a real store snapshot (sync.rs:109-115 hashes arbitrary &str pairs).
+//
+// A 64-lane wave only computes at full width when its 64 records need the same number of SHA blocks,
+// so the listed records are first bucketed by block count (class = min(blocks, 32) - 1): a per-
+// workgroup LDS histogram (k_ragged_count), one exclusive scan of the class-major (class, workgroup)
+// counts, and a scatter of record ids into class order (k_ragged_scatter; LDS cursors, no global
+// atomics). k_leaf_ragged then hands out 64-entry chunks of that list: within a chunk every lane runs
+// the same number of compressions.
+//
+// Per lane the padded encoding (R1 + SHA padding) is materialised as big-endian words in the wave's
+// private LDS region, three blocks (48 words) at a time: all the byte shifting happens once per message
+// word on the way in — one v_perm_b32 extracts (and byte-swaps) a word at any byte offset from two
+// aligned source dwords — instead of per-word region tests in the compression loop:
+//   words 1 .. ceil(k/4)      key bytes (the key starts word-aligned, at stream byte 4);
+//   words b1+1 .. b3          value bytes shifted by c = k & 3 (b1 = (4+k)/4, b3 = L/4);
+//   then three read-modify-writes fix the only words that mix fields: b1 (key tail | vlen head),
+//   b1+1 (vlen tail | value head) and b3 (value tail | 0x80); word 0 = klen, the last word = 8L, and
+//   everything else was zero-filled first.
+// Layout: quad q (words 4q..4q+3) of lane l at uint4 index q * 64 + l: the b32 writes of 64 lanes hit
+// 32 different banks per half-wave whatever each lane's word index, and the hash reads whole quads.
+// The source loads are aligned dwords (16 B at a time), kept inside [floor4(first byte), ceil4(last
+// byte)) of each blob so that reading past a record never leaves the blob's pages.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t RG_CLASSES = 32;
+constexpr uint32_t RG_WIN = 3;                   // blocks materialised per window
+constexpr uint32_t RG_WQ = 4 * RG_WIN;           // uint4 quads per lane per window
+constexpr int RG_WAVES = 4;
+constexpr uint32_t RG_CHUNKS_PER_WG = 16;        // listed chunks per workgroup in the bucketing passes
+
+__device__ __forceinline__ uint32_t rg_class(uint64_t klen, uint64_t vlen) {
+    const uint64_t nb = (8 + klen + vlen + 9 + 63) >> 6;
+    return nb >= RG_CLASSES ? RG_CLASSES - 1 : (uint32_t)nb - 1;
+}
+
+__global__ __launch_bounds__(256) void k_ragged_count(const uint64_t *__restrict__ koff,
+                                                     const uint64_t *__restrict__ voff, uint64_t n,
+                                                     const uint32_t *__restrict__ ctr, uint64_t *__restrict__ wcnt,
+                                                     uint32_t nwg) {
+    __shared__ uint32_t h[RG_CLASSES];
+    if (threadIdx.x < RG_CLASSES) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t listed = ctr[1];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
+        const uint64_t e = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
+        if (e >= listed) break;  // uniform per wave
+        const uint64_t r = (uint64_t)ctr[4 + e] * 64 + lane;
+        if (r < n) atomicAdd(&h[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < RG_CLASSES) wcnt[(uint64_t)threadIdx.x * nwg + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_ragged_scatter(const uint64_t *__restrict__ koff,
+                                                       const uint64_t *__restrict__ voff, uint64_t n,
+                                                       const uint32_t *__restrict__ ctr,
+                                                       const uint64_t *__restrict__ wbase, uint32_t nwg,
+                                                       uint32_t *__restrict__ list) {
+    __shared__ uint32_t cur[RG_CLASSES];
+    if (threadIdx.x < RG_CLASSES) cur[threadIdx.x] = (uint32_t)wbase[(uint64_t)threadIdx.x * nwg + blockIdx.x];
+    __syncthreads();
+    const uint32_t listed = ctr[1];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
+        const uint64_t e = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
+        if (e >= listed) break;
+        const uint64_t r = (uint64_t)ctr[4 + e] * 64 + lane;
+        if (r < n) list[atomicAdd(&cur[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u)] = (uint32_t)r;
+    }
+}
+
+typedef uint32_t rg_u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Four aligned dwords at a (4-B aligned), zero where a dword is outside [lo, hi).
+__device__ __forceinline__ rg_u32x4 rg_load4(const uint8_t *a, const uint8_t *lo, const uint8_t *hi) {
+    if (a >= lo && a + 16 <= hi) return *reinterpret_cast<const rg_u32x4 *>(a);
+    rg_u32x4 r = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (a + 4 * j >= lo && a + 4 * j + 4 <= hi) r[j] = reinterpret_cast<const uint32_t *>(a)[j];
+    return r;
+}
+__device__ __forceinline__ uint32_t rg_load1(const uint8_t *a, const uint8_t *lo, const uint8_t *hi) {
+    return (a >= lo && a + 4 <= hi) ? *reinterpret_cast<const uint32_t *>(a) : 0u;
+}
+// big-endian word of the 4 bytes at byte offset s (0..3) of the little-endian pair (lo, hi)
+__device__ __forceinline__ uint32_t rg_be(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+__device__ __forceinline__ uint32_t rg_head_mask(uint32_t nbytes) {  // first nbytes (0..3) of a BE word
+    return nbytes ? ~(0xFFFFFFFFu >> (8 * nbytes)) : 0u;
+}
+
+// Words [w0, w1] of a field that starts at stream word fw: stream word w = BE word of the source bytes
+// at (src + 4 (w - fw)); written into the lane's window (window-relative word u = w - W0).
+__device__ __forceinline__ void rg_copy_words(uint32_t *lw, uint32_t lane, uint32_t W0, uint32_t w0, uint32_t w1,
+                                              uint32_t fw, const uint8_t *src, const uint8_t *lo,
+                                              const uint8_t *hi) {
+    const uint8_t *A = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
+    const uint32_t sel = 0x00010203u + (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3) * 0x01010101u;
+    for (uint32_t w = w0; w <= w1; w += 4) {
+        const uint8_t *a = A + 4 * (w - fw);
+        const rg_u32x4 d = rg_load4(a, lo, hi);
+        const uint32_t d4 = rg_load1(a + 16, lo, hi);
+        const uint32_t x[4] = {rg_be(d.y, d.x, sel), rg_be(d.z, d.y, sel), rg_be(d.w, d.z, sel), rg_be(d4, d.w, sel)};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t u = w + j - W0;
+            if (w + j <= w1) lw[((u >> 2) * 64 + lane) * 4 + (u & 3)] = x[j];
+        }
+    }
+}
+
+template <bool SHORT>
+__global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__restrict__ kb,
+                                                              const uint64_t *__restrict__ koff,
+                                                              const uint8_t *__restrict__ vb,
+                                                              const uint64_t *__restrict__ voff, uint64_t n,
+                                                              uint8_t *__restrict__ out,
+                                                              const uint32_t *__restrict__ list,
+                                                              const uint64_t *__restrict__ total,
+                                                              uint32_t *__restrict__ gctr, uint32_t grain) {
+    __shared__ __attribute__((aligned(16))) uint4 lds_all[RG_WAVES * RG_WQ * 64];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint4 *lq = lds_all + wave * (RG_WQ * 64);
+    uint32_t *lw = reinterpret_cast<uint32_t *>(lq);
+    // the blobs' byte ranges, rounded out to whole dwords: no source load leaves them
+    const uint8_t *klo = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(kb + koff[0]) & ~uintptr_t(3));
+    const uint8_t *khi =
+        reinterpret_cast<const uint8_t *>((reinterpret_cast<uintptr_t>(kb + koff[n]) + 3) & ~uintptr_t(3));
+    const uint8_t *vlo = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(vb + voff[0]) & ~uintptr_t(3));
+    const uint8_t *vhi =
+        reinterpret_cast<const uint8_t *>((reinterpret_cast<uintptr_t>(vb + voff[n]) + 3) & ~uintptr_t(3));
+    const uint64_t T = *total;
+    const uint64_t nch = (T + 63) / 64;
+    ChunkSource<true> src{0, 0, 0, gctr, grain};
+    for (uint64_t c = src.get(lane); c < nch; c = src.get(lane)) {
+        const uint64_t p = c * 64 + lane;
+        const bool valid = p < T;
+        const uint32_t r = valid ? list[p] : 0u;
+        uint64_t k0 = 0, k1 = 0, v0 = 0, v1 = 0;
+        if (valid) {
+            k0 = koff[r];
+            k1 = koff[r + 1];
+            v0 = voff[r];
+            v1 = voff[r + 1];
+        }
+        const uint32_t k = (uint32_t)(k1 - k0), v = (uint32_t)(v1 - v0);
+        const uint32_t L = 8 + k + v;
+        const uint32_t nb = valid ? (L + 9 + 63) >> 6 : 0u;
+        const uint32_t W = 16 * nb;                     // message words
+        const uint32_t b1 = (4 + k) >> 2, c4 = k & 3;   // key ends in word b1; value shift c4
+        const uint32_t b3 = L >> 2, e4 = L & 3;         // value ends / 0x80 in word b3
+        const uint32_t nk = (k + 3) >> 2;               // key words 1..nk
+        const uint8_t *kp = kb + k0, *vp = vb + v0;
+        uint32_t st[8];
+        sha_init(st);
+        for (uint32_t win = 0; __any(win * RG_WIN < nb); ++win) {
+            const uint32_t blo = win * RG_WIN;
+            const uint32_t nbw = blo < nb ? min(RG_WIN, nb - blo) : 0u;  // this lane's blocks in the window
+            const uint32_t W0 = 16 * blo, W1 = W0 + 16 * nbw;            // words [W0, W1)
+            for (uint32_t q = 0; q < 4 * nbw; ++q) lq[q * 64 + lane] = make_uint4(0, 0, 0, 0);
+            if (nbw) {
+                const uint32_t kw0 = max(1u, W0), kw1 = min(nk, W1 - 1);
+                if (kw0 <= kw1) rg_copy_words(lw, lane, W0, kw0, kw1, 1, kp, klo, khi);
+                const uint32_t vw0 = max(b1 + 1, W0), vw1 = min(b3, W1 - 1);
+                if (vw0 <= vw1) rg_copy_words(lw, lane, W0, vw0, vw1, b1 + 1, vp - c4, vlo, vhi);
+                // the words that mix fields (read-modify-write, in this order)
+                const uint32_t hc = rg_head_mask(c4);
+                auto at = [&](uint32_t w) -> uint32_t & {
+                    const uint32_t u = w - W0;
+                    return lw[((u >> 2) * 64 + lane) * 4 + (u & 3)];
+                };
+                if (W0 == 0) at(0) = k;
+                if (b1 >= W0 && b1 < W1) {
+                    uint32_t &x = at(b1);
+                    x = (x & hc) | (v >> (8 * c4));
+                }
+                if (b1 + 1 >= W0 && b1 + 1 < W1) {
+                    uint32_t &x = at(b1 + 1);
+                    x = ((c4 ? v << (32 - 8 * c4) : 0u) & hc) | (x & ~hc);
+                }
+                if (b3 >= W0 && b3 < W1) {
+                    uint32_t &x = at(b3);
+                    const uint32_t he = rg_head_mask(e4);
+                    x = (x & he) | (0x80000000u >> (8 * e4));
+                }
+                if (W - 1 >= W0 && W - 1 < W1) at(W - 1) = L * 8;  // bit length (high word stays 0)
+            }
+            for (uint32_t b = 0; b < nbw; ++b) {
+                uint32_t w[16];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint4 x = lq[(4 * b + j) * 64 + lane];
+                    w[4 * j] = x.x;
+                    w[4 * j + 1] = x.y;
+                    w[4 * j + 2] = x.z;
+                    w[4 * j + 3] = x.w;
+                }
+                sha_compress<SHORT>(st, w);
+            }
+        }
+        if (valid) store_digest(out + 32 * (uint64_t)r, st);
+    }
+}
+
 }  // namespace
 
 void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uint8_t *out, hipStream_t st) {
@@ -757,7 +966,75 @@ void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uin
     MKV_LAUNCH_CHECK();
 }
 
-size_t leaf_ctr_words(uint64_t n) { return 4 + (size_t)((n + 63) / 64); }
+// The counter block (leaf_ctr_words): [0] k_leaf_direct's chunk counter, [1] listed chunks, [2]
+// k_leaf_ragged's chunk counter, [3] spare, [4 ..) listed chunk ids; then, 16-B aligned, the ragged
+// bucketing scratch: class-major per-workgroup counts (u64), their scan scratch, the list total (u64)
+// and the class-ordered record list (u32 per record).
+struct RaggedScratch {
+    uint64_t *wcnt;
+    void *scan;
+    uint64_t *total;
+    uint32_t *list;
+    uint32_t nwg;
+};
+static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+static RaggedScratch ragged_scratch(uint32_t *ctr, uint64_t n, size_t *bytes_out = nullptr) {
+    const uint64_t nch = (n + 63) / 64;
+    const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(nch, RG_CHUNKS_PER_WG));
+    const uint64_t m = (uint64_t)RG_CLASSES * nwg;
+    size_t off = align16(4 * (4 + (size_t)nch));
+    RaggedScratch R;
+    uint8_t *base = reinterpret_cast<uint8_t *>(ctr);
+    R.wcnt = reinterpret_cast<uint64_t *>(base + off);
+    off = align16(off + 8 * m);
+    R.scan = base + off;
+    off = align16(off + scan_scratch_bytes(m));
+    R.total = reinterpret_cast<uint64_t *>(base + off);
+    off = align16(off + 8);
+    R.list = reinterpret_cast<uint32_t *>(base + off);
+    off = align16(off + 4 * (size_t)n);
+    R.nwg = nwg;
+    if (bytes_out) *bytes_out = off;
+    return R;
+}
+
+size_t leaf_ctr_words(uint64_t n) {
+    size_t bytes = 0;
+    (void)ragged_scratch(nullptr, n, &bytes);
+    return bytes / 4 + 4;
+}
+
+// MKV_LEAF_RAGGED (A/B knob): 1 (default) = listed chunks go through the bucketed ragged kernel, 0 = the
+// round-2 LDS chunk kernel k_leaf_list.
+static int leaf_ragged_enabled() {
+    static const int v = [] {
+        const char *e = getenv("MKV_LEAF_RAGGED");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
+// The listed chunks of ctr (k_leaf_direct): bucket their records by block count, then hash them.
+template <bool SHORT>
+static void launch_ragged_stage(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff,
+                                uint64_t n, uint8_t *out, uint32_t *ctr, hipStream_t st) {
+    static int cus = [] {
+        int dev = 0, c = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+        return c > 0 ? c : 256;
+    }();
+    const RaggedScratch R = ragged_scratch(ctr, n);
+    const uint64_t m = (uint64_t)RG_CLASSES * R.nwg;
+    hipLaunchKernelGGL(k_ragged_count, dim3(R.nwg), dim3(256), 0, st, koff, voff, n, ctr, R.wcnt, R.nwg);
+    exclusive_scan_u64(R.wcnt, R.wcnt, m, R.total, R.scan, st);
+    hipLaunchKernelGGL(k_ragged_scatter, dim3(R.nwg), dim3(256), 0, st, koff, voff, n, ctr, R.wcnt, R.nwg, R.list);
+    // 48 KiB of LDS per workgroup: three per CU
+    const uint64_t grid = std::min<uint64_t>((uint64_t)cus * 3, ceil_div(ceil_div(n, 64), RG_WAVES));
+    hipLaunchKernelGGL(k_leaf_ragged<SHORT>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
+                       kb, koff, vb, voff, n, out, R.list, R.total, ctr + 2, 2u);
+    MKV_LAUNCH_CHECK();
+}
 
 // SHA round form of k_leaf_direct (MKV_LEAF_SHA, default 0 = plain association, fewer instructions):
 // with the LDS-free kernel the short-chain form (1) measured slower (leaf 1.38 vs 1.32 ms beside the sort)
@@ -812,17 +1089,23 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
         const uint32_t grain = std::max<uint32_t>(leaf_dyn_grain(), 1u);
         // the span copy of listed chunks rounds to 16 B like the staged paths: kb must be 16-B aligned
         const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
-        MKV_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), st));
+        MKV_HIP(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), st));
         if (leaf_sha_variant() == 0) {
             hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
                                koff, vb, voff, n, out, ctr, grain, KO);
-            hipLaunchKernelGGL(k_leaf_list<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb,
-                               voff, n, out, ctr);
+            if (leaf_ragged_enabled())
+                launch_ragged_stage<false>(kb, koff, vb, voff, n, out, ctr, st);
+            else
+                hipLaunchKernelGGL(k_leaf_list<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                                   vb, voff, n, out, ctr);
         } else {
             hipLaunchKernelGGL((k_leaf_direct<true, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
                                koff, vb, voff, n, out, ctr, grain, KO);
-            hipLaunchKernelGGL(k_leaf_list<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff, vb,
-                               voff, n, out, ctr);
+            if (leaf_ragged_enabled())
+                launch_ragged_stage<true>(kb, koff, vb, voff, n, out, ctr, st);
+            else
+                hipLaunchKernelGGL(k_leaf_list<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                                   vb, voff, n, out, ctr);
         }
         MKV_LAUNCH_CHECK();
         return KO.kdst != nullptr;

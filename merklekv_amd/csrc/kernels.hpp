@@ -313,6 +313,11 @@ void launch_route_lens(const uint32_t *perm, const uint64_t *off, uint64_t n, ui
 void launch_u32_to_u64(const uint32_t *in, uint64_t n, uint64_t *out, hipStream_t st);
 
 // ---- synthetic generator (k_gen.hip) — bench/test utility, not part of the reference API ----
+// Ragged mode 2 of orc_gen_records (keys [klen/8, klen], values [vlen/16, vlen], packed); scan_scratch =
+// scan_scratch_bytes(n) bytes.
+void launch_gen_records_ragged(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
+                               uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb,
+                               uint64_t *voff, void *scan_scratch, hipStream_t st);
 void launch_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, uint32_t shard,
                         uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb, uint64_t *voff,
                         hipStream_t st);

@@ -3072,6 +3072,28 @@ mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, 
     });
 }
 
+mkv_status mkv_gen_records_ragged_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,
+                                         uint32_t vlen, uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb,
+                                         uint64_t *koff, uint8_t *vb, uint64_t *voff) {
+    MKV_TRY({
+        NEED(kb && koff && vb && voff, "null buffer");
+        NEED(nshards >= 1 && nshards <= 64 && shard < nshards, "bad shard spec");
+        NEED(klen >= 1, "klen must be >= 1");
+        DevGuard g(hip_device);
+        void *scratch = nullptr;
+        MKV_HIP(hipMalloc(&scratch, scan_scratch_bytes(n + 1) + 256));
+        try {
+            launch_gen_records_ragged(seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb, voff, scratch,
+                                      nullptr);
+            MKV_HIP(hipDeviceSynchronize());
+        } catch (...) {
+            (void)hipFree(scratch);
+            throw;
+        }
+        MKV_HIP(hipFree(scratch));
+    });
+}
+
 mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint8_t *out) {
     MKV_TRY({
         NEED(out || keys.n == 0, "null out");

@@ -658,6 +658,14 @@ def gen_records_device(device: int, seed: int, idx0: int, n: int, klen: int, vle
                                        voff))
 
 
+def gen_records_ragged_device(device: int, seed: int, idx0: int, n: int, klen: int, vlen: int, kb: int, koff: int,
+                              vb: int, voff: int, shard: int = 0, nshards: int = 1, vfield: int = 1) -> None:
+    """Store-like ragged records (keys [klen/8, klen] B, values [vlen/16, vlen] B, packed): the oracle's
+    gen_records(..., ragged=2). kb >= n*klen, vb >= n*vlen bytes; koff/voff n + 1 entries."""
+    check(lib().mkv_gen_records_ragged_device(device, seed, idx0, n, klen, vlen, shard, nshards, vfield, kb, koff, vb,
+                                              voff))
+
+
 def route_splitters(samples, world: int) -> np.ndarray:
     """world-1 splitters (uint64) from every rank's prefix samples (mkv_route_splitters, host only)."""
     smp = np.ascontiguousarray(samples, dtype=np.uint64)

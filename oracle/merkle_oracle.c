@@ -515,9 +515,13 @@ void orc_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, ui
     for (uint64_t i = 0; i < n; ++i) {
         uint64_t idx = idx0 + i;
         uint32_t kl = klen, vl = vlen;
-        if (ragged) {
+        if (ragged == 1) {
             kl = 1 + (uint32_t)(orc_gen_word(seed, idx, 62, 0) % klen);
             vl = (uint32_t)(orc_gen_word(seed, idx, 62, 1) % (vlen + 1));
+        } else if (ragged == 2) {  /* "store-like" ragged: keys [klen/8, klen], values [vlen/16, vlen] */
+            const uint32_t kmin = klen / 8 ? klen / 8 : 1, vmin = vlen / 16;
+            kl = kmin + (uint32_t)(orc_gen_word(seed, idx, 62, 0) % (klen - kmin + 1));
+            vl = vmin + (uint32_t)(orc_gen_word(seed, idx, 62, 1) % (vlen - vmin + 1));
         }
         koff[i] = ko;
         voff[i] = vo;

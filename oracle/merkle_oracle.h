@@ -75,7 +75,8 @@ void orc_free(void *p);
  * to shard g of G (G | 64) so shards are contiguous key ranges. */
 uint64_t orc_gen_word(uint64_t seed, uint64_t idx, uint32_t field, uint32_t j);
 /* Generate records idx in [idx0, idx0+n) (fields: key 0, value `vfield`). Fixed lengths klen/vlen;
- * if ragged != 0, klen = 1 + w%klen, vlen = w'%(vlen+1) per record. Buffers: kb >= n*klen, vb >= n*vlen. */
+ * ragged == 1: klen = 1 + w%klen, vlen = w'%(vlen+1) per record; ragged == 2 ("store-like"): klen in
+ * [max(1, klen/8), klen], vlen in [vlen/16, vlen]. Buffers: kb >= n*klen, vb >= n*vlen. */
 void orc_gen_records(uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen, uint32_t vlen, int ragged,
                      uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb, uint64_t *koff, uint8_t *vb,
                      uint64_t *voff);

@@ -131,7 +131,11 @@ def gen_records(seed: int, idx0: int, n: int, klen: int = 32, vlen: int = 100, r
     """Vectorised twin of orc_gen_records: returns (kb, koff, vb, voff) numpy arrays."""
     alpha = np.frombuffer(SORTED_ALPHA, dtype=np.uint8)
     idx = np.arange(idx0, idx0 + n, dtype=np.uint64)
-    if ragged:
+    if ragged == 2:  # store-like ragged: keys [klen/8, klen], values [vlen/16, vlen] (orc_gen_records mode 2)
+        kmin, vmin = max(1, klen // 8), vlen // 16
+        kl = (kmin + gen_word_np(seed, idx, 62, 0) % np.uint64(klen - kmin + 1)).astype(np.int64)
+        vl = (vmin + gen_word_np(seed, idx, 62, 1) % np.uint64(vlen - vmin + 1)).astype(np.int64)
+    elif ragged:
         kl = (1 + gen_word_np(seed, idx, 62, 0) % np.uint64(klen)).astype(np.int64)
         vl = (gen_word_np(seed, idx, 62, 1) % np.uint64(vlen + 1)).astype(np.int64)
     else:

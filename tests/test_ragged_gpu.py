@@ -1,0 +1,142 @@
+"""Ragged records: the bucketed LDS-materialising leaf kernel (k_leaf_ragged) against
+the C oracle — store-like key / value lengths at arbitrary byte offsets, every padding / window / class
+edge, blob bases at every byte alignment, and records far larger than one window.
+Reference inputs are arbitrary &str pairs (/root/reference/src/store/merkle.rs:7-16, :45-49;
+/root/reference/src/sync.rs:109-115)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from merklekv_amd import MerkleTree, leaf_digests  # noqa: E402
+from oracle import coracle  # noqa: E402
+from oracle.merkle_oracle import DEFAULT_SEED, pack  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _free_torch_cache():
+    yield
+    import gc
+
+    import torch
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def _enc_digest(k: bytes, v: bytes) -> bytes:
+    return hashlib.sha256(len(k).to_bytes(4, "big") + k + len(v).to_bytes(4, "big") + v).digest()
+
+
+def test_ragged_store_like_1m_vs_oracle():
+    """1M records, keys 8-64 B, values 16-256 B, packed (unaligned offsets): root and every leaf digest
+    (level 0, in key order) equal the oracle's."""
+    n = 1_000_000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n, klen=64, vlen=256, ragged=2)
+    shani = coracle.set_backend(1)
+    try:
+        o = coracle.OracleTree.build(kb, ko, vb, vo)
+    finally:
+        coracle.set_backend(0)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    assert t.get_root_hash() == o.root()
+    assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
+    assert shani in (0, 1)
+
+
+def test_ragged_device_generator_matches_oracle():
+    import torch
+
+    from merklekv_amd.merkle import gen_records_ragged_device
+    n = 100_003
+    want = coracle.gen_records(DEFAULT_SEED, 7, n, klen=64, vlen=256, ragged=2, shard=3, nshards=8)
+    kb = torch.empty(n * 64, dtype=torch.uint8, device="cuda")
+    vb = torch.empty(n * 256, dtype=torch.uint8, device="cuda")
+    ko = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    vo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    gen_records_ragged_device(0, DEFAULT_SEED, 7, n, 64, 256, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
+                              vo.data_ptr(), shard=3, nshards=8)
+    gk, gv = ko.cpu().numpy().astype(np.uint64), vo.cpu().numpy().astype(np.uint64)
+    assert np.array_equal(gk, want[1]) and np.array_equal(gv, want[3])
+    assert np.array_equal(kb[: int(gk[-1])].cpu().numpy(), want[0])
+    assert np.array_equal(vb[: int(gv[-1])].cpu().numpy(), want[2])
+
+
+def _edge_records(rng):
+    """Lengths at every field / padding / window / class edge: total encodings L = 8 + k + v around
+    55/56 (1 -> 2 blocks), 183/184 (3 -> 4 blocks: the window edge), 375/376 (6 -> 7), 1975 (31 blocks),
+    1976+ (class 31 = 32 blocks and more), with every key length mod 4."""
+    keys, vals = [], []
+    for Lt in (8, 9, 12, 54, 55, 56, 57, 63, 64, 119, 120, 183, 184, 185, 247, 248, 375, 376, 377, 1975, 1976, 1977,
+               2100, 5000):
+        for k in (0, 1, 2, 3, 4, 5, 7, 31, 32, 33, 63, 64, 65, 200):
+            v = Lt - 8 - k
+            if v < 0:
+                continue
+            keys.append(rng.integers(0, 256, size=k, dtype=np.uint8).tobytes())
+            vals.append(rng.integers(0, 256, size=v, dtype=np.uint8).tobytes())
+    return keys, vals
+
+
+def test_ragged_window_and_class_edges_vs_hashlib():
+    rng = np.random.default_rng(11)
+    keys, vals = _edge_records(rng)
+    # shuffled, so that 64-record chunks mix classes before the bucketing
+    order = rng.permutation(len(keys))
+    keys = [keys[i] for i in order]
+    vals = [vals[i] for i in order]
+    got = leaf_digests(keys, vals)
+    for k, v, g in zip(keys, vals, got):
+        assert g == _enc_digest(k, v), (len(k), len(v))
+
+
+@pytest.mark.parametrize("kshift,vshift", [(0, 0), (1, 3), (2, 1), (3, 2)])
+def test_ragged_device_blobs_at_every_alignment(kshift, vshift):
+    """build_device from blobs whose base pointers sit 0-3 bytes past an allocation start (the loads
+    clamp to the blob's own byte range): root and leaves equal the oracle's."""
+    import torch
+    rng = np.random.default_rng(100 + kshift)
+    n = 5_000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n, klen=64, vlen=256, ragged=2)
+    ek, ev = _edge_records(rng)
+    keys = [kb[int(ko[i]):int(ko[i + 1])].tobytes() for i in range(n)] + ek
+    vals = [vb[int(vo[i]):int(vo[i + 1])].tobytes() for i in range(n)] + ev
+    (pk, pko), (pv, pvo) = pack(keys), pack(vals)
+    o = coracle.OracleTree.build(pk, pko, pv, pvo)
+    dk = torch.zeros(len(pk) + kshift, dtype=torch.uint8, device="cuda")
+    dv = torch.zeros(len(pv) + vshift, dtype=torch.uint8, device="cuda")
+    dk[kshift:] = torch.from_numpy(pk.copy()).cuda()
+    dv[vshift:] = torch.from_numpy(pv.copy()).cuda()
+    dko = torch.from_numpy(pko.astype(np.int64)).cuda()
+    dvo = torch.from_numpy(pvo.astype(np.int64)).cuda()
+    torch.cuda.synchronize()
+    t = MerkleTree()
+    t.build_device(dk.data_ptr() + kshift, dko.data_ptr(), dv.data_ptr() + vshift, dvo.data_ptr(), len(keys))
+    assert t.get_root_hash() == o.root()
+    assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
+
+
+def test_ragged_mixed_with_fixed_chunks_and_duplicates():
+    """Fixed-shape chunks (32 / 100 B, k_leaf_direct) interleaved with ragged ones, duplicate keys (last
+    write wins) and empty keys / values, against the oracle."""
+    rng = np.random.default_rng(5)
+    fk, fko, fv, fvo = coracle.gen_records(DEFAULT_SEED, 0, 64 * 40)
+    rk, rko, rv, rvo = coracle.gen_records(DEFAULT_SEED, 10**6, 64 * 40, klen=64, vlen=256, ragged=2)
+    keys, vals = [], []
+    for c in range(40):
+        src = (fk, fko, fv, fvo) if c % 3 else (rk, rko, rv, rvo)
+        for i in range(64 * c, 64 * c + 64):
+            keys.append(src[0][int(src[1][i]):int(src[1][i + 1])].tobytes())
+            vals.append(src[2][int(src[3][i]):int(src[3][i + 1])].tobytes())
+    for i in rng.choice(len(keys), size=200, replace=False):
+        keys.append(keys[int(i)])
+        vals.append(b"dup" * int(rng.integers(0, 90)))
+    keys += [b"", b"e"]
+    vals += [b"x" * 77, b""]
+    o = coracle.OracleTree.from_pairs(list(zip(keys, vals)))
+    t = MerkleTree()
+    t.build(keys, vals)
+    assert t.get_root_hash() == o.root()
+    assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
