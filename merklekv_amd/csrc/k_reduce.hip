@@ -92,6 +92,124 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
     }
 }
 
+// ---- top of the tree (round 3): every level from a <= 64-tile level to the root in ONE launch ----
+// Phase 1: each workgroup fuses up to RD_TOP_FUSE levels of its 512-parent tile in LDS (the tile's
+// subtree collapses to one node after 10 levels). Phase 2: the last workgroup to finish (agent-scope
+// arrival counter; it resets the counter for the next launch) reads the <= ntiles + 2 nodes the tiles
+// produced and climbs the remaining levels alone, in LDS. One cross-workgroup hand-off instead of one
+// kernel launch (and its drain / ramp) per 4 levels: the top of a 10M-key tree was three launches of
+// ~34 us each, almost all latency (a few hundred nodes per level, 2 dependent compressions per node).
+// The short-chain SHA form (latency) is used throughout.
+constexpr int RD_TOP_FUSE = 10;
+
+__global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
+    __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
+    __shared__ uint32_t last;
+    const uint64_t t = p.tile0 + blockIdx.x;
+    const int nf = p.nf;
+    for (int k = 1; k <= nf; ++k) {
+        const uint64_t Tk = (uint64_t)RD_TILE >> (k - 1);
+        const uint32_t i = threadIdx.x;
+        const uint64_t j = t * Tk + i;
+        const bool own = i < Tk && j >= p.a[k] && j < p.a[k] + p.c[k];
+        if (own) {
+            uint32_t l[8], r[8], o[8];
+            const uint64_t c0 = 2 * j;
+            const bool pair = c0 + 1 < p.S[k - 1];
+            if (k == 1 && p.perm) {
+                const uint64_t lc = c0 - p.a[0];
+                uint4 *dst0 = reinterpret_cast<uint4 *>(const_cast<uint8_t *>(p.in) + 32 * lc);
+                const uint4 *s0 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[lc]);
+                const uint4 x0 = s0[0], y0 = s0[1];
+                uint4 x1 = make_uint4(0, 0, 0, 0), y1 = x1;
+                if (pair) {
+                    const uint4 *s1 = reinterpret_cast<const uint4 *>(p.dig + 32 * (uint64_t)p.perm[lc + 1]);
+                    x1 = s1[0];
+                    y1 = s1[1];
+                    dst0[2] = x1;
+                    dst0[3] = y1;
+                }
+                dst0[0] = x0;
+                dst0[1] = y0;
+                l[0] = bswap32(x0.x); l[1] = bswap32(x0.y); l[2] = bswap32(x0.z); l[3] = bswap32(x0.w);
+                l[4] = bswap32(y0.x); l[5] = bswap32(y0.y); l[6] = bswap32(y0.z); l[7] = bswap32(y0.w);
+                r[0] = bswap32(x1.x); r[1] = bswap32(x1.y); r[2] = bswap32(x1.z); r[3] = bswap32(x1.w);
+                r[4] = bswap32(y1.x); r[5] = bswap32(y1.y); r[6] = bswap32(y1.z); r[7] = bswap32(y1.w);
+            } else if (k == 1) {
+                const uint8_t *src = p.in + 32 * (c0 - p.a[0]);
+                load_digest(src, l);
+                if (pair) load_digest(src + 32, r);
+            } else {
+                const uint32_t *src = buf[(k - 1) & 1] + 16 * i;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    l[q] = src[q];
+                    r[q] = src[8 + q];
+                }
+            }
+            if (pair) {
+                sha_node<true>(l, r, o);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) o[q] = l[q];  // R5: promote unchanged
+            }
+            uint32_t *dst = buf[k & 1] + 8 * i;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dst[q] = o[q];
+            store_digest(p.out[k - 1] + 32 * (j - p.a[k]), o);
+        }
+        __syncthreads();
+    }
+    if (nf >= p.nl) return;
+    // ---- hand-off: the last tile to finish climbs the rest ----
+    if (p.ntiles > 1) {
+        __threadfence();  // this thread's level writes, visible device-wide before the arrival
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t prev = __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            last = prev + 1 == (uint32_t)p.ntiles;
+            if (last) __hip_atomic_store(p.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+    }
+    // level nf (owned nodes [a, a + c), c <= RD_TILE) into LDS as BE words, read coherently
+    {
+        const uint64_t cnt = p.c[nf];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(nf == 0 ? p.in : p.out[nf - 1]);
+        for (uint32_t w = threadIdx.x; w < 8 * cnt; w += RD_TILE)
+            buf[nf & 1][w] = bswap32(__hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+    __syncthreads();
+    for (int k = nf + 1; k <= p.nl; ++k) {
+        const uint32_t i = threadIdx.x;
+        const uint64_t j = p.a[k] + i;  // owned parents [a[k], a[k] + c[k]), children owned at level k-1
+        if (i < p.c[k]) {
+            uint32_t l[8], r[8], o[8];
+            const uint64_t c0 = 2 * j;
+            const bool pair = c0 + 1 < p.S[k - 1];
+            const uint32_t *src = buf[(k - 1) & 1] + 8 * (c0 - p.a[k - 1]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                l[q] = src[q];
+                r[q] = pair ? src[8 + q] : 0u;
+            }
+            if (pair) {
+                sha_node<true>(l, r, o);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) o[q] = l[q];
+            }
+            uint32_t *dst = buf[k & 1] + 8 * i;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dst[q] = o[q];
+            store_digest(p.out[k - 1] + 32 * i, o);
+        }
+        __syncthreads();
+    }
+}
+
 // ---- seam combine ----
 struct SeamEntry {
     uint32_t level;
@@ -302,6 +420,12 @@ void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
     } else {
         hipLaunchKernelGGL((k_reduce_fused<true, 512>), dim3((uint32_t)p.ntiles), dim3(512), 0, st, p);
     }
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_reduce_top(const TopPlan &p, hipStream_t st) {
+    if (p.ntiles == 0) return;
+    hipLaunchKernelGGL(k_reduce_top, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 

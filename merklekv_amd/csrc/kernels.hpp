@@ -133,6 +133,24 @@ struct FusePlan {
     const uint8_t *dig;
 };
 void launch_reduce_fused(const FusePlan &p, hipStream_t st);
+// Every remaining level in one launch (k_reduce_top): ntiles <= RD_TOP_TILES tiles of 512 parents fuse
+// nf (<= 10) levels each, then the last tile to arrive climbs levels nf+1 .. nl (<= 512 nodes at level
+// nf). arrive: a device counter that is 0 before the launch (the kernel leaves it 0 again).
+constexpr int TOP_MAX_LEVELS = 40;
+constexpr uint64_t RD_TOP_TILES = 64;
+struct TopPlan {
+    const uint8_t *in;
+    uint8_t *out[TOP_MAX_LEVELS];
+    uint64_t a[TOP_MAX_LEVELS + 1];
+    uint64_t c[TOP_MAX_LEVELS + 1];
+    uint64_t S[TOP_MAX_LEVELS + 1];
+    int nl, nf;
+    uint64_t tile0, ntiles;
+    const uint32_t *perm;
+    const uint8_t *dig;
+    uint32_t *arrive;
+};
+void launch_reduce_top(const TopPlan &p, hipStream_t st);
 
 // Seam combine for sharded trees (k_reduce.hip). entries: (level, index, digest) records sorted by
 // (level, index); see tree.cpp. Writes the root.

@@ -222,6 +222,7 @@ struct mkv_tree {
     DevBuf s_k1, s_k2, s_v1, s_v2;
     DevBuf s_tie, s_flags, s_scan, s_pos, s_pos0, s_lens;
     DevBuf s_radix, s_misc;
+    DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf leaf_ctr;  // dynamic chunk counter of the leaf hash
@@ -660,6 +661,16 @@ uint64_t total_nodes(const mkv_tree *t) {
     return s;
 }
 
+// MKV_TOP_REDUCE (A/B knob): 1 (default) = the tree's top levels in one k_reduce_top launch, 0 = the
+// round-2 per-4-level launches all the way up.
+static bool top_reduce_enabled() {
+    static const bool v = [] {
+        const char *e = getenv("MKV_TOP_REDUCE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch. Leaves whose
 // parent is not owned (at most the first and the last of a shard) are gathered directly; a plan without
 // an owned level-1 node (single leaf, or a one-leaf shard) gathers everything directly.
@@ -684,6 +695,37 @@ void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, co
         const uint64_t t0 = a1 / 512, t1 = (a1 + c1 - 1) / 512;
         const uint64_t ntiles = t1 - t0 + 1;
         const size_t remaining = L - 1 - l;
+        // the latency-bound top: every remaining level in one launch (k_reduce_top). Only the levels
+        // with owned nodes (a shard stops at its last owned level; the seam combine does the rest).
+        size_t nown = 0;
+        while (nown < remaining && t->lev_cnt[l + 1 + nown] > 0) ++nown;
+        if (ntiles <= RD_TOP_TILES && nown <= (size_t)TOP_MAX_LEVELS && top_reduce_enabled()) {
+            const bool fresh = t->rd_arrive.p == nullptr;
+            uint32_t *arrive = ens<uint32_t>(t->rd_arrive, 16);
+            if (fresh) MKV_HIP(hipMemsetAsync(arrive, 0, 64, t->st));
+            TopPlan p{};
+            p.in = nodes + 32 * t->lev_off[l];
+            p.a[0] = t->lev_base[l];
+            p.c[0] = t->lev_cnt[l];
+            p.S[0] = t->lev_S[l];
+            for (size_t k = 1; k <= nown; ++k) {
+                p.out[k - 1] = nodes + 32 * t->lev_off[l + k];
+                p.a[k] = t->lev_base[l + k];
+                p.c[k] = t->lev_cnt[l + k];
+                p.S[k] = t->lev_S[l + k];
+            }
+            p.nl = (int)nown;
+            p.nf = (int)std::min<size_t>(nown, 10);
+            p.tile0 = t0;
+            p.ntiles = ntiles;
+            if (l == 0 && gperm) {
+                p.perm = gperm;
+                p.dig = gdig;
+            }
+            p.arrive = arrive;
+            launch_reduce_top(p, t->st);
+            return;
+        }
         const size_t nl = std::min<size_t>(remaining, ntiles == 1 ? MAX_FUSE : 4);
         FusePlan p{};
         p.in = nodes + 32 * t->lev_off[l];
