@@ -354,14 +354,11 @@ __device__ __forceinline__ uint4 shfl_u4(uint4 v, int src) {
 // each output lane's 8-output word through wave ballots. A pair with equal prefixes but different
 // digests gets the full key compare; if those keys differ the tile is not aligned and the wave runs the
 // general merge instead (which is exact for any key sets).
-__global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
-                                                    uint64_t nt, uint32_t *__restrict__ packed,
-                                                    uint32_t *__restrict__ tilecnt) {
-    __shared__ uint64_t lds[4 * (WTILE + 2)];  // per-wave prefix slices for the general merge
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= nt) return;  // wave-uniform
-    const uint32_t lane = threadIdx.x & 63;
-    const TileCtx c = wave_tile(A, B, split, t);
+// One 512-output tile (the body of pass 1): aligned fast path for near-identical replicas, else the
+// general merge. Returns this lane's packed (isplit << 16) | (fromA << 8) | div; *total = the tile's
+// divergent count (wave-uniform). lp: the wave's LDS prefix slice (WTILE + 2 entries).
+__device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide &B, const TileCtx &c, uint32_t lane,
+                                              uint64_t *lp, uint32_t *total) {
     const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
     uint32_t nd = 0, pk = 0;
     bool general = true;
@@ -460,14 +457,12 @@ __global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, cons
                     ((nib & 1u) | ((nib & 2u) << 1) | ((nib & 4u) << 2) | ((nib & 8u) << 3)) << phase;
                 const uint64_t dl = (uint64_t)lane * DI;
                 if (dl < na + nb) pk = ((uint32_t)(dl / 2) << 16) | ((phase ? 0xAAu : 0x55u) << 8) | div;
-                if (lane == 0)
-                    tilecnt[t] = (uint32_t)(__popcll(dm[0]) + __popcll(dm[1]) + __popcll(dm[2]) + __popcll(dm[3]));
+                *total = (uint32_t)(__popcll(dm[0]) + __popcll(dm[1]) + __popcll(dm[2]) + __popcll(dm[3]));
             }
         }
     }
     if (general) {
         // stage the tile's prefixes in the wave's LDS slice: pa = lp[0 .. na], pb = lp[na+1 .. na+1+nb]
-        uint64_t *lp = lds + (threadIdx.x >> 6) * (WTILE + 2);
         const uint64_t tot = na + nb + 2;
 #pragma unroll
         for (int r = 0; r < (WTILE + 2 + 63) / 64; ++r) {
@@ -488,10 +483,192 @@ __global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, cons
         if (__ballot(bad) != 0) pk = merge_lane(A, B, c, lane, &nd);  // exact merge (shared prefixes)
         uint32_t s = nd;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-        if (lane == 0) tilecnt[t] = s;
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        *total = s;
     }
+    return pk;
+}
+
+// Pass 1, one wave per 512-output tile (multi-pass form; k_diff_fused is the default).
+__global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
+                                                    uint64_t nt, uint32_t *__restrict__ packed,
+                                                    uint32_t *__restrict__ tilecnt) {
+    __shared__ uint64_t lds[4 * (WTILE + 2)];  // per-wave prefix slices for the general merge
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= nt) return;  // wave-uniform
+    const uint32_t lane = threadIdx.x & 63;
+    const TileCtx c = wave_tile(A, B, split, t);
+    uint32_t total = 0;
+    const uint32_t pk = diff_tile(A, B, c, lane, lds + (threadIdx.x >> 6) * (WTILE + 2), &total);
+    if (lane == 0) tilecnt[t] = total;
     packed[t * 64 + lane] = pk;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Single-pass merge-join (round 3, default): coarse splits by a 64-ary search (one wave per 64th tile),
+// then ONE kernel per diff — each wave finds its tile's two splits by a 32-ary search between the
+// coarse neighbours (half-wave each), runs the tile body, the workgroup publishes its divergent count
+// and looks back (decoupled, agent-scope status words tagged with a per-call epoch, so the status array
+// is never cleared) for its global offset, and the waves write their refs in merged = sorted order.
+// Replaces the fine partition, the packed-result round trip, the widen / scan kernels and pass 2.
+// ---------------------------------------------------------------------------------------------
+// split(d) in [L, H] (inclusive) by an NL-ary search on lanes [lane0, lane0 + NL) of the wave (hl = the
+// lane's index in that group). pred(a) = A[a] precedes B[d-1-a] (A first on equal keys) is monotone
+// (true below the split), so the true probes of a round are a prefix of the group.
+template <int NL>
+__device__ __forceinline__ uint64_t split_search(const DiffSide &A, const DiffSide &B, uint64_t d, uint64_t L,
+                                                 uint64_t H, uint32_t hl, uint32_t lane0) {
+    while (H > L) {
+        const uint64_t w = H - L;
+        const bool fine = w <= (uint64_t)NL;
+        const uint64_t p = fine ? L + hl : L + (w * (hl + 1)) / (NL + 1);
+        bool pr = false;
+        if (!fine || hl < w) {
+            const uint64_t jb = d - 1 - p;
+            pr = cmp_merge(A, p, A.pfx[p], B, jb, B.pfx[jb]) <= 0;
+        }
+        const uint64_t bal = __ballot(pr);
+        uint32_t cnt;
+        if constexpr (NL == 64) cnt = (uint32_t)__popcll(bal);
+        else cnt = (uint32_t)__popcll((bal >> lane0) & ((1ull << NL) - 1));
+        if (fine) {
+            L += cnt;
+            H = L;
+        } else {
+            const uint64_t nl = cnt ? L + (w * cnt) / (NL + 1) + 1 : L;
+            const uint64_t nh = cnt < (uint32_t)NL ? L + (w * (cnt + 1)) / (NL + 1) : H;
+            L = nl;
+            H = nh;
+        }
+    }
+    return L;
+}
+
+// coarse[q] = split of tile 64 q (q < nc), coarse[nc] = A.n (the end). One wave per entry.
+__global__ __launch_bounds__(256) void k_diff_coarse(DiffSide A, DiffSide B, uint64_t nc, uint64_t *__restrict__ coarse) {
+    const uint64_t q = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q > nc) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t M = A.n + B.n;
+    uint64_t d = q * PART_STRIDE * WTILE;
+    if (d > M || q == nc) d = M;
+    const uint64_t L = d > B.n ? d - B.n : 0, H = d < A.n ? d : A.n;
+    const uint64_t r = split_search<64>(A, B, d, L, H, lane, 0);
+    if (lane == 0) coarse[q] = r;
+}
+
+// split of tile tt (<= nt) from the coarse splits: exact at multiples of PART_STRIDE, else a search of
+// the bracket the coarse neighbours leave (as k_diff_partition_fine).
+__device__ __forceinline__ uint64_t fused_split(const DiffSide &A, const DiffSide &B, const uint64_t *coarse,
+                                                uint64_t nt, uint64_t tt, uint32_t hl, uint32_t lane0) {
+    const uint64_t M = A.n + B.n;
+    const uint64_t q = tt / PART_STRIDE, nc = (nt + PART_STRIDE - 1) / PART_STRIDE;
+    if (tt == nt) return coarse[nc];
+    if (tt % PART_STRIDE == 0) return coarse[q];
+    const uint64_t t0 = q * PART_STRIDE, t1 = t0 + PART_STRIDE < nt ? t0 + PART_STRIDE : nt;
+    const uint64_t d = tt * WTILE, d0 = t0 * WTILE, d1 = t1 * WTILE < M ? t1 * WTILE : M;
+    const uint64_t a0 = coarse[q], a1 = coarse[q + 1 <= nc ? q + 1 : nc];
+    uint64_t lo = a1 > d1 - d ? a1 - (d1 - d) : 0, hi = a0 + (d - d0);
+    if (lo < a0) lo = a0;
+    if (hi > a1) hi = a1;
+    if (d > B.n && lo < d - B.n) lo = d - B.n;
+    if (hi > A.n) hi = A.n;
+    if (hi > d) hi = d;
+    if (lo > hi) lo = hi;
+    return split_search<32>(A, B, d, lo, hi, hl, lane0);
+}
+
+constexpr uint64_t DS_AGG = 1ull << 62, DS_INC = 2ull << 62;
+constexpr int DS_EPOCH_SHIFT = 40;
+constexpr uint64_t DS_VAL = (1ull << DS_EPOCH_SHIFT) - 1;
+constexpr uint64_t DS_EPOCH = (1ull << 22) - 1;
+constexpr uint32_t DS_SPIN_LIMIT = 1u << 22;
+
+__global__ __launch_bounds__(256) void k_diff_fused(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
+                                                    uint64_t nt, uint64_t *__restrict__ status, uint32_t epoch,
+                                                    uint64_t *__restrict__ refs, uint64_t *__restrict__ out) {
+    __shared__ uint64_t lds[4 * (WTILE + 2)];
+    __shared__ uint32_t wcnt[4];
+    __shared__ uint64_t wg_excl;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + wave;
+    const uint64_t M = A.n + B.n;
+    uint32_t pk = 0, total = 0;
+    TileCtx c{};
+    if (t < nt) {  // wave-uniform
+        const uint64_t tt = t + (lane >> 5);  // lanes 0-31: split of tile t; lanes 32-63: of tile t + 1
+        const uint64_t sp = fused_split(A, B, coarse, nt, tt, lane & 31, lane & 32);
+        c.d0 = t * WTILE;
+        const uint64_t d1 = c.d0 + WTILE < M ? c.d0 + WTILE : M;
+        c.a0 = shfl_u64(sp, 0);
+        c.a1 = shfl_u64(sp, 32);
+        c.b0 = c.d0 - c.a0;
+        c.b1 = d1 - c.a1;
+        pk = diff_tile(A, B, c, lane, lds + wave * (WTILE + 2), &total);
+    }
+    if (lane == 0) wcnt[wave] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t agg = (uint64_t)wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+        const uint64_t tag = (uint64_t)(epoch & DS_EPOCH) << DS_EPOCH_SHIFT;
+        const uint64_t b = blockIdx.x;
+        uint64_t excl = 0;
+        if (b == 0) {
+            __hip_atomic_store(&status[0], DS_INC | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&status[b], DS_AGG | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t)b - 1;
+            uint32_t spins = 0;
+            constexpr int WIN = 4;
+            while (j >= 0) {
+                uint64_t v[WIN];
+#pragma unroll
+                for (int q = 0; q < WIN; ++q)
+                    v[q] = j - q >= 0 ? __hip_atomic_load(&status[j - q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                      : (DS_INC | tag);
+                int used = 0;
+                bool done = false;
+#pragma unroll
+                for (int q = 0; q < WIN; ++q) {
+                    if (done || used < q) break;
+                    const uint64_t x = v[q];
+                    if ((x & (DS_EPOCH << DS_EPOCH_SHIFT)) != tag || (x >> 62) == 0) break;  // not ready
+                    excl += x & DS_VAL;
+                    ++used;
+                    done = (x >> 62) == 2;
+                }
+                if (done) break;
+                j -= used;
+                if (used == 0) {
+                    if (++spins > DS_SPIN_LIMIT) {  // never hang: the host re-runs the multi-pass form
+                        __hip_atomic_store(&out[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __hip_atomic_store(&status[b], DS_INC | tag | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        wg_excl = excl;
+        if (b == gridDim.x - 1) out[0] = excl + agg;
+    }
+    __syncthreads();
+    if (t >= nt) return;
+    // refs of this tile's divergent keys at their global positions (pass 2 of the multi-pass form)
+    uint64_t base = wg_excl;
+    for (uint32_t w = 0; w < wave; ++w) base += wcnt[w];
+    const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
+    const uint32_t cnt = __popc(div);
+    uint64_t off = base + (wave_incl_scan<uint32_t>(cnt) - cnt);
+    if (!div) return;
+    const uint64_t dl = (uint64_t)lane * DI;
+    uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
+    for (int s = 0; s < DI; ++s) {
+        const bool fa = (fromA >> s) & 1u;
+        const uint64_t ref = fa ? i : (j | (1ull << 63));
+        if (fa) ++i; else ++j;
+        if ((div >> s) & 1u) refs[off++] = ref;
+    }
 }
 
 // Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
@@ -776,6 +953,26 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);
     exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
     hipLaunchKernelGGL(k_diff_pass2, wg, dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs);
+    MKV_LAUNCH_CHECK();
+}
+
+size_t diff_fused_status_words(uint64_t M) { return ceil_div(ceil_div(M ? M : 1, WTILE), 4) + 4; }
+size_t diff_fused_scratch_bytes(uint64_t M) {
+    const uint64_t nt = ceil_div(M ? M : 1, WTILE);
+    return (ceil_div(nt, PART_STRIDE) + 2) * sizeof(uint64_t);
+}
+
+void launch_diff_fused(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *status, uint32_t epoch,
+                       uint64_t *refs, uint64_t *out2, hipStream_t st) {
+    const uint64_t M = A.n + B.n;
+    MKV_HIP(hipMemsetAsync(out2, 0, 2 * sizeof(uint64_t), st));
+    if (M == 0) return;
+    const uint64_t nt = ceil_div(M, WTILE);
+    const uint64_t nc = ceil_div(nt, PART_STRIDE);
+    uint64_t *coarse = reinterpret_cast<uint64_t *>(scratch);
+    hipLaunchKernelGGL(k_diff_coarse, dim3((uint32_t)ceil_div(nc + 1, 4)), dim3(256), 0, st, A, B, nc, coarse);
+    hipLaunchKernelGGL(k_diff_fused, dim3((uint32_t)ceil_div(nt, 4)), dim3(256), 0, st, A, B, coarse, nt, status, epoch,
+                       refs, out2);
     MKV_LAUNCH_CHECK();
 }
 

@@ -179,6 +179,13 @@ size_t diff_scratch_bytes(uint64_t nmerged);
 // in sorted order; *count (device) receives the number. Returns nothing; host reads count.
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
                  hipStream_t st);
+// Single-pass merge-join (k_diff_coarse + k_diff_fused): refs in sorted order, out2[0] = count,
+// out2[1] != 0 if a look-back gave up (then re-run launch_diff). status: diff_fused_status_words(M)
+// u64, zeroed when allocated; epoch: 1 + a per-call counter (mod 2^22, never 0) so it is never cleared.
+size_t diff_fused_status_words(uint64_t nmerged);
+size_t diff_fused_scratch_bytes(uint64_t nmerged);
+void launch_diff_fused(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *status, uint32_t epoch,
+                       uint64_t *refs, uint64_t *out2, hipStream_t st);
 // Top-down diff for trees with equal leaf counts (identical level shapes).
 // fin/fout: local indices; a_par/a_child: global index of local 0 at the parent/child level; r0/r1:
 // extra child-level candidates (owned nodes with an unowned parent; UINT64_MAX = none).

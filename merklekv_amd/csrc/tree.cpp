@@ -223,6 +223,8 @@ struct mkv_tree {
     DevBuf s_tie, s_flags, s_scan, s_pos, s_pos0, s_lens;
     DevBuf s_radix, s_misc;
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
+    DevBuf d_status;   // k_diff_fused's look-back status words (zeroed when allocated; epoch-tagged)
+    uint32_t diff_epoch = 0;
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf leaf_ctr;  // dynamic chunk counter of the leaf hash
@@ -659,6 +661,15 @@ uint64_t total_nodes(const mkv_tree *t) {
     uint64_t s = 0;
     for (auto c : t->lev_cnt) s += c;
     return s;
+}
+
+// MKV_DIFF_FUSED (A/B knob): 1 (default) = single-pass merge-join (k_diff_fused), 0 = multi-pass.
+static bool fused_diff_enabled() {
+    static const bool v = [] {
+        const char *e = getenv("MKV_DIFF_FUSED");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
 }
 
 // MKV_TOP_REDUCE (A/B knob): 1 (default) = the tree's top levels in one k_reduce_top launch, 0 = the
@@ -2358,11 +2369,32 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     }
     if (!done) {
         size_t pd = prof_begin(t, "diff");
-        void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
         uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
-        launch_diff(A, B, scr, refs, cnt, t->st);
-        prof_end(t, pd);
-        m = d2h_u64(t, cnt);
+        bool ran = false;
+        if (fused_diff_enabled()) {
+            void *scr = t->d_diffscr.ensure(diff_fused_scratch_bytes(M));
+            const size_t sw = diff_fused_status_words(M);
+            const bool fresh = t->d_status.cap < 8 * sw || !t->d_status.p;
+            uint64_t *status = ens<uint64_t>(t->d_status, sw);
+            // epochs 1 .. 2^22 - 1 (never the zeroed tag); a wrap clears the words an older call left
+            if (fresh || ++t->diff_epoch >= (1u << 22)) {
+                MKV_HIP(hipMemsetAsync(status, 0, t->d_status.cap, t->st));
+                t->diff_epoch = 1;
+            }
+            launch_diff_fused(A, B, scr, status, t->diff_epoch, refs, cnt, t->st);
+            prof_end(t, pd);
+            small_d2h(t, t->h_small, cnt, 16, t->st);
+            wait_stream(t, t->st);
+            m = t->h_small[0];
+            ran = t->h_small[1] == 0;  // else a look-back gave up: the multi-pass form below
+            if (!ran) pd = prof_begin(t, "diff");
+        }
+        if (!ran) {
+            void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
+            launch_diff(A, B, scr, refs, cnt, t->st);
+            prof_end(t, pd);
+            m = d2h_u64(t, cnt);
+        }
     }
     return keylist_from_refs(t, refs, m, A, B);
 }
