@@ -37,7 +37,10 @@ sys.path.insert(0, ROOT)
 
 SEED = 0x4D65726B6C654B56
 KLEN, VLEN = 32, 100
-LEAF_BYTES = 8 + KLEN + VLEN + 32   # algorithmic bytes per leaf for Kernel A: 140-B record read + 32-B digest
+LEAF_BYTES = 8 + KLEN + VLEN + 32   # record model: 140-B record (k, v, 8 B of offsets) read + 32-B digest written
+# what the timed leaf kernel moves per leaf in a build from borrowed device buffers: the record model plus
+# the fused key-ownership copy (32-B key + 8-B offset written into the tree's own key store)
+LEAF_BYTES_BUILD = LEAF_BYTES + KLEN + 8
 HBM_PEAK_GBS = 8000.0                # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 SHA_OPS_PER_LEAF = 3 * 1450          # model: 3 compressions x ~1450 VALU lane-ops
@@ -164,13 +167,17 @@ def random_values(torch, m, dev, gen):
 
 # ============================================================================================ build
 def leaf_roofline(n, leaf_avg_ms, launches):
-    """roofline of the dominant kernel (the leaf hash, k_leaf_direct). achieved = 172 B/leaf x n / live launch time (HIP
+    """roofline of the dominant kernel (the leaf hash, k_leaf_direct). achieved = 212 B/leaf x n / live launch time
+    (172 B record model + the fused 40-B key-ownership copy the timed kernel also does; the 172-B figure is
+    reported beside it) (HIP
     events on the tree's stream, sort co-running); traffic and the VALU fractions come from the PMC file
     of the same tree (profiles/pmc_leaf_hash.json, written by scripts/prof_summary.py)."""
-    achieved = LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9
+    achieved = LEAF_BYTES_BUILD * n / (leaf_avg_ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_leaf_direct",
-           "bytes_per_leaf": LEAF_BYTES, "avg_launch_ms": leaf_avg_ms, "launches": launches,
+           "bytes_per_leaf": LEAF_BYTES_BUILD, "avg_launch_ms": leaf_avg_ms, "launches": launches,
+           "achieved_record_model": LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9,
+           "bytes_per_leaf_record_model": LEAF_BYTES,
            "gb_per_s_hashed": (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9,
            "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): the HBM frac ceiling is ~0.39; "
                    "avg_launch_ms is measured live while the ordering kernels co-run on the aux stream"}
@@ -814,6 +821,15 @@ def wl_incremental(ctx, args):
     el = ctx.max_over_ranks(time.perf_counter() - t0)
     upd_ms = variants[0].prof_read("update")[0] / args.steps  # one batched call: all R-1 replicas
     diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))  # batched walk: per-pair share
+    climb_ms = variants[0].prof_read("climb")[0] / args.steps      # shared dirty climb, all replicas
+    walk_ms = base.prof_read("walk")[0] / args.steps               # shared 1-vs-(R-1) walk launches
+    for t in [base] + variants:
+        t.prof_enable(False)
+    # work of the last step (stats of the last update / walk; every step does the same amount)
+    counts = [v.update_counts() for v in variants]
+    rehashed = sum(sum(c[1:]) for c in counts)  # internal nodes rehashed by the climb
+    changed = sum(c[0] for c in counts if c)
+    ws = base.walk_stats()
     ok = all(len(d) == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else
     total_updates = ctx.sum_over_ranks(m) * (R - 1)
     roots = []
@@ -824,8 +840,28 @@ def wl_incremental(ctx, args):
               f"{m} value updates per variant per rank; step = {R - 1} dirty-path batches + 1-vs-{R - 1} diff")
         out = base_line(ctx, args, "Incremental anti-entropy: update keys/s (dirty-path rehash + 8-replica diff)",
                         total_updates * args.steps / el, "keys/s", el / args.steps * 1e3, wl)
+        climb_bytes = 96 * rehashed  # per rehashed node: both children read (64 B) + the node written (32 B)
+        comp = 2 * rehashed          # one full + one constant-schedule compression per node
+        out["roofline"] = {
+            "bound": "hbm", "kernel": "dirty climb (k_dirty_level x levels + k_dirty_top), all replicas",
+            "achieved": climb_bytes / (climb_ms * 1e-3) / 1e9 if climb_ms else None, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": climb_bytes / (climb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if climb_ms else None,
+            "traffic": None, "bytes_per_rehashed_node": 96, "rehashed_nodes_per_step": rehashed,
+            "changed_leaves_per_step": changed, "climb_ms_per_step": climb_ms,
+            "valu": {"compressions_per_step": comp, "lane_ops_model": comp * 1376,
+                     "frac_of_78.6T": comp * 1376 / (climb_ms * 1e-3) / (VALU_PEAK_TOPS * 1e12) if climb_ms else None,
+                     "note": "1,376 VALU lane-ops per compression (measured on the leaf kernel, PMC)"},
+            "walk": {"ms_per_step": walk_ms, "ms_per_pair": walk_ms / (R - 1), "entries": ws["entries"],
+                     "bytes_compared": ws["bytes"], "bytes_per_pair": ws["bytes"] / (R - 1),
+                     "gb_per_s": ws["bytes"] / (walk_ms * 1e-3) / 1e9 if walk_ms else None,
+                     "launches": ws["launches"], "divergent_positions": ws["divergent_positions"]},
+            "note": "achieved = 96 B x rehashed nodes (read back from the trees) / HIP-event time of the climb "
+                    "launches on the group's stream; the climb is a random gather of sibling pairs plus 2 "
+                    "compressions per node (VALU-heavy), walk = the shared top-down launches (digests compared "
+                    "in both trees) without the key gather / PCIe copy of the key lists"}
         out["incremental"] = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
                               "update_device_ms_all_replicas": upd_ms, "diff_device_ms_per_pair": diff_ms,
+                              "climb_device_ms": climb_ms, "walk_device_ms_per_pair": walk_ms / (R - 1),
                               "diff_sizes_match_unique_updates": ok,
                               "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
         out["cpu_baseline"] = None if (args.no_cpu_baseline or ctx.world > 1) else cpu_baseline_update()

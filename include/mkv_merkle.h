@@ -211,6 +211,12 @@ mkv_status mkv_prof_reset(mkv_tree *t);
 mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms, uint64_t *count);
 /* Synthetic records (same generator as oracle/merkle_oracle.c) written to device buffers:
  * kb >= n*klen, vb >= n*vlen, koff/voff n+1 entries. Synchronous. */
+/* Introspection (benches / tests): per-level dirty entry counts of the tree's last dirty-path update
+ * (level 0 = changed leaves, level l > 0 = rehashed nodes), and the last batched top-down walk this tree
+ * ran as the base (mkv_tree_diff_many): out[0] = frontier entries expanded, out[1] = digest bytes the walk
+ * compared, out[2] = divergent leaf positions, out[3] = launches. Both synchronise the tree's stream. */
+mkv_status mkv_tree_update_counts(const mkv_tree *t, uint64_t *out, uint32_t cap, uint32_t *nlevels);
+mkv_status mkv_tree_walk_stats(const mkv_tree *t, uint64_t out[4]);
 mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,
                                   uint32_t vlen, uint32_t shard, uint32_t nshards, uint32_t vfield, uint8_t *kb,
                                   uint64_t *koff, uint8_t *vb, uint64_t *voff);

@@ -27,7 +27,8 @@ EXPORTS = [
     "mkv_tree_diff_many", "mkv_tree_node_digests", "mkv_tree_compare_nodes", "mkv_tree_keys_at",
     "mkv_tree_prefix_root", "mkv_keylist_get", "mkv_keylist_free", "mkv_last_error", "mkv_shard_prepare",
     "mkv_shard_reduce", "mkv_shard_fringe", "mkv_shard_combine", "mkv_prof_enable", "mkv_prof_reset",
-    "mkv_prof_read", "mkv_gen_records_device", "mkv_gen_records_ragged_device", "mkv_leaf_digests", "mkv_version",
+    "mkv_prof_read", "mkv_gen_records_device", "mkv_gen_records_ragged_device", "mkv_tree_update_counts",
+    "mkv_tree_walk_stats", "mkv_leaf_digests", "mkv_version",
     "mkv_tree_build_digests", "mkv_tree_hash_pattern", "mkv_shard_fringe_device", "mkv_shard_combine_device",
     "mkv_pool_trim", "mkv_pool_stats", "mkv_debug_trace",
     "mkv_route_sample", "mkv_route_splitters", "mkv_route_plan", "mkv_route_pack", "mkv_route_offsets",
@@ -93,6 +94,8 @@ def lib():
         "mkv_prof_read": ([vp, C.c_char_p, P(C.c_double), P(u64)], i32),
         "mkv_gen_records_device": ([i32, u64, u64, u64, u32, u32, u32, u32, u32, vp, vp, vp, vp], i32),
         "mkv_gen_records_ragged_device": ([i32, u64, u64, u64, u32, u32, u32, u32, u32, vp, vp, vp, vp], i32),
+        "mkv_tree_update_counts": ([vp, vp, u32, vp], i32),
+        "mkv_tree_walk_stats": ([vp, vp], i32),
         "mkv_leaf_digests": ([i32, Blob, Blob, vp], i32),
         "mkv_version": ([], C.c_char_p),
         "mkv_tree_build_digests": ([vp, Blob, vp], i32),

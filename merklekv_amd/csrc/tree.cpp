@@ -223,6 +223,9 @@ struct mkv_tree {
     DevBuf s_tie, s_flags, s_scan, s_pos, s_pos0, s_lens;
     DevBuf s_radix, s_misc;
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
+    // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
+    std::vector<std::pair<uint32_t, uint32_t>> walk_jumps;
+    uint32_t walk_L = 0, walk_k = 0;
     DevBuf d_status;   // k_diff_fused's look-back status words (zeroed when allocated; epoch-tagged)
     uint32_t diff_epoch = 0;
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
@@ -1759,6 +1762,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         for (size_t q = 0; q < g.size(); ++q) msum += bs[g[q]].m;
         const bool keep_bits = keep_env >= 0 ? keep_env == 1 : msum * 4096 >= total_nodes(t0);
         if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
+        const size_t pclimb = prof_begin(t0, "climb", st);
         for (size_t l = 0; l < ltop; ++l) {
             DirtyLevel D{};
             D.a = t0->lev_base[l];
@@ -1792,6 +1796,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             }
             launch_dirty_top(P, (int)ltop, T, k2, st);
         }
+        prof_end(t0, pclimb);
         // every tree's missing-key count and root, read back by one launch
         SmallCopies SC{};
         uint32_t nc = 0;
@@ -2418,6 +2423,10 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     uint64_t *fin = f0, *fout = f1;
     bool sharded = a->sharded;
     for (auto *v : vs) sharded |= v->sharded;
+    t->walk_jumps.clear();
+    t->walk_L = (uint32_t)L;
+    t->walk_k = k;
+    const size_t pwalk = prof_begin(t, "walk");
     if (!sharded && L > 1 && jumps_enabled()) {  // seed with every variant's root, then jump 4 levels per launch
         launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
                                    fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
@@ -2426,18 +2435,23 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         for (size_t q = 1; q < T.size(); ++q) {
             const size_t l = T[q - 1], lt = T[q];
             const int kk = (int)(l - lt);
+            t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
             launch_topdown_jump_batch(na + 32 * a->lev_off[lt], V, 32 * a->lev_off[lt], a->lev_cnt[lt], kk, fin, cnt + l,
                                       fout, cnt + lt, std::min<uint64_t>(k * (a->lev_cnt[l] << kk), 1ull << 40), t->st);
             std::swap(fin, fout);
             if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
                 const uint64_t c = d2h_u32(t, cnt + lt);
-                if (2 * c > k * a->lev_cnt[lt]) return false;
+                if (2 * c > k * a->lev_cnt[lt]) {
+                    prof_end(t, pwalk);
+                    return false;
+                }
             }
         }
     } else
     for (size_t l = L; l >= 1; --l) {
         uint64_t r[2];
         level_roots(a, l - 1, r);
+        if (l < L) t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)(l - 1));
         const uint64_t a_par = l < L ? a->lev_base[l] : 0, max_par = l < L ? k * a->lev_cnt[l] : 0;
         launch_topdown_level_batch(na + 32 * a->lev_off[l - 1], V, 32 * a->lev_off[l - 1], a->lev_cnt[l - 1], a_par,
                                    a->lev_base[l - 1], r[0], r[1], k, fin, cnt + l, fout, cnt + (l - 1), max_par,
@@ -2445,9 +2459,13 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         std::swap(fin, fout);
         if (l - 1 == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
             const uint64_t c = d2h_u32(t, cnt + (l - 1));
-            if (2 * c > k * a->lev_cnt[l - 1]) return false;
+            if (2 * c > k * a->lev_cnt[l - 1]) {
+                prof_end(t, pwalk);
+                return false;
+            }
         }
     }
+    prof_end(t, pwalk);
     const uint64_t m = d2h_u32(t, cnt);
     uint32_t *nbad = cnt + L + 2, *vcount = nbad + k;
     // per-variant key-check failures and segment starts come back through pinned memory with the
@@ -3131,6 +3149,48 @@ mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms,
         auto it = t->pg.find(group);
         *total_ms = it == t->pg.end() ? 0.0 : it->second.first;
         *count = it == t->pg.end() ? 0 : it->second.second;
+    });
+}
+
+mkv_status mkv_tree_update_counts(const mkv_tree *t, uint64_t *out, uint32_t cap, uint32_t *nlevels) {
+    MKV_TRY({
+        NEED(t && nlevels && (out || cap == 0), "null argument");
+        const uint32_t L = (uint32_t)t->lev_S.size();
+        *nlevels = L;
+        if (!t->u_cnt.p || L == 0) {
+            *nlevels = 0;
+            return MKV_OK;
+        }
+        DevGuard g(t->dev);
+        std::vector<uint32_t> h(L);
+        MKV_HIP(hipStreamSynchronize(t->st));
+        MKV_HIP(hipMemcpy(h.data(), t->u_cnt.p, 4ull * L, hipMemcpyDeviceToHost));
+        for (uint32_t l = 0; l < L && l < cap; ++l) out[l] = h[l];
+    });
+}
+
+mkv_status mkv_tree_walk_stats(const mkv_tree *t, uint64_t out[4]) {
+    MKV_TRY({
+        NEED(t && out, "null argument");
+        out[0] = out[1] = out[2] = out[3] = 0;
+        if (!t->td_cnt.p || t->walk_L == 0) return MKV_OK;
+        DevGuard g(t->dev);
+        const uint32_t L = t->walk_L;
+        std::vector<uint32_t> h(L + 1);
+        MKV_HIP(hipStreamSynchronize(t->st));
+        MKV_HIP(hipMemcpy(h.data(), t->td_cnt.p, 4ull * (L + 1), hipMemcpyDeviceToHost));
+        // a frontier entry at level l expanded to level lt compares its 2^(l-lt) descendants in the base
+        // and in its variant (32 B each); the seed compares the k + 1 roots
+        uint64_t entries = t->walk_k, bytes = 32ull * (t->walk_k + 1);
+        for (auto &j : t->walk_jumps) {
+            const uint64_t c = h[j.first];
+            entries += c;
+            bytes += c * 2ull * 32ull * (1ull << (j.first - j.second));
+        }
+        out[0] = entries;
+        out[1] = bytes;
+        out[2] = h[0];
+        out[3] = t->walk_jumps.size() + 1;
     });
 }
 

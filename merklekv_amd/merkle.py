@@ -569,6 +569,19 @@ class MerkleTree:
         check(lib().mkv_prof_read(self._h, group.encode(), C.byref(ms), C.byref(cnt)))
         return ms.value, cnt.value
 
+    def update_counts(self) -> list[int]:
+        """Per-level dirty entry counts of this tree's last dirty-path update (mkv_tree_update_counts)."""
+        out = (C.c_uint64 * 64)()
+        nl = C.c_uint32()
+        check(lib().mkv_tree_update_counts(self._h, out, 64, C.byref(nl)))
+        return [out[i] for i in range(min(nl.value, 64))]
+
+    def walk_stats(self) -> dict:
+        """The last batched top-down walk with this tree as the base (mkv_tree_walk_stats)."""
+        out = (C.c_uint64 * 4)()
+        check(lib().mkv_tree_walk_stats(self._h, out))
+        return {"entries": out[0], "bytes": out[1], "divergent_positions": out[2], "launches": out[3]}
+
     # ------------------------------------------------------------------ sharded build
     def shard_prepare(self, keys, values, on_device: bool = False) -> int:
         n = C.c_uint64()
