@@ -584,14 +584,52 @@ constexpr uint64_t DS_VAL = (1ull << DS_EPOCH_SHIFT) - 1;
 constexpr uint64_t DS_EPOCH = (1ull << 22) - 1;
 constexpr uint32_t DS_SPIN_LIMIT = 1u << 22;
 
-__global__ __launch_bounds__(256) void k_diff_fused(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
-                                                    uint64_t nt, uint64_t *__restrict__ status, uint32_t epoch,
-                                                    uint64_t *__restrict__ refs, uint64_t *__restrict__ out) {
-    __shared__ uint64_t lds[4 * (WTILE + 2)];
-    __shared__ uint32_t wcnt[4];
+constexpr int DF_WAVES = 8;  // tiles per workgroup of the single-pass form
+
+// Decoupled look-back by one wave: 64 predecessors' status words per round (lane q reads b-1-q). The
+// nearest inclusive word ends the walk; aggregates before it (and before any not-yet-published word) are
+// summed. Returns the exclusive prefix, or sets *gave_up after DS_SPIN_LIMIT empty rounds.
+__device__ __forceinline__ uint64_t df_lookback(uint64_t *status, uint64_t b, uint64_t tag, uint32_t lane,
+                                                bool *gave_up) {
+    uint64_t excl = 0;
+    int64_t j = (int64_t)b - 1;
+    uint32_t spins = 0;
+    while (j >= 0) {
+        const int64_t idx = j - (int64_t)lane;
+        const uint64_t x = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : (DS_INC | tag);  // before workgroup 0: an inclusive zero
+        const bool ready = (x & (DS_EPOCH << DS_EPOCH_SHIFT)) == tag && (x >> 62) != 0;
+        const bool inc = ready && (x >> 62) == 2;
+        const uint64_t nr = __ballot(!ready), im = __ballot(inc);
+        const uint32_t first_nr = nr ? (uint32_t)__builtin_ctzll(nr) : 64u;
+        const uint32_t first_inc = im ? (uint32_t)__builtin_ctzll(im) : 64u;
+        const bool done = first_inc < first_nr;
+        const uint32_t take = done ? first_inc + 1 : first_nr;  // lanes [0, take) are summed
+        uint64_t v = lane < take ? (x & DS_VAL) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += shfl_u64(v, (int)(lane ^ (uint32_t)o));
+        excl += v;
+        if (done) break;
+        j -= take;
+        if (take == 0) {
+            if (++spins > DS_SPIN_LIMIT) {
+                *gave_up = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return excl;
+}
+
+__global__ __launch_bounds__(64 * DF_WAVES) void k_diff_fused(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
+                                                              uint64_t nt, uint64_t *__restrict__ status, uint32_t epoch,
+                                                              uint64_t *__restrict__ refs, uint64_t *__restrict__ out) {
+    __shared__ uint64_t lds[DF_WAVES * (WTILE + 2)];
+    __shared__ uint32_t wcnt[DF_WAVES];
     __shared__ uint64_t wg_excl;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + wave;
+    const uint64_t t = (uint64_t)blockIdx.x * DF_WAVES + wave;
     const uint64_t M = A.n + B.n;
     uint32_t pk = 0, total = 0;
     TileCtx c{};
@@ -608,49 +646,28 @@ __global__ __launch_bounds__(256) void k_diff_fused(DiffSide A, DiffSide B, cons
     }
     if (lane == 0) wcnt[wave] = total;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint64_t agg = (uint64_t)wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (wave == 0) {
+        uint64_t agg = 0;
+#pragma unroll
+        for (int w = 0; w < DF_WAVES; ++w) agg += wcnt[w];
         const uint64_t tag = (uint64_t)(epoch & DS_EPOCH) << DS_EPOCH_SHIFT;
         const uint64_t b = blockIdx.x;
         uint64_t excl = 0;
         if (b == 0) {
-            __hip_atomic_store(&status[0], DS_INC | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) __hip_atomic_store(&status[0], DS_INC | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            __hip_atomic_store(&status[b], DS_AGG | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            int64_t j = (int64_t)b - 1;
-            uint32_t spins = 0;
-            constexpr int WIN = 4;
-            while (j >= 0) {
-                uint64_t v[WIN];
-#pragma unroll
-                for (int q = 0; q < WIN; ++q)
-                    v[q] = j - q >= 0 ? __hip_atomic_load(&status[j - q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                      : (DS_INC | tag);
-                int used = 0;
-                bool done = false;
-#pragma unroll
-                for (int q = 0; q < WIN; ++q) {
-                    if (done || used < q) break;
-                    const uint64_t x = v[q];
-                    if ((x & (DS_EPOCH << DS_EPOCH_SHIFT)) != tag || (x >> 62) == 0) break;  // not ready
-                    excl += x & DS_VAL;
-                    ++used;
-                    done = (x >> 62) == 2;
-                }
-                if (done) break;
-                j -= used;
-                if (used == 0) {
-                    if (++spins > DS_SPIN_LIMIT) {  // never hang: the host re-runs the multi-pass form
-                        __hip_atomic_store(&out[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                }
+            if (lane == 0) __hip_atomic_store(&status[b], DS_AGG | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool gave_up = false;
+            excl = df_lookback(status, b, tag, lane, &gave_up);
+            if (lane == 0) {
+                if (gave_up) __hip_atomic_store(&out[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&status[b], DS_INC | tag | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            __hip_atomic_store(&status[b], DS_INC | tag | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        wg_excl = excl;
-        if (b == gridDim.x - 1) out[0] = excl + agg;
+        if (lane == 0) {
+            wg_excl = excl;
+            if (b == gridDim.x - 1) out[0] = excl + agg;
+        }
     }
     __syncthreads();
     if (t >= nt) return;
@@ -956,7 +973,7 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     MKV_LAUNCH_CHECK();
 }
 
-size_t diff_fused_status_words(uint64_t M) { return ceil_div(ceil_div(M ? M : 1, WTILE), 4) + 4; }
+size_t diff_fused_status_words(uint64_t M) { return ceil_div(ceil_div(M ? M : 1, WTILE), DF_WAVES) + 4; }
 size_t diff_fused_scratch_bytes(uint64_t M) {
     const uint64_t nt = ceil_div(M ? M : 1, WTILE);
     return (ceil_div(nt, PART_STRIDE) + 2) * sizeof(uint64_t);
@@ -971,8 +988,8 @@ void launch_diff_fused(const DiffSide &A, const DiffSide &B, void *scratch, uint
     const uint64_t nc = ceil_div(nt, PART_STRIDE);
     uint64_t *coarse = reinterpret_cast<uint64_t *>(scratch);
     hipLaunchKernelGGL(k_diff_coarse, dim3((uint32_t)ceil_div(nc + 1, 4)), dim3(256), 0, st, A, B, nc, coarse);
-    hipLaunchKernelGGL(k_diff_fused, dim3((uint32_t)ceil_div(nt, 4)), dim3(256), 0, st, A, B, coarse, nt, status, epoch,
-                       refs, out2);
+    hipLaunchKernelGGL(k_diff_fused, dim3((uint32_t)ceil_div(nt, DF_WAVES)), dim3(64 * DF_WAVES), 0, st, A, B, coarse, nt,
+                       status, epoch, refs, out2);
     MKV_LAUNCH_CHECK();
 }
 

@@ -583,7 +583,8 @@ __global__ __launch_bounds__(256) void k_leaf_dma(const uint8_t *__restrict__ kb
         const uint32_t kbyte = (uint32_t)((kb + kbeg) - P.kstart);
         const uint32_t vbyte = P.kspan + (uint32_t)((vb + vbeg) - P.vstart);
         const bool fixed = P.staged && __all(!valid || (klen == K0 && vlen == V0 && ((kbyte | vbyte) & 3) == 0));
-        if (!fixed && lane == 0) ctr[4 + atomicAdd(&ctr[1], 1u)] = (uint32_t)c;  // for k_leaf_list
+        if (lane == 0) ctr[4 + c] = fixed ? 0u : 1u;  // chunk flags for k_leaf_list
+        if (!fixed && lane == 0) atomicAdd(&ctr[1], 1u);
         uint32_t m[MW];
         if (fixed) {
 #pragma unroll
@@ -670,6 +671,7 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nchunks = (n + 63) / 64;
     ChunkSource<true> src{0, 0, 0, ctr, grain};
+    uint32_t listed = 0;  // this wave's listed chunks: one atomic at the end, not one per chunk
     for (uint64_t c = src.get(lane); c < nchunks; c = src.get(lane)) {
         const uint64_t r = c * 64 + lane;
         const bool valid = r < n;
@@ -679,8 +681,9 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
         const bool fixed =
             __all(!valid || (kend - kbeg == K0 && vend - vbeg == V0 &&
                              ((reinterpret_cast<uintptr_t>(kp) | reinterpret_cast<uintptr_t>(vp)) & 3) == 0));
+        if (lane == 0) ctr[4 + c] = fixed ? 0u : 1u;  // chunk flags: listed chunks are hashed afterwards
         if (!fixed) {
-            if (lane == 0) ctr[4 + atomicAdd(&ctr[1], 1u)] = (uint32_t)c;  // hashed by k_leaf_list
+            ++listed;
             if (KO.kdst) {  // key-ownership copy of the chunk's span
                 const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
                 if (P.kcopy_end <= KO.kcap) {
@@ -712,6 +715,7 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
         hash_regs_block<SHORT, K0, V0, 0>(m, st);
         store_digest(out + 32 * r, st);
     }
+    if (listed && lane == 0) atomicAdd(&ctr[1], listed);
 }
 
 // The chunks k_leaf_dma / k_leaf_direct listed (any shape but the fixed one): one wave per listed chunk, staged through
@@ -725,9 +729,10 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *lds = lds_all + wave * (LEAF_LDS_WAVE / 4);
-    const uint32_t cnt = ctr[1];
-    for (uint64_t e = (uint64_t)blockIdx.x * LEAF_WAVES + wave; e < cnt; e += (uint64_t)gridDim.x * LEAF_WAVES) {
-        const uint64_t c = ctr[4 + e];
+    if (ctr[1] == 0) return;
+    const uint64_t nchunks = (n + 63) / 64;
+    for (uint64_t c = (uint64_t)blockIdx.x * LEAF_WAVES + wave; c < nchunks; c += (uint64_t)gridDim.x * LEAF_WAVES) {
+        if (!ctr[4 + c]) continue;  // flagged by k_leaf_direct / k_leaf_dma
         const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
         if (P.staged) {
             uint4 R[PF];
@@ -788,13 +793,16 @@ __global__ __launch_bounds__(256) void k_ragged_count(const uint64_t *__restrict
     __shared__ uint32_t h[RG_CLASSES];
     if (threadIdx.x < RG_CLASSES) h[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t listed = ctr[1];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
-        const uint64_t e = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
-        if (e >= listed) break;  // uniform per wave
-        const uint64_t r = (uint64_t)ctr[4 + e] * 64 + lane;
-        if (r < n) atomicAdd(&h[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u);
+    const uint64_t nchunks = (n + 63) / 64;
+    if (ctr[1]) {
+        for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
+            const uint64_t c = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
+            if (c >= nchunks) break;  // uniform per wave
+            if (!ctr[4 + c]) continue;
+            const uint64_t r = c * 64 + lane;
+            if (r < n) atomicAdd(&h[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u);
+        }
     }
     __syncthreads();
     if (threadIdx.x < RG_CLASSES) wcnt[(uint64_t)threadIdx.x * nwg + blockIdx.x] = h[threadIdx.x];
@@ -808,12 +816,14 @@ __global__ __launch_bounds__(256) void k_ragged_scatter(const uint64_t *__restri
     __shared__ uint32_t cur[RG_CLASSES];
     if (threadIdx.x < RG_CLASSES) cur[threadIdx.x] = (uint32_t)wbase[(uint64_t)threadIdx.x * nwg + blockIdx.x];
     __syncthreads();
-    const uint32_t listed = ctr[1];
+    if (ctr[1] == 0) return;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t nchunks = (n + 63) / 64;
     for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
-        const uint64_t e = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
-        if (e >= listed) break;
-        const uint64_t r = (uint64_t)ctr[4 + e] * 64 + lane;
+        const uint64_t c = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
+        if (c >= nchunks) break;
+        if (!ctr[4 + c]) continue;
+        const uint64_t r = c * 64 + lane;
         if (r < n) list[atomicAdd(&cur[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u)] = (uint32_t)r;
     }
 }
@@ -840,22 +850,42 @@ __device__ __forceinline__ uint32_t rg_head_mask(uint32_t nbytes) {  // first nb
     return nbytes ? ~(0xFFFFFFFFu >> (8 * nbytes)) : 0u;
 }
 
-// Words [w0, w1] of a field that starts at stream word fw: stream word w = BE word of the source bytes
-// at (src + 4 (w - fw)); written into the lane's window (window-relative word u = w - W0).
-__device__ __forceinline__ void rg_copy_words(uint32_t *lw, uint32_t lane, uint32_t W0, uint32_t w0, uint32_t w1,
-                                              uint32_t fw, const uint8_t *src, const uint8_t *lo,
-                                              const uint8_t *hi) {
-    const uint8_t *A = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
-    const uint32_t sel = 0x00010203u + (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3) * 0x01010101u;
-    for (uint32_t w = w0; w <= w1; w += 4) {
-        const uint8_t *a = A + 4 * (w - fw);
-        const rg_u32x4 d = rg_load4(a, lo, hi);
-        const uint32_t d4 = rg_load1(a + 16, lo, hi);
-        const uint32_t x[4] = {rg_be(d.y, d.x, sel), rg_be(d.z, d.y, sel), rg_be(d.w, d.z, sel), rg_be(d4, d.w, sel)};
+// 16 stream words of one field: w = BE word of the source bytes at (src + 4 (w - fw)), for the words of
+// [w, w1] (at most 16), from 17 aligned source dwords.
+struct RgField {
+    const uint8_t *A;  // floor4(src)
+    uint32_t sel;      // v_perm selector of the source's byte alignment
+    uint32_t fw;       // stream word of the field's first word
+};
+__device__ __forceinline__ RgField rg_field(const uint8_t *src, uint32_t fw) {
+    RgField f;
+    f.A = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(src) & ~uintptr_t(3));
+    f.sel = 0x00010203u + (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3) * 0x01010101u;
+    f.fw = fw;
+    return f;
+}
+__device__ __forceinline__ void rg_load16(const RgField &f, uint32_t w, uint32_t w1, const uint8_t *lo,
+                                          const uint8_t *hi, uint32_t d[17]) {
+    const uint8_t *a = f.A + 4 * (w - f.fw);
+    const uint32_t nw = w <= w1 ? w1 - w + 1 : 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) {
+    for (uint32_t g = 0; g < 4; ++g) {
+        rg_u32x4 x = {0u, 0u, 0u, 0u};
+        if (4 * g < nw) x = rg_load4(a + 16 * g, lo, hi);
+        d[4 * g] = x.x;
+        d[4 * g + 1] = x.y;
+        d[4 * g + 2] = x.z;
+        d[4 * g + 3] = x.w;
+    }
+    d[16] = nw > 15 ? rg_load1(a + 64, lo, hi) : 0u;
+}
+__device__ __forceinline__ void rg_store16(const RgField &f, uint32_t w, uint32_t w1, const uint32_t d[17],
+                                           uint32_t *lw, uint32_t lane, uint32_t W0) {
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        if (w + j <= w1) {
             const uint32_t u = w + j - W0;
-            if (w + j <= w1) lw[((u >> 2) * 64 + lane) * 4 + (u & 3)] = x[j];
+            lw[((u >> 2) * 64 + lane) * 4 + (u & 3)] = rg_be(d[j + 1], d[j], f.sel);
         }
     }
 }
@@ -883,6 +913,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__
         reinterpret_cast<const uint8_t *>((reinterpret_cast<uintptr_t>(vb + voff[n]) + 3) & ~uintptr_t(3));
     const uint64_t T = *total;
     const uint64_t nch = (T + 63) / 64;
+    if (nch == 0) return;  // nothing listed (every chunk had the fixed shape): no chunk counter traffic
     ChunkSource<true> src{0, 0, 0, gctr, grain};
     for (uint64_t c = src.get(lane); c < nch; c = src.get(lane)) {
         const uint64_t p = c * 64 + lane;
@@ -911,10 +942,18 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__
             const uint32_t W0 = 16 * blo, W1 = W0 + 16 * nbw;            // words [W0, W1)
             for (uint32_t q = 0; q < 4 * nbw; ++q) lq[q * 64 + lane] = make_uint4(0, 0, 0, 0);
             if (nbw) {
+                // key words [kw0, kw1] and value words [vw0, vw1] of the window, 16 of each per step with
+                // both fields' loads in flight together (one memory latency per step)
                 const uint32_t kw0 = max(1u, W0), kw1 = min(nk, W1 - 1);
-                if (kw0 <= kw1) rg_copy_words(lw, lane, W0, kw0, kw1, 1, kp, klo, khi);
                 const uint32_t vw0 = max(b1 + 1, W0), vw1 = min(b3, W1 - 1);
-                if (vw0 <= vw1) rg_copy_words(lw, lane, W0, vw0, vw1, b1 + 1, vp - c4, vlo, vhi);
+                const RgField fk = rg_field(kp, 1), fv = rg_field(vp - c4, b1 + 1);
+                for (uint32_t kw = kw0, vw = vw0; kw <= kw1 || vw <= vw1; kw += 16, vw += 16) {
+                    uint32_t dk[17], dv[17];
+                    rg_load16(fk, kw, kw1, klo, khi, dk);
+                    rg_load16(fv, vw, vw1, vlo, vhi, dv);
+                    rg_store16(fk, kw, kw1, dk, lw, lane, W0);
+                    rg_store16(fv, vw, vw1, dv, lw, lane, W0);
+                }
                 // the words that mix fields (read-modify-write, in this order)
                 const uint32_t hc = rg_head_mask(c4);
                 auto at = [&](uint32_t w) -> uint32_t & {

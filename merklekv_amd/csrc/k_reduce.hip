@@ -102,6 +102,11 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
 // The short-chain SHA form (latency) is used throughout.
 constexpr int RD_TOP_FUSE = 10;
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
+// stores (__syncthreads' release fence also drains the level's HBM stores, one memory round trip per
+// level on this latency-bound path).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
     __shared__ uint32_t last;
@@ -158,7 +163,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
             for (int q = 0; q < 8; ++q) dst[q] = o[q];
             store_digest(p.out[k - 1] + 32 * (j - p.a[k]), o);
         }
-        __syncthreads();
+        lds_barrier();
     }
     if (nf >= p.nl) return;
     // ---- hand-off: the last tile to finish climbs the rest ----
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
             for (int q = 0; q < 8; ++q) dst[q] = o[q];
             store_digest(p.out[k - 1] + 32 * i, o);
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 
