@@ -688,6 +688,36 @@ __global__ __launch_bounds__(64 * DF_WAVES) void k_diff_fused(DiffSide A, DiffSi
     }
 }
 
+// Pass 1 of the default multi-pass form (round 3): the wave finds its tile's splits itself (32-ary
+// searches between the 64-ary coarse splits, no fine-partition kernel), publishes split[t] (and
+// split[nt]) for pass 2, and writes its divergent count as u64 (the scan's input: no widen kernel).
+__global__ __launch_bounds__(256) void k_diff_pass1s(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
+                                                     uint64_t nt, uint64_t *__restrict__ split,
+                                                     uint32_t *__restrict__ packed, uint64_t *__restrict__ tilecnt) {
+    __shared__ uint64_t lds[4 * (WTILE + 2)];
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= nt) return;  // wave-uniform
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t M = A.n + B.n;
+    const uint64_t tt = t + (lane >> 5);
+    const uint64_t sp = fused_split(A, B, coarse, nt, tt, lane & 31, lane & 32);
+    TileCtx c;
+    c.d0 = t * WTILE;
+    const uint64_t d1 = c.d0 + WTILE < M ? c.d0 + WTILE : M;
+    c.a0 = shfl_u64(sp, 0);
+    c.a1 = shfl_u64(sp, 32);
+    c.b0 = c.d0 - c.a0;
+    c.b1 = d1 - c.a1;
+    uint32_t total = 0;
+    const uint32_t pk = diff_tile(A, B, c, lane, lds + (threadIdx.x >> 6) * (WTILE + 2), &total);
+    if (lane == 0) {
+        tilecnt[t] = total;
+        split[t] = c.a0;
+        if (t + 1 == nt) split[nt] = c.a1;
+    }
+    packed[t * 64 + lane] = pk;
+}
+
 // Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
 __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, const uint32_t *__restrict__ packed,
@@ -940,7 +970,18 @@ size_t diff_scratch_bytes(uint64_t M) {
     b += (nt + 2) * sizeof(uint32_t);             // tile counts
     b += (nt + 2) * sizeof(uint64_t);             // tile offsets
     b += scan_scratch_bytes(nt) + 1024;
+    b += (ceil_div(nt, PART_STRIDE) + 2) * sizeof(uint64_t) + 256;  // coarse splits (k_diff_pass1s form)
     return b;
+}
+
+// MKV_DIFF_PART (A/B knob): 1 (default) = 64-ary coarse splits + in-pass tile splits (k_diff_pass1s),
+// 0 = the round-2 binary-search partition + fine partition kernels.
+static int diff_part_variant() {
+    static const int v = [] {
+        const char *e = getenv("MKV_DIFF_PART");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
 }
 
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
@@ -962,9 +1003,20 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
     uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     void *sc = carve(scan_scratch_bytes(nt));
+    const dim3 wg((uint32_t)ceil_div(nt, 4));
+    if (diff_part_variant() == 1) {
+        const uint64_t nc = ceil_div(nt, PART_STRIDE);
+        uint64_t *coarse = reinterpret_cast<uint64_t *>(carve((nc + 2) * sizeof(uint64_t)));
+        hipLaunchKernelGGL(k_diff_coarse, dim3((uint32_t)ceil_div(nc + 1, 4)), dim3(256), 0, st, A, B, nc, coarse);
+        hipLaunchKernelGGL(k_diff_pass1s, wg, dim3(256), 0, st, A, B, coarse, nt, split, packed, tileoff);
+        MKV_LAUNCH_CHECK();
+        exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
+        hipLaunchKernelGGL(k_diff_pass2, wg, dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs);
+        MKV_LAUNCH_CHECK();
+        return;
+    }
     hipLaunchKernelGGL(k_diff_partition, grid1d(ceil_div(nt, PART_STRIDE) + 1), dim3(256), 0, st, A, B, nt, split);
     hipLaunchKernelGGL(k_diff_partition_fine, grid1d(nt), dim3(256), 0, st, A, B, nt, split);
-    const dim3 wg((uint32_t)ceil_div(nt, 4));
     hipLaunchKernelGGL(k_diff_pass1, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt);
     MKV_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);

@@ -31,6 +31,13 @@ constexpr int LEAF_WAVES = 4;                 // waves per workgroup
 // leaf workgroups (144 KiB) leave room on the CU for a sort workgroup running on the aux stream.
 constexpr uint32_t LEAF_LDS_WAVE = 9216;
 
+// Block-count class of a record for the ragged leaf path: min(SHA blocks of its encoding, 32) - 1.
+constexpr uint32_t RG_CLASSES = 32;
+__device__ __forceinline__ uint32_t rg_class(uint64_t klen, uint64_t vlen) {
+    const uint64_t nb = (8 + klen + vlen + 9 + 63) >> 6;
+    return nb >= RG_CLASSES ? RG_CLASSES - 1 : (uint32_t)nb - 1;
+}
+
 // Big-endian word of the 4 bytes at byte offset `off` of an LDS byte region starting at `base` (bytes).
 __device__ __forceinline__ uint32_t lds_be_word(const uint32_t *lds, uint32_t byte) {
     uint32_t a = byte >> 2, sh = byte & 3;
@@ -325,6 +332,8 @@ struct KeyOut {
     uint8_t *kdst;    // null: no copy
     uint64_t *odst;   // null: offsets not copied
     uint64_t kcap;    // bytes available at kdst
+    uint8_t *cls;     // k_leaf_direct: block-count class of every record of a listed chunk (null: none)
+    uint32_t listed_keys_later;  // k_leaf_direct: listed chunks' keys are copied by k_leaf_ragged
 };
 
 template <uint32_t CAP = LEAF_LDS_WAVE>
@@ -684,7 +693,8 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
         if (lane == 0) ctr[4 + c] = fixed ? 0u : 1u;  // chunk flags: listed chunks are hashed afterwards
         if (!fixed) {
             ++listed;
-            if (KO.kdst) {  // key-ownership copy of the chunk's span
+            if (KO.cls && valid) KO.cls[r] = (uint8_t)rg_class(kend - kbeg, vend - vbeg);
+            if (KO.kdst && !KO.listed_keys_later) {  // key-ownership copy of the chunk's span
                 const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
                 if (P.kcopy_end <= KO.kcap) {
                     uint8_t *d = KO.kdst + (P.kstart - kb);
@@ -775,19 +785,13 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
 // The source loads are aligned dwords (16 B at a time), kept inside [floor4(first byte), ceil4(last
 // byte)) of each blob so that reading past a record never leaves the blob's pages.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t RG_CLASSES = 32;
 constexpr uint32_t RG_WIN = 3;                   // blocks materialised per window
 constexpr uint32_t RG_WQ = 4 * RG_WIN;           // uint4 quads per lane per window
 constexpr int RG_WAVES = 4;
 constexpr uint32_t RG_CHUNKS_PER_WG = 16;        // listed chunks per workgroup in the bucketing passes
 
-__device__ __forceinline__ uint32_t rg_class(uint64_t klen, uint64_t vlen) {
-    const uint64_t nb = (8 + klen + vlen + 9 + 63) >> 6;
-    return nb >= RG_CLASSES ? RG_CLASSES - 1 : (uint32_t)nb - 1;
-}
 
-__global__ __launch_bounds__(256) void k_ragged_count(const uint64_t *__restrict__ koff,
-                                                     const uint64_t *__restrict__ voff, uint64_t n,
+__global__ __launch_bounds__(256) void k_ragged_count(const uint8_t *__restrict__ cls, uint64_t n,
                                                      const uint32_t *__restrict__ ctr, uint64_t *__restrict__ wcnt,
                                                      uint32_t nwg) {
     __shared__ uint32_t h[RG_CLASSES];
@@ -801,15 +805,14 @@ __global__ __launch_bounds__(256) void k_ragged_count(const uint64_t *__restrict
             if (c >= nchunks) break;  // uniform per wave
             if (!ctr[4 + c]) continue;
             const uint64_t r = c * 64 + lane;
-            if (r < n) atomicAdd(&h[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u);
+            if (r < n) atomicAdd(&h[cls[r]], 1u);
         }
     }
     __syncthreads();
     if (threadIdx.x < RG_CLASSES) wcnt[(uint64_t)threadIdx.x * nwg + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void k_ragged_scatter(const uint64_t *__restrict__ koff,
-                                                       const uint64_t *__restrict__ voff, uint64_t n,
+__global__ __launch_bounds__(256) void k_ragged_scatter(const uint8_t *__restrict__ cls, uint64_t n,
                                                        const uint32_t *__restrict__ ctr,
                                                        const uint64_t *__restrict__ wbase, uint32_t nwg,
                                                        uint32_t *__restrict__ list) {
@@ -824,7 +827,7 @@ __global__ __launch_bounds__(256) void k_ragged_scatter(const uint64_t *__restri
         if (c >= nchunks) break;
         if (!ctr[4 + c]) continue;
         const uint64_t r = c * 64 + lane;
-        if (r < n) list[atomicAdd(&cur[rg_class(koff[r + 1] - koff[r], voff[r + 1] - voff[r])], 1u)] = (uint32_t)r;
+        if (r < n) list[atomicAdd(&cur[cls[r]], 1u)] = (uint32_t)r;
     }
 }
 
@@ -867,11 +870,11 @@ __device__ __forceinline__ RgField rg_field(const uint8_t *src, uint32_t fw) {
 __device__ __forceinline__ void rg_load16(const RgField &f, uint32_t w, uint32_t w1, const uint8_t *lo,
                                           const uint8_t *hi, uint32_t d[17]) {
     const uint8_t *a = f.A + 4 * (w - f.fw);
-    const uint32_t nw = w <= w1 ? w1 - w + 1 : 0;
+    const uint32_t nw = w <= w1 ? w1 - w + 1 : 0;  // words of this step: they need dwords 0 .. nw
 #pragma unroll
     for (uint32_t g = 0; g < 4; ++g) {
         rg_u32x4 x = {0u, 0u, 0u, 0u};
-        if (4 * g < nw) x = rg_load4(a + 16 * g, lo, hi);
+        if (nw && 4 * g <= nw) x = rg_load4(a + 16 * g, lo, hi);
         d[4 * g] = x.x;
         d[4 * g + 1] = x.y;
         d[4 * g + 2] = x.z;
@@ -890,6 +893,23 @@ __device__ __forceinline__ void rg_store16(const RgField &f, uint32_t w, uint32_
     }
 }
 
+// The key-ownership copy of a ragged record (builds from borrowed buffers): the aligned source dwords
+// just loaded for its key words go to the tree's key store at the same byte offsets. Dwords shared with a
+// neighbouring key carry the same bytes from every writer; none leaves the blob's dword range or kcap.
+__device__ __forceinline__ void rg_copy_out(const RgField &f, uint32_t w, uint32_t w1, const uint32_t d[17],
+                                            const uint8_t *kb, const uint8_t *lo, const uint8_t *hi,
+                                            const KeyOut &KO) {
+    if (w > w1) return;
+    const uint8_t *a = f.A + 4 * (w - f.fw);
+    const uint32_t nd = w1 - w + 2;  // source dwords that carry this step's words
+#pragma unroll
+    for (uint32_t j = 0; j < 17; ++j) {
+        const uint8_t *p = a + 4 * j;
+        if (j < nd && p >= lo && p + 4 <= hi && p >= kb && (uint64_t)(p + 4 - kb) <= KO.kcap)
+            *reinterpret_cast<uint32_t *>(KO.kdst + (p - kb)) = d[j];
+    }
+}
+
 template <bool SHORT>
 __global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__restrict__ kb,
                                                               const uint64_t *__restrict__ koff,
@@ -898,7 +918,8 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__
                                                               uint8_t *__restrict__ out,
                                                               const uint32_t *__restrict__ list,
                                                               const uint64_t *__restrict__ total,
-                                                              uint32_t *__restrict__ gctr, uint32_t grain) {
+                                                              uint32_t *__restrict__ gctr, uint32_t grain,
+                                                              KeyOut KO) {
     __shared__ __attribute__((aligned(16))) uint4 lds_all[RG_WAVES * RG_WQ * 64];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -951,6 +972,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__
                     uint32_t dk[17], dv[17];
                     rg_load16(fk, kw, kw1, klo, khi, dk);
                     rg_load16(fv, vw, vw1, vlo, vhi, dv);
+                    if (KO.kdst) rg_copy_out(fk, kw, kw1, dk, kb, klo, khi, KO);  // key ownership, same offsets
                     rg_store16(fk, kw, kw1, dk, lw, lane, W0);
                     rg_store16(fv, vw, vw1, dv, lw, lane, W0);
                 }
@@ -1010,6 +1032,7 @@ void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uin
 // bucketing scratch: class-major per-workgroup counts (u64), their scan scratch, the list total (u64)
 // and the class-ordered record list (u32 per record).
 struct RaggedScratch {
+    uint8_t *cls;  // block-count class per record (written for listed chunks by k_leaf_direct)
     uint64_t *wcnt;
     void *scan;
     uint64_t *total;
@@ -1032,6 +1055,8 @@ static RaggedScratch ragged_scratch(uint32_t *ctr, uint64_t n, size_t *bytes_out
     off = align16(off + 8);
     R.list = reinterpret_cast<uint32_t *>(base + off);
     off = align16(off + 4 * (size_t)n);
+    R.cls = base + off;
+    off = align16(off + (size_t)n + 64);
     R.nwg = nwg;
     if (bytes_out) *bytes_out = off;
     return R;
@@ -1054,9 +1079,20 @@ static int leaf_ragged_enabled() {
 }
 
 // The listed chunks of ctr (k_leaf_direct): bucket their records by block count, then hash them.
+// MKV_RAGGED_WGS (A/B knob): k_leaf_ragged workgroups per CU (48 KiB of LDS each; default 2 leaves LDS
+// for an ordering workgroup beside them, 3 fills the CU's LDS).
+static int ragged_wgs() {
+    static const int v = [] {
+        const char *e = getenv("MKV_RAGGED_WGS");
+        const int x = e ? atoi(e) : 2;
+        return x < 1 ? 1 : (x > 3 ? 3 : x);
+    }();
+    return v;
+}
+
 template <bool SHORT>
 static void launch_ragged_stage(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff,
-                                uint64_t n, uint8_t *out, uint32_t *ctr, hipStream_t st) {
+                                uint64_t n, uint8_t *out, uint32_t *ctr, const KeyOut &KO, hipStream_t st) {
     static int cus = [] {
         int dev = 0, c = 0;
         (void)hipGetDevice(&dev);
@@ -1065,13 +1101,12 @@ static void launch_ragged_stage(const uint8_t *kb, const uint64_t *koff, const u
     }();
     const RaggedScratch R = ragged_scratch(ctr, n);
     const uint64_t m = (uint64_t)RG_CLASSES * R.nwg;
-    hipLaunchKernelGGL(k_ragged_count, dim3(R.nwg), dim3(256), 0, st, koff, voff, n, ctr, R.wcnt, R.nwg);
+    hipLaunchKernelGGL(k_ragged_count, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.wcnt, R.nwg);
     exclusive_scan_u64(R.wcnt, R.wcnt, m, R.total, R.scan, st);
-    hipLaunchKernelGGL(k_ragged_scatter, dim3(R.nwg), dim3(256), 0, st, koff, voff, n, ctr, R.wcnt, R.nwg, R.list);
-    // 48 KiB of LDS per workgroup: three per CU
-    const uint64_t grid = std::min<uint64_t>((uint64_t)cus * 3, ceil_div(ceil_div(n, 64), RG_WAVES));
+    hipLaunchKernelGGL(k_ragged_scatter, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.wcnt, R.nwg, R.list);
+    const uint64_t grid = std::min<uint64_t>((uint64_t)cus * ragged_wgs(), ceil_div(ceil_div(n, 64), RG_WAVES));
     hipLaunchKernelGGL(k_leaf_ragged<SHORT>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
-                       kb, koff, vb, voff, n, out, R.list, R.total, ctr + 2, 2u);
+                       kb, koff, vb, voff, n, out, R.list, R.total, ctr + 2, 2u, KO);
     MKV_LAUNCH_CHECK();
 }
 
@@ -1126,22 +1161,27 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
         }();
         const uint64_t pblocks = std::min<uint64_t>(blocks, grid3 > 0 ? (uint64_t)grid3 : (uint64_t)cus3 * wgs3);
         const uint32_t grain = std::max<uint32_t>(leaf_dyn_grain(), 1u);
-        // the span copy of listed chunks rounds to 16 B like the staged paths: kb must be 16-B aligned
-        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
+        // the span copy of listed chunks rounds to 16 B like the staged paths: kb must be 16-B aligned. With
+        // the ragged stage, listed chunks' keys are copied by k_leaf_ragged instead (it loads them anyway)
+        const bool rag = leaf_ragged_enabled() != 0;
+        const RaggedScratch R = ragged_scratch(ctr, n);
+        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap,
+                        rag ? R.cls : nullptr, rag ? 1u : 0u};
+        const KeyOut KOr{KO.kdst, nullptr, kcap, nullptr, 0u};
         MKV_HIP(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), st));
         if (leaf_sha_variant() == 0) {
             hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
                                koff, vb, voff, n, out, ctr, grain, KO);
-            if (leaf_ragged_enabled())
-                launch_ragged_stage<false>(kb, koff, vb, voff, n, out, ctr, st);
+            if (rag)
+                launch_ragged_stage<false>(kb, koff, vb, voff, n, out, ctr, KOr, st);
             else
                 hipLaunchKernelGGL(k_leaf_list<false>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
                                    vb, voff, n, out, ctr);
         } else {
             hipLaunchKernelGGL((k_leaf_direct<true, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
                                koff, vb, voff, n, out, ctr, grain, KO);
-            if (leaf_ragged_enabled())
-                launch_ragged_stage<true>(kb, koff, vb, voff, n, out, ctr, st);
+            if (rag)
+                launch_ragged_stage<true>(kb, koff, vb, voff, n, out, ctr, KOr, st);
             else
                 hipLaunchKernelGGL(k_leaf_list<true>, dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
                                    vb, voff, n, out, ctr);
@@ -1165,7 +1205,7 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
         }();
         const uint64_t pblocks = std::min<uint64_t>(blocks, (uint64_t)cus2 * wgs2);
         const uint32_t grain = std::max<uint32_t>(leaf_dyn_grain(), 1u);
-        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
+        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap, nullptr, 0u};
         MKV_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(uint32_t), st));
         if (sha_variant() == 0) {
             hipLaunchKernelGGL((k_leaf_dma<false, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
@@ -1204,7 +1244,7 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
         const uint64_t pblocks = std::min<uint64_t>(blocks, grid > 0 ? (uint64_t)grid : (uint64_t)cus * wgs);
         const uint32_t grain = ctr ? leaf_dyn_grain() : 0;
         // the fused copy needs kb 16-B aligned (same alignment as the destination)
-        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
+        const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap, nullptr, 0u};
         if (grain) {
             MKV_HIP(hipMemsetAsync(ctr, 0, sizeof(uint32_t), st));
             if (sha_variant() == 0)
