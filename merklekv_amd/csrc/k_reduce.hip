@@ -107,6 +107,7 @@ constexpr int RD_TOP_FUSE = 10;
 // level on this latency-bound path).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+template <bool SHORT>
 __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
     __shared__ uint32_t last;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
                 }
             }
             if (pair) {
-                sha_node<true>(l, r, o);
+                sha_node<SHORT>(l, r, o);
             } else {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) o[q] = l[q];  // R5: promote unchanged
@@ -201,7 +202,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
                 r[q] = pair ? src[8 + q] : 0u;
             }
             if (pair) {
-                sha_node<true>(l, r, o);
+                sha_node<SHORT>(l, r, o);
             } else {
 #pragma unroll
                 for (int q = 0; q < 8; ++q) o[q] = l[q];
@@ -430,7 +431,14 @@ void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
 
 void launch_reduce_top(const TopPlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
-    hipLaunchKernelGGL(k_reduce_top, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+    static const int form = [] {  // MKV_TOP_SHA (A/B knob): 1 (default) short-chain rounds, 0 plain
+        const char *e = getenv("MKV_TOP_SHA");
+        return e ? atoi(e) : 1;
+    }();
+    if (form)
+        hipLaunchKernelGGL(k_reduce_top<true>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+    else
+        hipLaunchKernelGGL(k_reduce_top<false>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 
