@@ -489,8 +489,9 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
     return pk;
 }
 
-// Pass 1, one wave per 512-output tile (multi-pass form; k_diff_fused is the default).
-__global__ __launch_bounds__(256) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
+// Pass 1, one wave per 512-output tile (multi-pass form). Pinned to 3 waves per SIMD: the compiler's
+// 170 VGPRs allowed only 2; at 168 (12 B of spills) the 100M mixed pass runs 1.63 instead of 1.82 ms.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, uint32_t *__restrict__ packed,
                                                     uint32_t *__restrict__ tilecnt) {
     __shared__ uint64_t lds[4 * (WTILE + 2)];  // per-wave prefix slices for the general merge
@@ -575,6 +576,21 @@ __device__ __forceinline__ uint64_t fused_split(const DiffSide &A, const DiffSid
     if (hi > A.n) hi = A.n;
     if (hi > d) hi = d;
     if (lo > hi) lo = hi;
+    // One window round around the linear interpolation of the coarse neighbours first: for
+    // near-identical replicas the guess is off by the few inserts / deletes inside the bracket, so the
+    // 32 probes straddle the split and the search ends after one dependent round instead of ~3 (the
+    // 32-ary search alone made pass 1 0.74 ms slower at 100M mixed). A miss narrows the bracket.
+    if (hi - lo > 32) {
+        const uint64_t g = a0 + (uint64_t)((double)(a1 - a0) * (double)(d - d0) / (double)(d1 - d0) + 0.5);
+        uint64_t s = g > lo + 16 ? g - 16 : lo;
+        if (s > hi - 32) s = hi - 32;
+        const uint64_t pp = s + hl, jb = d - 1 - pp;
+        const bool pr = cmp_merge(A, pp, A.pfx[pp], B, jb, B.pfx[jb]) <= 0;
+        const uint32_t cnt = (uint32_t)__popcll((__ballot(pr) >> lane0) & 0xFFFFFFFFull);
+        if (cnt > 0 && cnt < 32) return s + cnt;  // pred(s + cnt - 1) true, pred(s + cnt) false
+        if (cnt == 0) hi = s;                     // pred(s) false: split <= s
+        else lo = s + 32;                         // pred(s + 31) true: split >= s + 32
+    }
     return split_search<32>(A, B, d, lo, hi, hl, lane0);
 }
 
@@ -691,7 +707,7 @@ __global__ __launch_bounds__(64 * DF_WAVES) void k_diff_fused(DiffSide A, DiffSi
 // Pass 1 of the default multi-pass form (round 3): the wave finds its tile's splits itself (32-ary
 // searches between the 64-ary coarse splits, no fine-partition kernel), publishes split[t] (and
 // split[nt]) for pass 2, and writes its divergent count as u64 (the scan's input: no widen kernel).
-__global__ __launch_bounds__(256) void k_diff_pass1s(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_diff_pass1s(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
                                                      uint64_t nt, uint64_t *__restrict__ split,
                                                      uint32_t *__restrict__ packed, uint64_t *__restrict__ tilecnt) {
     __shared__ uint64_t lds[4 * (WTILE + 2)];
@@ -974,12 +990,13 @@ size_t diff_scratch_bytes(uint64_t M) {
     return b;
 }
 
-// MKV_DIFF_PART (A/B knob): 1 (default) = 64-ary coarse splits + in-pass tile splits (k_diff_pass1s),
-// 0 = the round-2 binary-search partition + fine partition kernels.
+// MKV_DIFF_PART (A/B knob): 0 (default) = binary-search partition + fine partition kernels, then pass 1;
+// 1 = 64-ary coarse splits + in-pass tile splits (k_diff_pass1s): the splits lengthen every wave's
+// dependency chain (100M mixed: pass1s 1.85 ms vs 1.70 ms for pass 1 + 0.08 ms of partition kernels).
 static int diff_part_variant() {
     static const int v = [] {
         const char *e = getenv("MKV_DIFF_PART");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 0;
     }();
     return v;
 }

@@ -670,6 +670,8 @@ __device__ __forceinline__ void store_words_a4(uint8_t *p, const uint32_t *w) {
     for (uint32_t i = NW / 4 * 4; i < NW; ++i) reinterpret_cast<uint32_t *>(p)[i] = w[i];
 }
 
+constexpr uint32_t LIST_GRAIN = 32;  // k_leaf_direct: chunks per counter grab once a wave lists
+
 template <bool SHORT, uint32_t K0, uint32_t V0>
 __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                     const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
@@ -686,16 +688,21 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
         const bool valid = r < n;
         const uint64_t kbeg = valid ? koff[r] : 0, kend = valid ? koff[r + 1] : 0;
         const uint64_t vbeg = valid ? voff[r] : 0, vend = valid ? voff[r + 1] : 0;
+        const uint64_t cc = c;
         const uint8_t *kp = kb + kbeg, *vp = vb + vbeg;
         const bool fixed =
             __all(!valid || (kend - kbeg == K0 && vend - vbeg == V0 &&
                              ((reinterpret_cast<uintptr_t>(kp) | reinterpret_cast<uintptr_t>(vp)) & 3) == 0));
-        if (lane == 0) ctr[4 + c] = fixed ? 0u : 1u;  // chunk flags: listed chunks are hashed afterwards
+        if (lane == 0) ctr[4 + cc] = fixed ? 0u : 1u;  // chunk flags: listed chunks are hashed afterwards
         if (!fixed) {
             ++listed;
+            // a listed chunk costs a few stores, so grabs of `grain` chunks would make the shared chunk
+            // counter the bottleneck (same-address atomics serialise in L2: 0.5 ms for 10M ragged
+            // records at grain 4); once this wave lists, it grabs LIST_GRAIN chunks at a time
+            src.grain = LIST_GRAIN;
             if (KO.cls && valid) KO.cls[r] = (uint8_t)rg_class(kend - kbeg, vend - vbeg);
             if (KO.kdst && !KO.listed_keys_later) {  // key-ownership copy of the chunk's span
-                const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
+                const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, cc * 64);
                 if (P.kcopy_end <= KO.kcap) {
                     uint8_t *d = KO.kdst + (P.kstart - kb);
                     const uint64_t span = P.kcopy_end - (uint64_t)(P.kstart - kb);
@@ -1015,6 +1022,199 @@ __global__ __launch_bounds__(64 * RG_WAVES) void k_leaf_ragged(const uint8_t *__
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ragged records, register form (round 3, MKV_LEAF_RAGGED=2): the bucketed list of k_leaf_ragged, but
+// no LDS. Per block each lane loads the 17 aligned source dwords that cover its 16 message words of the
+// key field (stream words 1..b1, key at stream byte 4) and of the value field (stream words b1+1..b3,
+// addressed from vp - (k & 3) so that it starts on a stream word), extracts every word with one v_perm
+// (byte swap + byte offset), picks key or value word by a per-lane compare, and patches the few words
+// that mix fields — b1 (key tail | vlen head), b1+1 (vlen tail | value head), b3 (value tail | 0x80),
+// the words past b3 (zero) and the bit length — only in the blocks where some lane of the wave has them
+// (wave-uniform tests: for a record class these are the first and the last one or two blocks; the
+// middle blocks are plain value words). The next block's source dwords are loaded before the current
+// block is compressed, so their latency hides behind the 64 rounds. Lanes of one chunk share the block
+// count (the list is bucketed by it), except in the open-ended last class, where lanes simply stop.
+// ---------------------------------------------------------------------------------------------
+// Dwords [d0, d1] (0 <= d0, d1 <= 16) of the 17 at a (4-B aligned), zero elsewhere: only the 16-B
+// groups that meet [d0, d1] are loaded (a lane's words of one field rarely fill the block, and every
+// address a wave-wide load carries costs the texture path a cycle). safe: every group this lane can
+// touch lies inside the blob (decided once per record), else each dword is range-checked.
+__device__ __forceinline__ void rr_load17(const uint8_t *a, int32_t d0, int32_t d1, bool safe, const uint8_t *lo,
+                                          const uint8_t *hi, uint32_t d[17]) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        rg_u32x4 x = {0u, 0u, 0u, 0u};
+        const uint8_t *q = a + 16 * g;
+        if (4 * g + 3 >= d0 && 4 * g <= d1) {
+            if (safe) x = *reinterpret_cast<const rg_u32x4 *>(q);
+            else x = rg_load4(q, lo, hi);
+        }
+        d[4 * g] = x.x;
+        d[4 * g + 1] = x.y;
+        d[4 * g + 2] = x.z;
+        d[4 * g + 3] = x.w;
+    }
+    d[16] = 0u;
+    if (d1 >= 16) d[16] = safe ? reinterpret_cast<const uint32_t *>(a)[16] : rg_load1(a + 64, lo, hi);
+}
+
+// One lane's record in the register form: the two field sources and the stream positions of the
+// words that mix fields (b1: key tail | vlen head, b1 + 1: vlen tail | value head, b3: value tail | 0x80).
+struct RrLane {
+    const uint8_t *kp, *ka, *va;  // key start; floor4 of the key field / value field sources
+    uint32_t ksel, vsel;          // v_perm selectors of their byte alignments
+    uint32_t k, v, L, nb, b1, b3;
+    uint32_t hc, vh, vt, he, term;
+    bool ksafe, vsafe;
+};
+
+__device__ __forceinline__ RrLane rr_lane(const uint8_t *kb, const uint8_t *vb, uint64_t k0, uint64_t k1, uint64_t v0,
+                                          uint64_t v1, bool valid, const uint8_t *klo, const uint8_t *khi,
+                                          const uint8_t *vlo, const uint8_t *vhi) {
+    RrLane R;
+    R.k = (uint32_t)(k1 - k0);
+    R.v = (uint32_t)(v1 - v0);
+    R.L = 8 + R.k + R.v;
+    R.nb = valid ? (R.L + 9 + 63) >> 6 : 0u;
+    R.b1 = (4 + R.k) >> 2;
+    R.b3 = R.L >> 2;
+    const uint32_t c4 = R.k & 3, e4 = R.L & 3;
+    R.hc = rg_head_mask(c4);
+    R.vh = R.v >> (8 * c4);
+    R.vt = c4 ? R.v << (32 - 8 * c4) : 0u;
+    R.he = rg_head_mask(e4);
+    R.term = 0x80000000u >> (8 * e4);
+    R.kp = kb + k0;
+    const uint8_t *vq = vb + v0 - c4;
+    R.ka = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(R.kp) & ~uintptr_t(3));
+    R.va = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(vq) & ~uintptr_t(3));
+    R.ksel = 0x00010203u + (uint32_t)(reinterpret_cast<uintptr_t>(R.kp) & 3) * 0x01010101u;
+    R.vsel = 0x00010203u + (uint32_t)(reinterpret_cast<uintptr_t>(vq) & 3) * 0x01010101u;
+    // every group a block can load: key field [ka - 4, ka + 4 b1 + 68), value field
+    // [va - 4 (b1 + 1) + 16 floor((b1 + 1) / 4) - 16, va + 4 (b3 - b1) + 68); generous bounds below
+    R.ksafe = R.ka >= klo + 8 && R.ka + 4 * (uint64_t)R.b1 + 80 <= khi;
+    R.vsafe = R.va >= vlo + 4 * (uint64_t)R.b1 + 24 && R.va + 4 * (uint64_t)(R.b3 - R.b1) + 80 <= vhi;
+    return R;
+}
+
+// Source dwords of block b. Word j of the block (stream word 16b + j) takes dwords j and j + 1 of its
+// field's 17; a field's words in the block are j in [1 (block 0) or 0, tb1] (key) and [tb1 + 1, tb3]
+// (value); the second dword is needed only for a misaligned source.
+__device__ __forceinline__ void rr_fetch(const RrLane &R, uint32_t b, bool fk, bool fv, const uint8_t *klo,
+                                         const uint8_t *khi, const uint8_t *vlo, const uint8_t *vhi, uint32_t dk[17],
+                                         uint32_t dv[17]) {
+    const int32_t tb1 = (int32_t)R.b1 - (int32_t)(16 * b), tb3 = (int32_t)R.b3 - (int32_t)(16 * b);
+    const bool act = R.nb > b;
+    if (fk) {
+        const int32_t j0 = b == 0 ? 1 : 0, j1 = min(tb1, 15);
+        const int32_t d0 = act ? j0 : 99, d1 = act ? j1 + (R.ksel != 0x00010203u) : -1;
+        rr_load17(R.ka + 4 * ((int64_t)(16 * b) - 1), d0, d1, R.ksafe, klo, khi, dk);
+    }
+    if (fv) {
+        const int32_t j0 = max(tb1 + 1, 0), j1 = min(tb3, 15);
+        const int32_t d0 = act ? j0 : 99, d1 = act ? j1 + (R.vsel != 0x00010203u) : -1;
+        rr_load17(R.va + 4 * ((int64_t)(16 * b) - (int64_t)R.b1 - 1), d0, d1, R.vsafe, vlo, vhi, dv);
+    }
+}
+
+// key field present in block b iff b1 >= 16b for some lane; value field iff b3 >= 16b and b1 + 1 <=
+// 16b + 15 for some lane that still has block b
+__device__ __forceinline__ bool rr_need_k(const RrLane &R, uint32_t b) { return __any(R.nb > b && R.b1 >= 16 * b); }
+__device__ __forceinline__ bool rr_need_v(const RrLane &R, uint32_t b) {
+    return __any(R.nb > b && R.b3 >= 16 * b && R.b1 + 1 <= 16 * b + 15);
+}
+
+template <bool SHORT>
+__global__ __launch_bounds__(256) void k_leaf_rreg(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                   const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                   uint64_t n, uint8_t *__restrict__ out,
+                                                   const uint32_t *__restrict__ list, const uint64_t *__restrict__ total,
+                                                   uint32_t *__restrict__ gctr, uint32_t grain, KeyOut KO) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint8_t *klo = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(kb + koff[0]) & ~uintptr_t(3));
+    const uint8_t *khi =
+        reinterpret_cast<const uint8_t *>((reinterpret_cast<uintptr_t>(kb + koff[n]) + 3) & ~uintptr_t(3));
+    const uint8_t *vlo = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(vb + voff[0]) & ~uintptr_t(3));
+    const uint8_t *vhi =
+        reinterpret_cast<const uint8_t *>((reinterpret_cast<uintptr_t>(vb + voff[n]) + 3) & ~uintptr_t(3));
+    const uint64_t T = *total;
+    const uint64_t nch = (T + 63) / 64;
+    if (nch == 0) return;
+    ChunkSource<true> src{0, 0, 0, gctr, grain};
+    for (uint64_t c = src.get(lane); c < nch; c = src.get(lane)) {
+        const uint64_t p = c * 64 + lane;
+        const bool valid = p < T;
+        const uint32_t r = list[valid ? p : c * 64];  // idle lanes shadow the chunk's first record
+        const RrLane R = rr_lane(kb, vb, koff[r], koff[r + 1], voff[r], voff[r + 1], valid, klo, khi, vlo, vhi);
+        uint32_t nbw = R.nb;  // wave-uniform block count
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nbw = max(nbw, (uint32_t)__shfl_xor((int)nbw, o));
+        nbw = __builtin_amdgcn_readfirstlane(nbw);
+        uint32_t dk[17], dv[17];
+        bool fk = rr_need_k(R, 0), fv = rr_need_v(R, 0);
+        rr_fetch(R, 0, fk, fv, klo, khi, vlo, vhi, dk, dv);
+        uint32_t st[8];
+        sha_init(st);
+        for (uint32_t b = 0; b < nbw; ++b) {
+            const int32_t tb1 = (int32_t)R.b1 - (int32_t)(16 * b), tb3 = (int32_t)R.b3 - (int32_t)(16 * b);
+            const bool act = R.nb > b;
+            uint32_t w[16];
+            if (fk && KO.kdst) {  // key ownership: the key dwords just loaded, at the same offsets
+                const uint8_t *a = R.ka + 4 * ((int64_t)(16 * b) - 1);
+                const uint8_t *kend = R.kp + R.k;
+#pragma unroll
+                for (int j = 0; j < 17; ++j) {
+                    const uint8_t *q = a + 4 * j;
+                    if (act && q + 4 > R.kp && q < kend && q >= klo && q >= kb && q + 4 <= khi &&
+                        (uint64_t)(q + 4 - kb) <= KO.kcap)
+                        *reinterpret_cast<uint32_t *>(KO.kdst + (q - kb)) = dk[j];
+                }
+            }
+            if (fk) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const uint32_t kw = rg_be(dk[j + 1], dk[j], R.ksel);
+                    const uint32_t vw = fv ? rg_be(dv[j + 1], dv[j], R.vsel) : 0u;
+                    w[j] = j <= tb1 ? kw : vw;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) w[j] = rg_be(dv[j + 1], dv[j], R.vsel);
+            }
+            if (__any(act && tb1 >= -1 && tb1 <= 15)) {  // b1 / b1 + 1 in this block
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if (j == tb1) w[j] = (w[j] & R.hc) | R.vh;
+                    if (j == tb1 + 1) w[j] = (R.vt & R.hc) | (w[j] & ~R.hc);
+                }
+            }
+            if (b == 0) w[0] = R.k;
+            if (__any(act && tb3 <= 15)) {  // b3 (and the zero tail) in this block
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    if (j == tb3) w[j] = (w[j] & R.he) | R.term;
+                    if (j > tb3) w[j] = 0u;
+                }
+                if (b + 1 == R.nb) w[15] = R.L * 8;  // bit length (L < 2^29: the high word stays 0)
+            }
+            if (b + 1 < nbw) {  // next block's sources in flight during this block's rounds
+                fk = rr_need_k(R, b + 1);
+                fv = rr_need_v(R, b + 1);
+                rr_fetch(R, b + 1, fk, fv, klo, khi, vlo, vhi, dk, dv);
+            }
+            if (act) {
+                uint32_t s2[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) s2[i] = st[i];
+                sha_compress<SHORT>(s2, w);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) st[i] = s2[i];
+            }
+        }
+        if (valid) store_digest(out + 32 * (uint64_t)r, st);
+    }
+}
+
 }  // namespace
 
 void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uint8_t *out, hipStream_t st) {
@@ -1068,8 +1268,8 @@ size_t leaf_ctr_words(uint64_t n) {
     return bytes / 4 + 4;
 }
 
-// MKV_LEAF_RAGGED (A/B knob): 1 (default) = listed chunks go through the bucketed ragged kernel, 0 = the
-// round-2 LDS chunk kernel k_leaf_list.
+// MKV_LEAF_RAGGED (A/B knob): listed chunks go through the bucketed ragged kernels — 1 (default) the LDS
+// form k_leaf_ragged, 2 the register form k_leaf_rreg — or 0: the round-2 LDS chunk kernel k_leaf_list.
 static int leaf_ragged_enabled() {
     static const int v = [] {
         const char *e = getenv("MKV_LEAF_RAGGED");
@@ -1090,6 +1290,16 @@ static int ragged_wgs() {
     return v;
 }
 
+// MKV_RREG_WGS (A/B knob): k_leaf_rreg workgroups (4 waves, no LDS) per CU.
+static int rreg_wgs() {
+    static const int v = [] {
+        const char *e = getenv("MKV_RREG_WGS");
+        const int x = e ? atoi(e) : 4;
+        return x < 1 ? 1 : (x > 8 ? 8 : x);
+    }();
+    return v;
+}
+
 template <bool SHORT>
 static void launch_ragged_stage(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff,
                                 uint64_t n, uint8_t *out, uint32_t *ctr, const KeyOut &KO, hipStream_t st) {
@@ -1104,6 +1314,13 @@ static void launch_ragged_stage(const uint8_t *kb, const uint64_t *koff, const u
     hipLaunchKernelGGL(k_ragged_count, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.wcnt, R.nwg);
     exclusive_scan_u64(R.wcnt, R.wcnt, m, R.total, R.scan, st);
     hipLaunchKernelGGL(k_ragged_scatter, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.wcnt, R.nwg, R.list);
+    if (leaf_ragged_enabled() == 2) {
+        const uint64_t grid = std::min<uint64_t>((uint64_t)cus * rreg_wgs(), ceil_div(ceil_div(n, 64), 4));
+        hipLaunchKernelGGL(k_leaf_rreg<SHORT>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(256), 0, st, kb, koff,
+                           vb, voff, n, out, R.list, R.total, ctr + 2, 2u, KO);
+        MKV_LAUNCH_CHECK();
+        return;
+    }
     const uint64_t grid = std::min<uint64_t>((uint64_t)cus * ragged_wgs(), ceil_div(ceil_div(n, 64), RG_WAVES));
     hipLaunchKernelGGL(k_leaf_ragged<SHORT>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
                        kb, koff, vb, voff, n, out, R.list, R.total, ctr + 2, 2u, KO);

@@ -5,7 +5,7 @@ R=$(pwd)
 mkdir -p "$R/gpurun_out/p3"
 cd /tmp && export TMPDIR=/tmp
 for spec in ${SPECS:-"build:X=1" "ragged:X=1" "mixed:MKV_DIFF_FUSED=1" "mixed:MKV_DIFF_FUSED=0"}; do
-  mode=${spec%%:*}; envs=${spec#*:}; tag=${mode}_${envs//[=,]/_}
+  mode=${spec%%:*}; envs=${spec#*:}; tag=${mode}_${envs//[=,\/]/_}
   env ${envs//,/ } timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/p3/$tag" -o run --output-format csv -- python3 "$R/tools/r03_paths.py" $mode > "$R/gpurun_out/p3/$tag.log" 2>&1; rc=$?
   echo "== $tag rc=$rc"; grep -E "ms/step" "$R/gpurun_out/p3/$tag.log"
   [ $rc -eq 0 ] || { tail -20 "$R/gpurun_out/p3/$tag.log"; exit $rc; }

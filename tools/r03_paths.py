@@ -56,6 +56,26 @@ def main():
             t = MerkleTree()
             ms = timed(lambda: t.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n), steps)
             print(f"ragged build 10M: {ms:.3f} ms/step", flush=True)
+        elif mode in ("vo", "ident"):
+            # merge-join over equal key sets (run with MKV_DIFF_TOPDOWN=0): "vo" = 0.1 % changed values
+            # (aligned tiles + digest mismatches), "ident" = identical replicas (pure streaming)
+            n = 100_000_000
+            kb, ko, vb, vo = recs(n)
+            A = MerkleTree()
+            A.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+            if mode == "vo":
+                g = torch.Generator(device="cuda")
+                g.manual_seed(12)
+                idx = torch.randperm(n, device="cuda", generator=g)[: n // 1000]
+                vv = vb[: n * V].view(n, V)
+                vv[idx, 0] ^= 1
+            torch.cuda.synchronize()
+            B = MerkleTree()
+            B.build_device(kb.data_ptr(), ko.data_ptr(), vb.data_ptr(), vo.data_ptr(), n)
+            del kb, vb
+            torch.cuda.empty_cache()
+            ms = timed(lambda: A.diff_keys_view(B), steps)
+            print(f"{mode} merge diff 100M: {ms:.3f} ms/step ({len(A.diff_keys_view(B))} keys)", flush=True)
         elif mode == "mixed":
             n = 100_000_000
             kb, ko, vb, vo = recs(n)
