@@ -33,6 +33,11 @@ constexpr uint32_t LEAF_LDS_WAVE = 9216;
 
 // Block-count class of a record for the ragged leaf path: min(SHA blocks of its encoding, 32) - 1.
 constexpr uint32_t RG_CLASSES = 32;
+// Counter block layout (leaf_ctr_words): [0] leaf chunk counter, [1] listed chunks, [2] ragged chunk
+// counter, [3] spare, [CTR_CLS, +32) listed records per block-count class (k_leaf_direct),
+// [CTR_CUR, +32) class cursors (k_ragged_scatter), [CTR_FLAGS ..) one listed flag per chunk. The head
+// (CTR_FLAGS words) is zeroed before every leaf stage.
+constexpr uint32_t CTR_CLS = 4, CTR_CUR = CTR_CLS + RG_CLASSES, CTR_FLAGS = CTR_CUR + RG_CLASSES;
 __device__ __forceinline__ uint32_t rg_class(uint64_t klen, uint64_t vlen) {
     const uint64_t nb = (8 + klen + vlen + 9 + 63) >> 6;
     return nb >= RG_CLASSES ? RG_CLASSES - 1 : (uint32_t)nb - 1;
@@ -517,7 +522,7 @@ __global__ __launch_bounds__(256) void k_leaf_persist(const uint8_t *__restrict_
 // free again before the compressions start and the DMA of the next chunk lands behind them. Without the
 // 36 prefetch VGPRs and with 8.5 KiB of LDS per wave, three workgroups per CU fit beside an ordering
 // workgroup (3 x 34 KiB + 55 KiB <= 160 KiB; 101 VGPRs). Chunks of any other shape are only listed
-// (ctr[1] = count, ctr[4..] = chunk ids) and hashed by k_leaf_list right after, so the general paths'
+// (ctr[1] = count, ctr[CTR_FLAGS..] = chunk flags) and hashed by k_leaf_list right after, so the general paths'
 // registers do not weigh on this kernel.
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t LEAF_LDS_DMA = 8704;  // 64 x 132-B records + 2 x 16-B alignment slack + 32
@@ -592,7 +597,7 @@ __global__ __launch_bounds__(256) void k_leaf_dma(const uint8_t *__restrict__ kb
         const uint32_t kbyte = (uint32_t)((kb + kbeg) - P.kstart);
         const uint32_t vbyte = P.kspan + (uint32_t)((vb + vbeg) - P.vstart);
         const bool fixed = P.staged && __all(!valid || (klen == K0 && vlen == V0 && ((kbyte | vbyte) & 3) == 0));
-        if (lane == 0) ctr[4 + c] = fixed ? 0u : 1u;  // chunk flags for k_leaf_list
+        if (lane == 0) ctr[CTR_FLAGS + c] = fixed ? 0u : 1u;  // chunk flags for k_leaf_list
         if (!fixed && lane == 0) atomicAdd(&ctr[1], 1u);
         uint32_t m[MW];
         if (fixed) {
@@ -679,7 +684,10 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
                                                     uint32_t grain, KeyOut KO) {
     using Sh = LeafShape<K0, V0>;
     constexpr uint32_t MW = Sh::kw + Sh::vw;
+    __shared__ uint32_t hist_all[4][RG_CLASSES];  // per wave: listed records per block-count class
     const uint32_t lane = threadIdx.x & 63;
+    uint32_t *hist = hist_all[(threadIdx.x >> 6) & 3];
+    if (lane < RG_CLASSES) hist[lane] = 0;
     const uint64_t nchunks = (n + 63) / 64;
     ChunkSource<true> src{0, 0, 0, ctr, grain};
     uint32_t listed = 0;  // this wave's listed chunks: one atomic at the end, not one per chunk
@@ -693,14 +701,18 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
         const bool fixed =
             __all(!valid || (kend - kbeg == K0 && vend - vbeg == V0 &&
                              ((reinterpret_cast<uintptr_t>(kp) | reinterpret_cast<uintptr_t>(vp)) & 3) == 0));
-        if (lane == 0) ctr[4 + cc] = fixed ? 0u : 1u;  // chunk flags: listed chunks are hashed afterwards
+        if (lane == 0) ctr[CTR_FLAGS + cc] = fixed ? 0u : 1u;  // chunk flags: listed chunks are hashed afterwards
         if (!fixed) {
             ++listed;
             // a listed chunk costs a few stores, so grabs of `grain` chunks would make the shared chunk
             // counter the bottleneck (same-address atomics serialise in L2: 0.5 ms for 10M ragged
             // records at grain 4); once this wave lists, it grabs LIST_GRAIN chunks at a time
             src.grain = LIST_GRAIN;
-            if (KO.cls && valid) KO.cls[r] = (uint8_t)rg_class(kend - kbeg, vend - vbeg);
+            if (KO.cls && valid) {
+                const uint32_t k = rg_class(kend - kbeg, vend - vbeg);
+                KO.cls[r] = (uint8_t)k;
+                atomicAdd(&hist[k], 1u);
+            }
             if (KO.kdst && !KO.listed_keys_later) {  // key-ownership copy of the chunk's span
                 const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, cc * 64);
                 if (P.kcopy_end <= KO.kcap) {
@@ -733,6 +745,10 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
         store_digest(out + 32 * r, st);
     }
     if (listed && lane == 0) atomicAdd(&ctr[1], listed);
+    if (listed && KO.cls && lane < RG_CLASSES) {  // the wave's class counts into the block totals
+        const uint32_t h = hist[lane];
+        if (h) atomicAdd(&ctr[CTR_CLS + lane], h);
+    }
 }
 
 // The chunks k_leaf_dma / k_leaf_direct listed (any shape but the fixed one): one wave per listed chunk, staged through
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
     if (ctr[1] == 0) return;
     const uint64_t nchunks = (n + 63) / 64;
     for (uint64_t c = (uint64_t)blockIdx.x * LEAF_WAVES + wave; c < nchunks; c += (uint64_t)gridDim.x * LEAF_WAVES) {
-        if (!ctr[4 + c]) continue;  // flagged by k_leaf_direct / k_leaf_dma
+        if (!ctr[CTR_FLAGS + c]) continue;  // flagged by k_leaf_direct / k_leaf_dma
         const ChunkPlan P = plan_chunk(kb, koff, vb, voff, n, c * 64);
         if (P.staged) {
             uint4 R[PF];
@@ -795,46 +811,61 @@ __global__ __launch_bounds__(256) void k_leaf_list(const uint8_t *__restrict__ k
 constexpr uint32_t RG_WIN = 3;                   // blocks materialised per window
 constexpr uint32_t RG_WQ = 4 * RG_WIN;           // uint4 quads per lane per window
 constexpr int RG_WAVES = 4;
-constexpr uint32_t RG_CHUNKS_PER_WG = 16;        // listed chunks per workgroup in the bucketing passes
+constexpr uint32_t RG_SCATTER_CHUNKS = 256;      // listed chunks per workgroup of k_ragged_scatter
 
 
-__global__ __launch_bounds__(256) void k_ragged_count(const uint8_t *__restrict__ cls, uint64_t n,
-                                                     const uint32_t *__restrict__ ctr, uint64_t *__restrict__ wcnt,
-                                                     uint32_t nwg) {
-    __shared__ uint32_t h[RG_CLASSES];
-    if (threadIdx.x < RG_CLASSES) h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t nchunks = (n + 63) / 64;
-    if (ctr[1]) {
-        for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
-            const uint64_t c = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
-            if (c >= nchunks) break;  // uniform per wave
-            if (!ctr[4 + c]) continue;
-            const uint64_t r = c * 64 + lane;
-            if (r < n) atomicAdd(&h[cls[r]], 1u);
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < RG_CLASSES) wcnt[(uint64_t)threadIdx.x * nwg + blockIdx.x] = h[threadIdx.x];
-}
-
+// Bucketing of the listed records by class, one launch: the class totals came from k_leaf_direct, so a
+// workgroup takes its classes' bases from their exclusive scan (32 values) plus one atomic per class on
+// the class cursors, then scatters its records through LDS cursors. RG_SCATTER_CHUNKS chunks per
+// workgroup keep those same-address atomics few (at 16 chunks per workgroup they serialised to
+// 0.44 ms for 10M ragged records). Order inside a class is arbitrary
+// (every digest goes to its own record's slot).
 __global__ __launch_bounds__(256) void k_ragged_scatter(const uint8_t *__restrict__ cls, uint64_t n,
-                                                       const uint32_t *__restrict__ ctr,
-                                                       const uint64_t *__restrict__ wbase, uint32_t nwg,
+                                                       uint32_t *__restrict__ ctr, uint64_t *__restrict__ total,
                                                        uint32_t *__restrict__ list) {
     __shared__ uint32_t cur[RG_CLASSES];
-    if (threadIdx.x < RG_CLASSES) cur[threadIdx.x] = (uint32_t)wbase[(uint64_t)threadIdx.x * nwg + blockIdx.x];
+    if (ctr[1] == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *total = 0;
+        return;
+    }
+    if (threadIdx.x < RG_CLASSES) cur[threadIdx.x] = 0;
     __syncthreads();
-    if (ctr[1] == 0) return;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t nchunks = (n + 63) / 64;
-    for (uint32_t q = 0; q < RG_CHUNKS_PER_WG / 4; ++q) {
-        const uint64_t c = (uint64_t)blockIdx.x * RG_CHUNKS_PER_WG + wave * (RG_CHUNKS_PER_WG / 4) + q;
-        if (c >= nchunks) break;
-        if (!ctr[4 + c]) continue;
-        const uint64_t r = c * 64 + lane;
-        if (r < n) list[atomicAdd(&cur[cls[r]], 1u)] = (uint32_t)r;
+    // each wave takes RG_SCATTER_CHUNKS / 4 consecutive chunks, 8 at a time with their flags and
+    // classes loaded together (one memory latency per 8 chunks)
+    const uint64_t c0 = (uint64_t)blockIdx.x * RG_SCATTER_CHUNKS + wave * (RG_SCATTER_CHUNKS / 4);
+    for (uint32_t q = 0; q < RG_SCATTER_CHUNKS / 4; q += 8) {
+        uint32_t k[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t c = c0 + q + u, r = c * 64 + lane;
+            k[u] = (c < nchunks && r < n && ctr[CTR_FLAGS + c]) ? cls[r] : RG_CLASSES;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (k[u] < RG_CLASSES) atomicAdd(&cur[k[u]], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < RG_CLASSES) {
+        const uint32_t k = threadIdx.x;
+        uint32_t cb = 0;
+        for (uint32_t j = 0; j < k; ++j) cb += ctr[CTR_CLS + j];
+        const uint32_t cnt = cur[k];
+        cur[k] = cb + (cnt ? atomicAdd(&ctr[CTR_CUR + k], cnt) : 0u);
+        if (blockIdx.x == 0 && k == RG_CLASSES - 1) *total = (uint64_t)cb + ctr[CTR_CLS + k];
+    }
+    __syncthreads();
+    for (uint32_t q = 0; q < RG_SCATTER_CHUNKS / 4; q += 8) {
+        uint32_t k[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const uint64_t c = c0 + q + u, r = c * 64 + lane;
+            k[u] = (c < nchunks && r < n && ctr[CTR_FLAGS + c]) ? cls[r] : RG_CLASSES;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (k[u] < RG_CLASSES) list[atomicAdd(&cur[k[u]], 1u)] = (uint32_t)((c0 + q + u) * 64 + lane);
     }
 }
 
@@ -1227,14 +1258,11 @@ void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uin
     MKV_LAUNCH_CHECK();
 }
 
-// The counter block (leaf_ctr_words): [0] k_leaf_direct's chunk counter, [1] listed chunks, [2]
-// k_leaf_ragged's chunk counter, [3] spare, [4 ..) listed chunk ids; then, 16-B aligned, the ragged
-// bucketing scratch: class-major per-workgroup counts (u64), their scan scratch, the list total (u64)
-// and the class-ordered record list (u32 per record).
+// The counter block (leaf_ctr_words): the head described at CTR_FLAGS, one flag per chunk; then, 16-B
+// aligned, the ragged bucketing scratch: the list total (u64), the class-ordered record list (u32 per
+// record) and the block-count class of every record (u8).
 struct RaggedScratch {
     uint8_t *cls;  // block-count class per record (written for listed chunks by k_leaf_direct)
-    uint64_t *wcnt;
-    void *scan;
     uint64_t *total;
     uint32_t *list;
     uint32_t nwg;
@@ -1242,15 +1270,10 @@ struct RaggedScratch {
 static size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 static RaggedScratch ragged_scratch(uint32_t *ctr, uint64_t n, size_t *bytes_out = nullptr) {
     const uint64_t nch = (n + 63) / 64;
-    const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(nch, RG_CHUNKS_PER_WG));
-    const uint64_t m = (uint64_t)RG_CLASSES * nwg;
-    size_t off = align16(4 * (4 + (size_t)nch));
+    const uint32_t nwg = (uint32_t)std::max<uint64_t>(1, ceil_div(nch, RG_SCATTER_CHUNKS));
+    size_t off = align16(4 * (CTR_FLAGS + (size_t)nch));
     RaggedScratch R;
     uint8_t *base = reinterpret_cast<uint8_t *>(ctr);
-    R.wcnt = reinterpret_cast<uint64_t *>(base + off);
-    off = align16(off + 8 * m);
-    R.scan = base + off;
-    off = align16(off + scan_scratch_bytes(m));
     R.total = reinterpret_cast<uint64_t *>(base + off);
     off = align16(off + 8);
     R.list = reinterpret_cast<uint32_t *>(base + off);
@@ -1310,10 +1333,7 @@ static void launch_ragged_stage(const uint8_t *kb, const uint64_t *koff, const u
         return c > 0 ? c : 256;
     }();
     const RaggedScratch R = ragged_scratch(ctr, n);
-    const uint64_t m = (uint64_t)RG_CLASSES * R.nwg;
-    hipLaunchKernelGGL(k_ragged_count, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.wcnt, R.nwg);
-    exclusive_scan_u64(R.wcnt, R.wcnt, m, R.total, R.scan, st);
-    hipLaunchKernelGGL(k_ragged_scatter, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.wcnt, R.nwg, R.list);
+    hipLaunchKernelGGL(k_ragged_scatter, dim3(R.nwg), dim3(256), 0, st, R.cls, n, ctr, R.total, R.list);
     if (leaf_ragged_enabled() == 2) {
         const uint64_t grid = std::min<uint64_t>((uint64_t)cus * rreg_wgs(), ceil_div(ceil_div(n, 64), 4));
         hipLaunchKernelGGL(k_leaf_rreg<SHORT>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(256), 0, st, kb, koff,
@@ -1385,7 +1405,7 @@ bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
         const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap,
                         rag ? R.cls : nullptr, rag ? 1u : 0u};
         const KeyOut KOr{KO.kdst, nullptr, kcap, nullptr, 0u};
-        MKV_HIP(hipMemsetAsync(ctr, 0, 4 * sizeof(uint32_t), st));
+        MKV_HIP(hipMemsetAsync(ctr, 0, CTR_FLAGS * sizeof(uint32_t), st));
         if (leaf_sha_variant() == 0) {
             hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3((uint32_t)pblocks), dim3(64 * LEAF_WAVES), 0, st, kb,
                                koff, vb, voff, n, out, ctr, grain, KO);

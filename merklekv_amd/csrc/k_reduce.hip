@@ -93,14 +93,12 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
 }
 
 // ---- top of the tree (round 3): every level from a <= 64-tile level to the root in ONE launch ----
-// Phase 1: each workgroup fuses up to RD_TOP_FUSE levels of its 512-parent tile in LDS (the tile's
+// Phase 1: each workgroup fuses up to 10 levels of its 512-parent tile in LDS (the tile's
 // subtree collapses to one node after 10 levels). Phase 2: the last workgroup to finish (agent-scope
 // arrival counter; it resets the counter for the next launch) reads the <= ntiles + 2 nodes the tiles
 // produced and climbs the remaining levels alone, in LDS. One cross-workgroup hand-off instead of one
 // kernel launch (and its drain / ramp) per 4 levels: the top of a 10M-key tree was three launches of
 // ~34 us each, almost all latency (a few hundred nodes per level, 2 dependent compressions per node).
-// The short-chain SHA form (latency) is used throughout.
-constexpr int RD_TOP_FUSE = 10;
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
 // stores (__syncthreads' release fence also drains the level's HBM stores, one memory round trip per
@@ -431,9 +429,12 @@ void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
 
 void launch_reduce_top(const TopPlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
-    static const int form = [] {  // MKV_TOP_SHA (A/B knob): 1 (default) short-chain rounds, 0 plain
+    // MKV_TOP_SHA (A/B knob): 0 (default) plain rounds, 1 short-chain rounds. One wave per SIMD is
+    // bound by its own issue rate (~4 cycles per VALU instruction), not by the round's dependency
+    // chain, so the form with fewer instructions wins even here (10M build: 110 vs 116 us).
+    static const int form = [] {
         const char *e = getenv("MKV_TOP_SHA");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 0;
     }();
     if (form)
         hipLaunchKernelGGL(k_reduce_top<true>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
