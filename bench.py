@@ -823,6 +823,7 @@ def wl_incremental(ctx, args):
     diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))  # batched walk: per-pair share
     climb_ms = variants[0].prof_read("climb")[0] / args.steps      # shared dirty climb, all replicas
     walk_ms = base.prof_read("walk")[0] / args.steps               # shared 1-vs-(R-1) walk launches
+    d2h_ms = base.prof_read("d2h")[0] / (args.steps * (R - 1))     # key lists into pinned host memory
     for t in [base] + variants:
         t.prof_enable(False)
     # work of the last step (stats of the last update / walk; every step does the same amount)
@@ -862,6 +863,8 @@ def wl_incremental(ctx, args):
         out["incremental"] = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
                               "update_device_ms_all_replicas": upd_ms, "diff_device_ms_per_pair": diff_ms,
                               "climb_device_ms": climb_ms, "walk_device_ms_per_pair": walk_ms / (R - 1),
+                              "keys_d2h_ms_per_pair": d2h_ms,
+                              "diff_device_ms_per_pair_excl_d2h": diff_ms - d2h_ms,
                               "diff_sizes_match_unique_updates": ok,
                               "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
         out["cpu_baseline"] = None if (args.no_cpu_baseline or ctx.world > 1) else cpu_baseline_update()

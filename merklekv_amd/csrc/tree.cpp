@@ -2117,8 +2117,10 @@ static void keylist_fill(mkv_tree *t, mkv_keylist *l, const uint64_t *d_off, con
     l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
     uint64_t *ho = reinterpret_cast<uint64_t *>(l->blk->p);
     uint8_t *hb = l->blk->p + kpos;
+    const size_t ph = prof_begin(t, "d2h", t->st);  // the PCIe part of a key list (profiling only)
     copy_to_host(d_off, l->blk->dp, (m + 1) * 8, t->st);
     copy_to_host(d_bytes, l->blk->dp + kpos, bytes, t->st);
+    prof_end(t, ph);
     l->offsets = ho;
     l->bytes = hb;
 }
