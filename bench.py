@@ -5,10 +5,12 @@ Default workload (`--workload build`, what the driver runs): a step = one full t
 + key ordering + dedup + gathers + level reduction + root readback) over n synthetic records (32-B
 keys, 100-B values, generated on the device, already resident in HBM when the timed region starts).
 N=1: n = 10M (configs[1]). N>1 ranks (torch.distributed.run, one process per GPU): each rank owns a
-contiguous key range of 125M records by default, so N=8 is configs[3] (1B keys over 8 GPUs; weak
-scaling); the step adds the RCCL all-gathers of shard leaf counts and seam fringes (device-resident
-buffers) and the on-device seam combine that yields the global root on every rank. The N=1 line also
-carries `anchor_125m` (the same build at 125M keys on one GPU: the per-GPU anchor of that curve),
+contiguous key range of the same 10M records per rank (weak scaling: equal work per GPU at every N, so
+the driver's per-N values compare directly); the step adds the RCCL all-gathers of shard leaf counts
+and seam fringes (device-resident buffers) and the on-device seam combine that yields the global root on
+every rank. The N>1 line also carries `sharded_125m_per_rank` (the same sharded build at 125M records
+per rank: configs[3] = 1B keys at N=8) and `diff_sharded`; the N=1 line carries `anchor_125m` (125M
+keys on one GPU: the per-GPU anchor of the 125M-per-rank curve),
 `diff_100m` (configs[2], both divergence modes, exactness vs construction), `configs0` (the 100K CPU
 config on the GPU) and the CPU baselines (cpu_ref: the reference's data structures, single thread;
 cpu_mt: all host cores).
@@ -337,6 +339,30 @@ def anchor_block(ctx, n, steps=5, warmup=2):
     return out
 
 
+def sharded_anchor_block(ctx, n, steps=5, warmup=2):
+    """N>1: the sharded build at n keys per rank (125M: configs[3], 1B keys over 8 ranks), timed like the
+    default step (barriers, max over ranks). The N=1 point of the same per-rank size is anchor_125m."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    kb, ko, vb, vo = ctx.records(n)
+    t = MerkleTree(ctx.local)
+    root, N = ctx.build(t, kb, ko, vb, vo, n, validate=True)
+    for _ in range(warmup - 1):
+        root, N = ctx.build(t, kb, ko, vb, vo, n, validate=False)
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        root, N = ctx.build(t, kb, ko, vb, vo, n, validate=False)
+    ctx.barrier()
+    el = ctx.max_over_ranks(time.perf_counter() - t0)
+    ctx.check_roots_agree(root)
+    out = {"keys_per_rank": n, "global_keys": N, "ranks": ctx.world, "steps": steps,
+           "ms_per_step": el / steps * 1e3, "leaves_per_s": N * steps / el, "root": root.hex() if root else None}
+    del t, kb, vb
+    torch.cuda.empty_cache()
+    return out
+
+
 def route_block(ctx, n, reps=2):
     """n unpartitioned records per rank (keys from the whole key space) -> sampled
     splitters -> one all-to-all -> key-range shards -> sharded build. Reports the redistribution time
@@ -589,6 +615,9 @@ def wl_build(ctx, args):
         torch.cuda.empty_cache()
         if args.anchor_records:
             anchor = anchor_block(ctx, args.anchor_records)
+    c3 = None
+    if not args.no_diff and ctx.dist is not None and args.anchor_records:
+        c3 = sharded_anchor_block(ctx, args.anchor_records)
 
     route = None
     if args.route_records and ctx.dist is not None:
@@ -600,7 +629,8 @@ def wl_build(ctx, args):
 
     if ctx.rank == 0:
         wl = ("configs[1]: 10M keys x 1 MI355X, 32-B keys / 100-B values" if n == 10_000_000 and ctx.world == 1
-              else f"{n} keys per rank x {ctx.world} GPUs (configs[3] = 125M x 8 ranks = 1B keys), 32-B keys / 100-B values")
+              else f"{n} keys per rank x {ctx.world} GPUs (configs[1] per rank, key-range shards; configs[3] = "
+                   f"125M x 8 ranks in sharded_125m_per_rank), 32-B keys / 100-B values")
         out = base_line(ctx, args, "Merkle build leaves/s (full tree: hash+sort+reduce)", value,
                         "leaves/s", ms_per_step, wl)
         out["root"] = root.hex() if root else None
@@ -618,6 +648,7 @@ def wl_build(ctx, args):
         if ctx.dist is not None:
             out["diff_sharded"] = dN
             out["collectives_build"] = coll
+            out["sharded_125m_per_rank"] = c3  # configs[3] at N = 8 (1B keys); N = 1 point: anchor_125m
         if route is not None:
             out["route"] = route
         out["cpu_baseline"] = cpu
@@ -1075,7 +1106,8 @@ def main():
     ap.add_argument("--no-diff", action="store_true", help="build workload: skip the secondary blocks")
     ap.add_argument("--diff-records", type=int, default=100_000_000, help="build workload: diff_100m keys")
     ap.add_argument("--anchor-records", type=int, default=125_000_000,
-                    help="build workload at N=1: anchor build size (0 = skip)")
+                    help="build workload: the 125M-per-GPU block (N=1 anchor_125m, N>1 sharded_125m_per_rank; "
+                         "0 = skip)")
     ap.add_argument("--route-records", type=int, default=None,
                     help="build workload with a process group: also time the all-to-all redistribution of "
                          "this many unpartitioned records per rank (SURVEY 8f-3; default 10M at N>1; 0 = skip)")
@@ -1090,9 +1122,9 @@ def main():
     if args.route_records is None:
         args.route_records = 10_000_000 if int(os.environ.get("WORLD_SIZE", "1")) > 1 else 0
     if args.n is None:
-        multi = int(os.environ.get("WORLD_SIZE", "1")) > 1
-        args.n = {"build": 125_000_000 if multi else 10_000_000, "diff": 100_000_000,
-                  "incremental": 125_000_000}[args.workload]
+        # the same work per rank at every N (weak scaling against the N = 1 line); the 125M-per-rank
+        # sharded build (configs[3] at N = 8) is the sharded_125m_per_rank block of the N > 1 line
+        args.n = {"build": 10_000_000, "diff": 100_000_000, "incremental": 125_000_000}[args.workload]
     ctx = Ctx()
     {"build": wl_build, "diff": wl_diff, "incremental": wl_incremental}[args.workload](ctx, args)
     ctx.finish()
