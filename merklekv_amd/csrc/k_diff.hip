@@ -363,36 +363,73 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
     uint32_t nd = 0, pk = 0;
     bool general = true;
     if (na == nb) {
-        // slot q of lane l holds pair x = l + 64 q (q < 4); B[b0 + 256] and A[a0 - 1] are wave-uniform
-        // (scalar loads)
-        uint64_t pA[4], pB[4];
-        uint4 dA[4][2], dB[4][2];
+        // slot q of lane l holds pair x = l + 64 q (q < 4), in two halves (q = 0, 1 then 2, 3) so that
+        // only half of the tile's prefixes and digests are in registers at once; the phase-1 partner of
+        // lane 63's last slot in a half is B[b0 + 128 (h + 1)] (loaded as the half's end element)
+        uint64_t pA[4];
+        bool ok0 = true, ok1 = true;
+        uint32_t eq0 = 0, eq1 = 0;
+        const int src = (int)((lane + 1) & 63);
+        uint4 dB00[2];  // B[b0]'s digest (lane 0's slot 0): the phase-1 partner of A[a0 - 1]
+        uint64_t pB00 = ~0ull;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t x = lane + 64 * q;
-            pA[q] = 0;
-            pB[q] = ~0ull;
-            dA[q][0] = dA[q][1] = dB[q][0] = dB[q][1] = make_uint4(0, 0, 0, 0);
-            if (x < na) {
-                pA[q] = A.pfx[c.a0 + x];
-                const uint4 *p = reinterpret_cast<const uint4 *>(A.dig + 32 * (c.a0 + x));
-                dA[q][0] = p[0];
-                dA[q][1] = p[1];
+        for (int h = 0; h < 2; ++h) {
+            uint64_t pB[2];
+            uint4 dA[2][2], dB[2][2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = 2 * h + u;
+                const uint64_t x = lane + 64 * q;
+                pA[q] = 0;
+                pB[u] = ~0ull;
+                dA[u][0] = dA[u][1] = dB[u][0] = dB[u][1] = make_uint4(0, 0, 0, 0);
+                if (x < na) {
+                    pA[q] = A.pfx[c.a0 + x];
+                    const uint4 *p = reinterpret_cast<const uint4 *>(A.dig + 32 * (c.a0 + x));
+                    dA[u][0] = p[0];
+                    dA[u][1] = p[1];
+                }
+                if (x <= nb && c.b0 + x < B.n) {
+                    pB[u] = B.pfx[c.b0 + x];
+                    const uint4 *p = reinterpret_cast<const uint4 *>(B.dig + 32 * (c.b0 + x));
+                    dB[u][0] = p[0];
+                    dB[u][1] = p[1];
+                }
             }
-            if (x <= nb && c.b0 + x < B.n) {
-                pB[q] = B.pfx[c.b0 + x];
-                const uint4 *p = reinterpret_cast<const uint4 *>(B.dig + 32 * (c.b0 + x));
-                dB[q][0] = p[0];
-                dB[q][1] = p[1];
+            const uint64_t xe = 128ull * (h + 1);
+            uint64_t pEnd = ~0ull;
+            uint4 dEnd[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+            if (xe <= nb && c.b0 + xe < B.n) {
+                pEnd = B.pfx[c.b0 + xe];
+                const uint4 *p = reinterpret_cast<const uint4 *>(B.dig + 32 * (c.b0 + xe));
+                dEnd[0] = p[0];
+                dEnd[1] = p[1];
             }
-        }
-        uint64_t pEnd = ~0ull;  // B[b0 + 256]
-        uint4 dEnd[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-        if (nb == 256 && c.b0 + 256 < B.n) {
-            pEnd = B.pfx[c.b0 + 256];
-            const uint4 *p = reinterpret_cast<const uint4 *>(B.dig + 32 * (c.b0 + 256));
-            dEnd[0] = p[0];
-            dEnd[1] = p[1];
+            if (h == 0) {
+                dB00[0] = dB[0][0];
+                dB00[1] = dB[0][1];
+                pB00 = pB[0];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int q = 2 * h + u;
+                const uint64_t x = lane + 64 * q;
+                const uint64_t pn = shfl_u64(pB[u], src), pw = u < 1 ? shfl_u64(pB[u + 1], 0) : pEnd;
+                const uint4 n0 = shfl_u4(dB[u][0], src), n1 = shfl_u4(dB[u][1], src);
+                const uint4 w0 = u < 1 ? shfl_u4(dB[u + 1][0], 0) : dEnd[0];
+                const uint4 w1 = u < 1 ? shfl_u4(dB[u + 1][1], 0) : dEnd[1];
+                const uint64_t pN = lane == 63 ? pw : pn;
+                const bool e0 = u4eq(dA[u][0], dB[u][0]) && u4eq(dA[u][1], dB[u][1]);
+                const bool e1 = lane == 63 ? (u4eq(dA[u][0], w0) && u4eq(dA[u][1], w1))
+                                           : (u4eq(dA[u][0], n0) && u4eq(dA[u][1], n1));
+                if (x < na) {
+                    ok0 &= pA[q] == pB[u];
+                    ok1 &= (c.b0 + x + 1 < B.n) && pA[q] == pN;
+                }
+                eq0 |= (uint32_t)e0 << q;
+                eq1 |= (uint32_t)e1 << q;
+            }
+            asm volatile("" ::: "memory");  // keep the second half's loads behind the first half's use
         }
         uint64_t pPrev = 0;  // A[a0-1], the phase-1 partner of B[b0]
         uint4 dPrev[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
@@ -402,31 +439,9 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
             dPrev[0] = p[0];
             dPrev[1] = p[1];
         }
-        // phase-1 partner of pair x is B[b0 + x + 1]: lane l+1's slot q, or lane 0's slot q+1 for lane 63.
-        // Digest equality is evaluated for both phases right away, so only flags stay live.
-        const int src = (int)((lane + 1) & 63);
-        bool ok0 = true, ok1 = true;
-        uint32_t eq0 = 0, eq1 = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint64_t x = lane + 64 * q;
-            const uint64_t pn = shfl_u64(pB[q], src), pw = q < 3 ? shfl_u64(pB[q + 1], 0) : pEnd;
-            const uint4 n0 = shfl_u4(dB[q][0], src), n1 = shfl_u4(dB[q][1], src);
-            const uint4 w0 = q < 3 ? shfl_u4(dB[q + 1][0], 0) : dEnd[0];
-            const uint4 w1 = q < 3 ? shfl_u4(dB[q + 1][1], 0) : dEnd[1];
-            const uint64_t pN = lane == 63 ? pw : pn;
-            const bool e0 = u4eq(dA[q][0], dB[q][0]) && u4eq(dA[q][1], dB[q][1]);
-            const bool e1 = lane == 63 ? (u4eq(dA[q][0], w0) && u4eq(dA[q][1], w1))
-                                       : (u4eq(dA[q][0], n0) && u4eq(dA[q][1], n1));
-            if (x < na) {
-                ok0 &= pA[q] == pB[q];
-                ok1 &= (c.b0 + x + 1 < B.n) && pA[q] == pN;
-            }
-            eq0 |= (uint32_t)e0 << q;
-            eq1 |= (uint32_t)e1 << q;
-        }
-        const bool eqPrev = u4eq(dPrev[0], dB[0][0]) && u4eq(dPrev[1], dB[0][1]);  // meaningful in lane 0
-        if (lane == 0) ok1 &= c.a0 > 0 && pPrev == pB[0];
+        const uint64_t pB0 = pB00;
+        const bool eqPrev = u4eq(dPrev[0], dB00[0]) && u4eq(dPrev[1], dB00[1]);  // meaningful in lane 0
+        if (lane == 0) ok1 &= c.a0 > 0 && pPrev == pB0;
         int phase = -1;
         if (__ballot(!ok0) == 0) phase = 0;
         else if (__ballot(!ok1) == 0) phase = 1;
@@ -489,8 +504,9 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
     return pk;
 }
 
-// Pass 1, one wave per 512-output tile (multi-pass form). Pinned to 3 waves per SIMD: the compiler's
-// 170 VGPRs allowed only 2; at 168 (12 B of spills) the 100M mixed pass runs 1.63 instead of 1.82 ms.
+// Pass 1, one wave per 512-output tile (multi-pass form). Pinned to 3 waves per SIMD (the aligned path in
+// two halves leaves 159 VGPRs, no spill): 100M identical replicas 1.49 -> 1.33 ms (6.0 TB/s of the
+// algorithmic 80 B per key), mixed 1.64 -> 1.56 ms; at 4 waves the compiler spills 176 B per lane (1.95 ms).
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, uint32_t *__restrict__ packed,
                                                     uint32_t *__restrict__ tilecnt) {

@@ -7,6 +7,6 @@ cd "$(dirname "$0")/.."
 name=$1; patch=$2
 rm -rf ab/$name && mkdir -p ab/$name && cp -r merklekv_amd/csrc ab/$name/src
 ln -sfn ../include ab/include
-if [ -n "$patch" ]; then (cd ab/$name/src && python3 "$OLDPWD/$patch"); fi
+if [ -n "$patch" ]; then (p=$(readlink -f "$patch"); cd ab/$name/src && python3 "$p"); fi
 make -C ab/$name/src -j8 > ab/$name/build.log 2>&1 || { tail -20 ab/$name/build.log; exit 1; }
 ls -la ab/$name/lib/libmerklekv_hip.so
