@@ -357,8 +357,31 @@ __device__ __forceinline__ uint4 shfl_u4(uint4 v, int src) {
 // One 512-output tile (the body of pass 1): aligned fast path for near-identical replicas, else the
 // general merge. Returns this lane's packed (isplit << 16) | (fromA << 8) | div; *total = the tile's
 // divergent count (wave-uniform). lp: the wave's LDS prefix slice (WTILE + 2 entries).
+// Deferred key checks of the aligned path (round 3): a pair with equal 8-byte prefixes and different
+// digests is taken as the same key with a changed value, and its (A index, B index) goes to this list;
+// k_diff_verify then compares all their keys at once, off pass 1's critical path (each inline check is
+// three dependent random reads per side that hold the wave). A failed check or a full list makes the
+// caller run the diff again without deferral (exact for any key sets).
+struct DeferList {
+    uint64_t *ent;    // (A index << 32) | B index
+    uint32_t *count;  // entries appended (may exceed cap: overflow)
+    uint32_t cap;
+};
+
+__device__ __forceinline__ void defer_pairs(const DeferList &V, bool want, uint64_t e, uint32_t lane) {
+    const uint64_t bal = __ballot(want);
+    if (!bal) return;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(bal);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(V.count, (uint32_t)__popcll(bal));
+    base = __shfl(base, (int)leader);
+    const uint32_t k = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (want && k < V.cap) V.ent[k] = e;
+}
+
+template <bool DEFER = false>
 __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide &B, const TileCtx &c, uint32_t lane,
-                                              uint64_t *lp, uint32_t *total) {
+                                              uint64_t *lp, uint32_t *total, const DeferList &V = DeferList{}) {
     const uint64_t na = c.a1 - c.a0, nb = c.b1 - c.b0;
     uint32_t nd = 0, pk = 0;
     bool general = true;
@@ -456,12 +479,15 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
                 bool dv = false;
                 if (x < na && !((eq >> q) & 1u)) {
                     dv = true;
-                    if (cmp_ab(A, c.a0 + x, pA[q], B, c.b0 + x + phase, pA[q]) != 0) bad = true;
+                    if (!DEFER && cmp_ab(A, c.a0 + x, pA[q], B, c.b0 + x + phase, pA[q]) != 0) bad = true;
                 }
+                if (DEFER) defer_pairs(V, dv, ((c.a0 + x) << 32) | (c.b0 + x + phase), lane);
                 dm[q] = __ballot(dv);
             }
-            if (phase == 1 && lane == 0 && !eqPrev && cmp_ab(A, c.a0 - 1, pPrev, B, c.b0, pPrev) != 0)
-                bad = true;  // B[b0] must be the key of A[a0-1]
+            // B[b0] must be the key of A[a0-1]
+            if (DEFER) defer_pairs(V, phase == 1 && lane == 0 && !eqPrev, ((c.a0 - 1) << 32) | c.b0, lane);
+            else if (phase == 1 && lane == 0 && !eqPrev && cmp_ab(A, c.a0 - 1, pPrev, B, c.b0, pPrev) != 0)
+                bad = true;
             if (__ballot(bad) == 0) {
                 general = false;
                 // output lane L holds pairs 4L .. 4L+3: A outputs at even (phase 0) / odd (phase 1) bits
@@ -507,16 +533,17 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
 // Pass 1, one wave per 512-output tile (multi-pass form). Pinned to 3 waves per SIMD (the aligned path in
 // two halves leaves 159 VGPRs, no spill): 100M identical replicas 1.49 -> 1.33 ms (6.0 TB/s of the
 // algorithmic 80 B per key), mixed 1.64 -> 1.56 ms; at 4 waves the compiler spills 176 B per lane (1.95 ms).
+template <bool DEFER>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, uint32_t *__restrict__ packed,
-                                                    uint32_t *__restrict__ tilecnt) {
+                                                    uint32_t *__restrict__ tilecnt, DeferList V) {
     __shared__ uint64_t lds[4 * (WTILE + 2)];  // per-wave prefix slices for the general merge
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= nt) return;  // wave-uniform
     const uint32_t lane = threadIdx.x & 63;
     const TileCtx c = wave_tile(A, B, split, t);
     uint32_t total = 0;
-    const uint32_t pk = diff_tile(A, B, c, lane, lds + (threadIdx.x >> 6) * (WTILE + 2), &total);
+    const uint32_t pk = diff_tile<DEFER>(A, B, c, lane, lds + (threadIdx.x >> 6) * (WTILE + 2), &total, V);
     if (lane == 0) tilecnt[t] = total;
     packed[t * 64 + lane] = pk;
 }
@@ -773,6 +800,27 @@ __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, cons
     }
 }
 
+// The deferred key checks: fail[0] = 1 if any pair holds different keys or the list overflowed.
+__global__ __launch_bounds__(256) void k_diff_verify(DiffSide A, DiffSide B, DeferList V, uint64_t *__restrict__ fail) {
+    const uint32_t cnt = *V.count;
+    if (cnt > V.cap) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) fail[0] = 1;
+        return;
+    }
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = V.ent[k], i = e >> 32, j = e & 0xFFFFFFFFull;
+        if (cmp_ab(A, i, A.pfx[i], B, j, B.pfx[j]) != 0) fail[0] = 1;
+    }
+}
+
+// Zeroes the deferred-check counter and the fail word of this diff (one launch before pass 1).
+__global__ void k_diff_defer_reset(uint32_t *__restrict__ count, uint64_t *__restrict__ fail) {
+    if (threadIdx.x == 0) {
+        *count = 0;
+        fail[0] = 0;
+    }
+}
+
 __global__ void k_diff_keylens(const uint64_t *__restrict__ refs, uint64_t m, DiffSide A, DiffSide B,
                                uint64_t *__restrict__ lens) {
     uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -994,6 +1042,8 @@ inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_d
 
 }  // namespace
 
+static uint64_t defer_cap(uint64_t M) { return std::min<uint64_t>(M, 1ull << 21); }
+
 size_t diff_scratch_bytes(uint64_t M) {
     uint64_t nt = ceil_div(M ? M : 1, WTILE);
     size_t b = 0;
@@ -1003,6 +1053,7 @@ size_t diff_scratch_bytes(uint64_t M) {
     b += (nt + 2) * sizeof(uint64_t);             // tile offsets
     b += scan_scratch_bytes(nt) + 1024;
     b += (ceil_div(nt, PART_STRIDE) + 2) * sizeof(uint64_t) + 256;  // coarse splits (k_diff_pass1s form)
+    b += defer_cap(M) * sizeof(uint64_t) + 512;                     // deferred key checks + their count
     return b;
 }
 
@@ -1018,10 +1069,10 @@ static int diff_part_variant() {
 }
 
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
-                 hipStream_t st) {
+                 hipStream_t st, bool defer) {
     const uint64_t M = A.n + B.n;
     if (M == 0) {
-        MKV_HIP(hipMemsetAsync(count, 0, sizeof(uint64_t), st));
+        MKV_HIP(hipMemsetAsync(count, 0, 2 * sizeof(uint64_t), st));
         return;
     }
     const uint64_t nt = ceil_div(M, WTILE);
@@ -1036,10 +1087,15 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
     uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     void *sc = carve(scan_scratch_bytes(nt));
+    const uint64_t nc0 = ceil_div(nt, PART_STRIDE);
+    uint64_t *coarse0 = reinterpret_cast<uint64_t *>(carve((nc0 + 2) * sizeof(uint64_t)));
+    DeferList V{reinterpret_cast<uint64_t *>(carve(defer_cap(M) * sizeof(uint64_t))),
+                reinterpret_cast<uint32_t *>(carve(256)), (uint32_t)defer_cap(M)};
+    hipLaunchKernelGGL(k_diff_defer_reset, dim3(1), dim3(64), 0, st, V.count, count + 1);
     const dim3 wg((uint32_t)ceil_div(nt, 4));
     if (diff_part_variant() == 1) {
-        const uint64_t nc = ceil_div(nt, PART_STRIDE);
-        uint64_t *coarse = reinterpret_cast<uint64_t *>(carve((nc + 2) * sizeof(uint64_t)));
+        const uint64_t nc = nc0;
+        uint64_t *coarse = coarse0;
         hipLaunchKernelGGL(k_diff_coarse, dim3((uint32_t)ceil_div(nc + 1, 4)), dim3(256), 0, st, A, B, nc, coarse);
         hipLaunchKernelGGL(k_diff_pass1s, wg, dim3(256), 0, st, A, B, coarse, nt, split, packed, tileoff);
         MKV_LAUNCH_CHECK();
@@ -1050,11 +1106,17 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     }
     hipLaunchKernelGGL(k_diff_partition, grid1d(ceil_div(nt, PART_STRIDE) + 1), dim3(256), 0, st, A, B, nt, split);
     hipLaunchKernelGGL(k_diff_partition_fine, grid1d(nt), dim3(256), 0, st, A, B, nt, split);
-    hipLaunchKernelGGL(k_diff_pass1, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt);
+    if (defer)
+        hipLaunchKernelGGL(k_diff_pass1<true>, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt, V);
+    else
+        hipLaunchKernelGGL(k_diff_pass1<false>, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt, V);
     MKV_LAUNCH_CHECK();
     hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);
     exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
     hipLaunchKernelGGL(k_diff_pass2, wg, dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs);
+    if (defer)
+        hipLaunchKernelGGL(k_diff_verify, dim3((uint32_t)std::min<uint64_t>(ceil_div(defer_cap(M), 256), 1024)),
+                           dim3(256), 0, st, A, B, V, count + 1);
     MKV_LAUNCH_CHECK();
 }
 

@@ -176,9 +176,11 @@ constexpr int DIFF_ITEMS = 8;     // merged outputs per thread
 constexpr int DIFF_THREADS = 256;
 size_t diff_scratch_bytes(uint64_t nmerged);
 // Pass 1 + scan + pass 2: writes refs (bit 63 = side B, low bits = sorted index) of the divergent keys
-// in sorted order; *count (device) receives the number. Returns nothing; host reads count.
+// in sorted order; count[0] (device) receives the number. defer: the aligned tiles' key checks run in a
+// separate kernel after pass 2; count[1] = 1 when one failed (or their list overflowed): the refs are
+// then not valid and the caller runs launch_diff again with defer = false (exact for any key sets).
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
-                 hipStream_t st);
+                 hipStream_t st, bool defer = true);
 // Single-pass merge-join (k_diff_coarse + k_diff_fused): refs in sorted order, out2[0] = count,
 // out2[1] != 0 if a look-back gave up (then re-run launch_diff). status: diff_fused_status_words(M)
 // u64, zeroed when allocated; epoch: 1 + a per-call counter (mod 2^22, never 0) so it is never cleared.

@@ -677,6 +677,16 @@ static bool fused_diff_enabled() {
     return v;
 }
 
+// MKV_DIFF_DEFER (A/B knob): 1 (default) = the merge-join's aligned tiles defer their key checks to
+// k_diff_verify; 0 = checked inline in pass 1 (round 2).
+static bool defer_enabled() {
+    static const bool v = [] {
+        const char *e = getenv("MKV_DIFF_DEFER");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // MKV_TOP_REDUCE (A/B knob): 1 (default) = the tree's top levels in one k_reduce_top launch, 0 = the
 // round-2 per-4-level launches all the way up.
 static bool top_reduce_enabled() {
@@ -2400,9 +2410,17 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
         }
         if (!ran) {
             void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
-            launch_diff(A, B, scr, refs, cnt, t->st);
+            launch_diff(A, B, scr, refs, cnt, t->st, defer_enabled());
             prof_end(t, pd);
-            m = d2h_u64(t, cnt);
+            small_d2h(t, t->h_small, cnt, 16, t->st);  // count + deferred-check verdict
+            wait_stream(t, t->st);
+            m = t->h_small[0];
+            if (t->h_small[1]) {  // equal prefixes with different keys (or too many checks): exact rerun
+                pd = prof_begin(t, "diff");
+                launch_diff(A, B, scr, refs, cnt, t->st, false);
+                prof_end(t, pd);
+                m = d2h_u64(t, cnt);
+            }
         }
     }
     return keylist_from_refs(t, refs, m, A, B);
