@@ -7,6 +7,7 @@ step() { local tag=$1 lim=$2; shift 2; echo "== $tag"; timeout -k 10 $lim "$@" >
   echo "$tag rc=$rc"; tail -${TAILN:-3} gpurun_out/ev/$tag.log; [ $rc -eq 0 ] || exit $rc; }
 if [ "${EVID:-1}" = 1 ]; then
   step pytest_gpu 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
   step bench 600 python bench.py
 else
   PROF_DIR=prof_build PMC="FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU,SQ_INSTS_SALU,GRBM_GUI_ACTIVE,SQ_WAVE_CYCLES" bash scripts/gpu_prof.sh || exit $?
