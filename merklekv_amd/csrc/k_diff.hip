@@ -1033,6 +1033,80 @@ __global__ void k_topdown_leaves(const uint64_t *__restrict__ pos, uint64_t m, D
     if (check && !key_eq_at(A, B, i)) atomicAdd(nbad, 1u);
 }
 
+// ---- one-wait tail of the unsharded top-down pair diff (round 3) ----
+// The same steps as the round-2 tail (leaf-key check, key lengths, scan, key gather, copy into pinned
+// host memory), but sized from the device's divergent count (*mdev) and a host capacity (cap_m keys,
+// cap_b bytes) instead of a host readback between them, so the whole diff is queued before the host
+// waits once. k_td_gate makes the walk's level-4 abort test on the device.
+__global__ void k_td_gate(uint32_t *__restrict__ cnt, uint32_t word, uint32_t level, uint64_t level_count) {
+    if (threadIdx.x != 0) return;
+    if (cnt[word] != 0 || 2 * (uint64_t)cnt[level] > level_count) {
+        cnt[word] |= 0x80000000u;  // screen failed or frontier over half the level: merge-join
+        cnt[level] = 0;            // the jumps below see an empty frontier
+    }
+}
+
+// refs[k] (k < *mdev, side-A positions) checked against B's keys (leaf-key check).
+__global__ void k_td_check_dev(const uint64_t *__restrict__ refs, const uint32_t *__restrict__ mdev, DiffSide A,
+                               DiffSide B, uint32_t *__restrict__ nbad) {
+    const uint64_t m = *mdev;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x)
+        if (!key_eq_at(A, B, refs[k])) atomicAdd(nbad, 1u);
+}
+
+// lens[k] = key length of refs[k] for k < min(*mdev, cap), 0 up to cap (the scan's padding).
+__global__ void k_keylens_dev(const uint64_t *__restrict__ refs, const uint32_t *__restrict__ mdev, uint64_t cap,
+                              DiffSide A, uint64_t *__restrict__ lens) {
+    const uint64_t m = *mdev;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cap; k += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t len = 0;
+        if (k < m) (void)key_at(A, refs[k], &len);
+        lens[k] = len;
+    }
+}
+
+// Key bytes of refs[k] at off[k]; nothing when the list outgrew the capacity (the host falls back).
+__global__ void k_keys_dev(const uint64_t *__restrict__ refs, const uint32_t *__restrict__ mdev, uint64_t cap_m,
+                           uint64_t cap_b, DiffSide A, const uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+    const uint64_t m = *mdev;
+    if (m > cap_m || off[cap_m] > cap_b) return;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t len;
+        const uint8_t *src = key_at(A, refs[k], &len);
+        uint8_t *d = out + off[k];
+        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d) | (uintptr_t)len;
+        if ((al & 15) == 0) {
+            for (uint64_t x = 0; x < len; x += 16)
+                *reinterpret_cast<uint4 *>(d + x) = *reinterpret_cast<const uint4 *>(src + x);
+        } else if ((al & 3) == 0) {
+            for (uint64_t x = 0; x < len; x += 4)
+                *reinterpret_cast<uint32_t *>(d + x) = *reinterpret_cast<const uint32_t *>(src + x);
+        } else {
+            for (uint64_t x = 0; x < len; ++x) d[x] = src[x];
+        }
+    }
+}
+
+// Offsets (m + 1) and key bytes into the mapped pinned block (16-B stores), unless over capacity.
+__global__ __launch_bounds__(256) void k_tail_copy_dev(const uint64_t *__restrict__ off, const uint8_t *__restrict__ kout,
+                                                       const uint32_t *__restrict__ mdev, uint64_t cap_m, uint64_t cap_b,
+                                                       uint8_t *__restrict__ doff, uint8_t *__restrict__ dkeys) {
+    const uint64_t m = *mdev;
+    if (m > cap_m) return;
+    const uint64_t bytes = off[cap_m];
+    if (bytes > cap_b) return;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t no = 8 * (m + 1), nvo = no / 16;
+    const uint8_t *so = reinterpret_cast<const uint8_t *>(off);
+    for (uint64_t v = t; v < nvo; v += stride)
+        reinterpret_cast<uint4 *>(doff)[v] = reinterpret_cast<const uint4 *>(so)[v];
+    if (t < no - nvo * 16) doff[nvo * 16 + t] = so[nvo * 16 + t];
+    const uint64_t nvk = bytes / 16;
+    for (uint64_t v = t; v < nvk; v += stride)
+        reinterpret_cast<uint4 *>(dkeys)[v] = reinterpret_cast<const uint4 *>(kout)[v];
+    if (t < bytes - nvk * 16) dkeys[nvk * 16 + t] = kout[nvk * 16 + t];
+}
+
 __global__ void k_widen_u32(const uint32_t *__restrict__ c, uint64_t *__restrict__ o, uint64_t n) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) o[i] = c[i];
@@ -1262,6 +1336,25 @@ void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const
 
 void launch_prefix_bounds(const DiffSide &A, const uint8_t *prefix, uint32_t plen, uint64_t *lohi, hipStream_t st) {
     hipLaunchKernelGGL(k_prefix_bounds, dim3(1), dim3(64), 0, st, A, prefix, plen, lohi);
+    MKV_LAUNCH_CHECK();
+}
+
+
+void launch_td_gate(uint32_t *cnt, uint32_t word, uint32_t level, uint64_t level_count, hipStream_t st) {
+    hipLaunchKernelGGL(k_td_gate, dim3(1), dim3(64), 0, st, cnt, word, level, level_count);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
+                          uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
+                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st) {
+    const dim3 g((uint32_t)std::min<uint64_t>(ceil_div(cap_m, 256), 2048));
+    if (check) hipLaunchKernelGGL(k_td_check_dev, g, dim3(256), 0, st, refs, mdev, A, B, nbad);
+    hipLaunchKernelGGL(k_keylens_dev, g, dim3(256), 0, st, refs, mdev, cap_m, A, lens);
+    exclusive_scan_u64(lens, off, cap_m, off + cap_m, scan_scr, st);
+    hipLaunchKernelGGL(k_keys_dev, g, dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, off, kout);
+    const uint64_t cb = std::min<uint64_t>(ceil_div(std::max(8 * (cap_m + 1), cap_b) / 16 + 1, 256), 2048);
+    hipLaunchKernelGGL(k_tail_copy_dev, dim3((uint32_t)cb), dim3(256), 0, st, off, kout, mdev, cap_m, cap_b, doff, dkeys);
     MKV_LAUNCH_CHECK();
 }
 

@@ -204,6 +204,15 @@ void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, co
                          hipStream_t st);
 void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,
                       uint8_t *out, hipStream_t st);
+// One-wait tail of the unsharded top-down pair diff: k_td_gate after the landing on level 4 (screen word
+// cnt[word] != 0 or a frontier over half the level: bit 31 set there, frontier emptied); then from the
+// sorted side-A refs (count *mdev on the device): leaf-key check (nbad), key lengths padded to cap_m,
+// scan (total at off[cap_m]), key bytes (cap_b) and their copy into the mapped pinned views doff / dkeys
+// -- skipped when the list outgrows the capacity (the host then copies it from the refs).
+void launch_td_gate(uint32_t *cnt, uint32_t word, uint32_t level, uint64_t level_count, hipStream_t st);
+void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
+                          uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
+                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st);
 // Batched top-down walk (one base vs up to TD_MAX_VARIANTS trees with the same level plan).
 constexpr int TD_MAX_VARIANTS = 64;
 struct TdVariants {

@@ -234,6 +234,7 @@ struct mkv_tree {
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf td_bm, td_bc;            // divergent-position bitmap (all-zero between calls) + block counts
+    uint64_t tail_cap_m = 0, tail_cap_b = 0;  // one-wait top-down tail: key-list capacity (keys, bytes)
     uint64_t td_bm_words = 0;       // words of td_bm known to be zero
     DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
     DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
@@ -404,6 +405,15 @@ __global__ void k_pos_setbits(const uint32_t *__restrict__ f, uint64_t m, uint32
     }
 }
 
+__global__ void k_pos_setbits_dev(const uint32_t *__restrict__ f, const uint32_t *__restrict__ mdev,
+                                  uint32_t *__restrict__ bm) {
+    const uint64_t m = *mdev;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = f[i];
+        atomicOr(bm + (p >> 5), 1u << (p & 31));
+    }
+}
+
 __device__ __forceinline__ uint4 pos_words(const uint32_t *bm, uint64_t w0, uint64_t words) {
     if (w0 + 3 < words) return *reinterpret_cast<const uint4 *>(bm + w0);
     uint4 x = make_uint4(0, 0, 0, 0);
@@ -477,6 +487,18 @@ bool positions_sorted_bitmap(const uint32_t *f, uint64_t m, uint64_t n, uint32_t
     if (nb > POS_MAX_BLOCKS) return false;
     if (!m) return true;
     hipLaunchKernelGGL(k_pos_setbits, dim3((uint32_t)ceil_div(m, 256)), dim3(256), 0, st, f, m, bm);
+    hipLaunchKernelGGL(k_pos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
+    hipLaunchKernelGGL(k_pos_emit, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc, out);
+    MKV_LAUNCH_CHECK();
+    return true;
+}
+
+// The same from a device count (*mdev entries of f), positions into out (room for every position < n).
+bool positions_sorted_bitmap_dev(const uint32_t *f, const uint32_t *mdev, uint64_t n, uint32_t *bm, uint32_t *bc,
+                                 uint64_t *out, hipStream_t st) {
+    const uint64_t words = (n + 31) / 32, nb = ceil_div(words, POS_BLOCK_WORDS);
+    if (nb > POS_MAX_BLOCKS) return false;
+    hipLaunchKernelGGL(k_pos_setbits_dev, dim3(1024), dim3(256), 0, st, f, mdev, bm);
     hipLaunchKernelGGL(k_pos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
     hipLaunchKernelGGL(k_pos_emit, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc, out);
     MKV_LAUNCH_CHECK();
@@ -2311,6 +2333,102 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     return true;
 }
 
+static bool onewait_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("MKV_DIFF_ONEWAIT");  // A/B knob: 0 = the round-2 walk with 4 host waits
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Unsharded top-down pair diff queued whole before ONE host wait (round 3): the jumping walk, the level-4
+// abort test on the device (k_td_gate), the divergent positions (bitmap, device count) written straight
+// into refs, the leaf-key check, key lengths, scan, key gather and the copy into a mapped pinned block
+// sized from earlier calls. Returns the key list, or nullptr with *fallback = 1 (key sets differ or the
+// walk was abandoned: merge-join) or 2 (the list outgrew the pinned capacity: refs hold *m_out sorted
+// positions; the caller copies them with keylist_from_refs). Round 2 waited four times: level-4 count,
+// leaf count, key bytes, result.
+static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, const DiffSide &A,
+                                         const DiffSide &B, uint64_t *refs, int *fallback, uint64_t *m_out) {
+    *fallback = 0;
+    *m_out = 0;
+    const bool roots_valid = !a->combine_pending && !b->combine_pending && a->has_root && b->has_root;
+    if (roots_valid && std::memcmp(a->root, b->root, 32) == 0) return new mkv_keylist();  // identical leaves
+    const size_t L = a->lev_S.size();
+    const uint64_t n = a->n;
+    uint32_t *f0 = ens<uint32_t>(t->td_f0, n + 2);
+    uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 2);
+    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2);
+    if (!t->tail_cap_m) {
+        t->tail_cap_m = std::max<uint64_t>(65536, n / 256);
+        t->tail_cap_b = 48 * t->tail_cap_m;
+    }
+    const uint64_t cap_m = t->tail_cap_m, cap_b = t->tail_cap_b;
+    const uint64_t words = (n + 31) / 32;
+    uint32_t *bm = ens<uint32_t>(t->td_bm, words + 4);
+    uint32_t *bc = ens<uint32_t>(t->td_bc, ceil_div(words, 1024) + 1);
+    uint64_t *lens = ens<uint64_t>(t->s_lens, cap_m + 1);
+    uint64_t *off = ens<uint64_t>(t->d_outoff, cap_m + 1);
+    void *scr = t->d_diffscr.ensure(scan_scratch_bytes(cap_m + 1));
+    uint8_t *kout = ens<uint8_t>(t->d_out, cap_b + 16);
+    const uint64_t kpos = (8 * (cap_m + 1) + 15) & ~uint64_t(15);
+    auto blk = std::make_shared<PinnedBlock>(kpos + cap_b + 16);
+    const size_t pd = prof_begin(t, "diff");  // the queued device work (the wait excluded)
+    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
+    launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
+    const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
+    uint32_t *fin = f0, *fout = f1;
+    launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin, cnt + L,
+                         fout, cnt + (L - 1), 0, t->st);
+    std::swap(fin, fout);
+    const std::vector<size_t> T = jump_targets(L);
+    for (size_t q = 1; q < T.size(); ++q) {
+        const size_t l = T[q - 1], lt = T[q];
+        const int k = (int)(l - lt);
+        launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
+                            cnt + lt, std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
+        std::swap(fin, fout);
+        if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2)
+            launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)lt, a->lev_cnt[lt], t->st);
+    }
+    if (t->td_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
+    t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
+    positions_sorted_bitmap_dev(fin, cnt, n, bm, bc, refs, t->st);  // side-A refs = sorted positions
+    t->td_bm_words = words;
+    launch_diff_tail_dev(refs, cnt, A, B, !same_keyset(a, b), cnt + L + 1, cap_m, cap_b, lens, off, scr, kout, blk->dp,
+                         blk->dp + kpos, t->st);
+    small_d2h(t, t->h_small, cnt, 4, t->st);                // divergent positions
+    small_d2h(t, t->h_small + 1, cnt + L + 1, 4, t->st);    // screen / abort / leaf-key mismatches
+    small_d2h(t, t->h_small + 2, off + cap_m, 8, t->st);    // key bytes (when m <= cap_m)
+    prof_end(t, pd);
+    HTRACE("onewait-queued");
+    sync(t);
+    const uint64_t m = (uint32_t)t->h_small[0];
+    const uint32_t word = (uint32_t)t->h_small[1];
+    const uint64_t bytes = t->h_small[2];
+    if (word != 0) {
+        *fallback = 1;
+        return nullptr;
+    }
+    if (m > cap_m || bytes > cap_b) {
+        if (16 * m <= (256ull << 20)) {  // grow for the next call (bounded)
+            t->tail_cap_m = std::max(cap_m, 2 * m);
+            t->tail_cap_b = std::max(cap_b, m > cap_m ? 2 * m * 64 : 2 * bytes + 4096);
+        }
+        *fallback = 2;
+        *m_out = m;
+        return nullptr;
+    }
+    auto *l = new mkv_keylist();
+    l->n = m;
+    if (m) {
+        l->blk = blk;
+        l->offsets = reinterpret_cast<const uint64_t *>(blk->p);
+        l->bytes = blk->p + kpos;
+    }
+    return l;
+}
+
 static DiffSide side_of(const mkv_tree *t) {
     DiffSide s;
     s.kb = t->kb.as<uint8_t>();
@@ -2371,7 +2489,16 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     uint64_t *refs = ens<uint64_t>(t->d_refs, M + 1);
     uint64_t m = 0;
     bool done = false;
-    if (A.n > 0 && same_plan(a, b) && topdown_enabled()) {
+    const uint64_t nwords = (A.n + 31) / 32;
+    if (A.n > 0 && same_plan(a, b) && topdown_enabled() && onewait_enabled() && !a->sharded && !b->sharded &&
+        a->lev_S.size() > 1 && jumps_enabled() && ceil_div(nwords, 1024) <= 8192) {
+        int fb = 0;
+        mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);
+        HTRACE("topdown-done");
+        if (l) return l;
+        if (fb == 2) return keylist_from_refs(t, refs, m, A, B);
+        m = 0;  // key sets differ (or the walk was abandoned): the merge-join below
+    } else if (A.n > 0 && same_plan(a, b) && topdown_enabled()) {
         // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
         size_t pd = prof_begin(t, "diff");
         const uint32_t *nbad = nullptr;

@@ -20,6 +20,7 @@ VARIANTS = [
     {"MKV_DIFF_FUSED": "1"},                       # single-pass merge-join with decoupled look-back
     {"MKV_DIFF_TOPDOWN": "0"},                     # merge-join for equal key sets too
     {"MKV_DIFF_DEFER": "0"},                       # merge-join key checks inline in pass 1
+    {"MKV_DIFF_ONEWAIT": "0"},                     # top-down pair diff with the round-2 host waits
     {"MKV_DIFF_DEFER": "0", "MKV_DIFF_TOPDOWN": "0"},
     {"MKV_TOP_SHA": "1"},                          # short-chain SHA form at the reduction top
     {"MKV_TOP_REDUCE": "0"},                       # round-2 per-4-level launches up to the root
