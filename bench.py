@@ -718,9 +718,9 @@ def diff_modes(ctx, n, steps, warmup, gather=False):
         B = MerkleTree(ctx.local)
         ctx.build(B, kBf, koB, vBf, voB, nB, validate=True)
         torch.cuda.synchronize()
-        for _ in range(warmup):
-            d = A.diff_keys_view(B)
-            del d
+        d = None
+        for _ in range(max(warmup, 2)):  # like the timed loop, the previous result stays alive while the
+            d = A.diff_keys_view(B)      # next call runs: the pinned-block pool reaches its steady state
         ctx.barrier()
         t0 = time.perf_counter()
         for _ in range(steps):  # timed without the library's HIP-event pairs
