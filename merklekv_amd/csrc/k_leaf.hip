@@ -675,7 +675,7 @@ __device__ __forceinline__ void store_words_a4(uint8_t *p, const uint32_t *w) {
     for (uint32_t i = NW / 4 * 4; i < NW; ++i) reinterpret_cast<uint32_t *>(p)[i] = w[i];
 }
 
-constexpr uint32_t LIST_GRAIN = 32;  // k_leaf_direct: chunks per counter grab once a wave lists
+constexpr uint32_t LIST_GRAIN = 16;  // k_leaf_direct: chunks per counter grab while a wave lists
 
 template <bool SHORT, uint32_t K0, uint32_t V0>
 __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
@@ -706,7 +706,8 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
             ++listed;
             // a listed chunk costs a few stores, so grabs of `grain` chunks would make the shared chunk
             // counter the bottleneck (same-address atomics serialise in L2: 0.5 ms for 10M ragged
-            // records at grain 4); once this wave lists, it grabs LIST_GRAIN chunks at a time
+            // records at grain 4); while this wave lists, it grabs LIST_GRAIN chunks at a time (back to
+            // `grain` at its next fixed-shape chunk, so a grab of fixed chunks stays small at the end)
             src.grain = LIST_GRAIN;
             if (KO.cls && valid) {
                 const uint32_t k = rg_class(kend - kbeg, vend - vbeg);
@@ -728,6 +729,7 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
             }
             continue;
         }
+        src.grain = grain;
         if (!valid) continue;
         uint32_t m[MW];
         load_words_a4<Sh::kw>(kp, m);
