@@ -16,6 +16,7 @@ VARIANTS = [
     {"MKV_LEAF_RAGGED": "2"},                      # register-form ragged leaf kernel (k_leaf_rreg)
     {"MKV_LEAF_RAGGED": "2", "MKV_RREG_WGS": "4"},
     {"MKV_LEAF_RAGGED": "0"},                      # round-2 LDS chunk kernel for listed chunks
+    {"MKV_RAGGED_WGS": "2"},                       # LDS ragged kernel at 2 workgroups per CU
     {"MKV_DIFF_PART": "1"},                        # in-pass tile splits (k_diff_pass1s)
     {"MKV_DIFF_FUSED": "1"},                       # single-pass merge-join with decoupled look-back
     {"MKV_DIFF_TOPDOWN": "0"},                     # merge-join for equal key sets too
