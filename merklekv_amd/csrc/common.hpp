@@ -66,8 +66,4 @@ struct DevBuf {
 
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
-// SHA round variant for A/B measurement in one binary: MKV_SHA_VARIANT=0 plain C association,
-// 1 (default) pinned short dependency chain (sha256.hpp sha_round).
-int sha_variant();
-
 }  // namespace mkv

@@ -548,235 +548,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     packed[t * 64 + lane] = pk;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Single-pass merge-join (round 3, default): coarse splits by a 64-ary search (one wave per 64th tile),
-// then ONE kernel per diff — each wave finds its tile's two splits by a 32-ary search between the
-// coarse neighbours (half-wave each), runs the tile body, the workgroup publishes its divergent count
-// and looks back (decoupled, agent-scope status words tagged with a per-call epoch, so the status array
-// is never cleared) for its global offset, and the waves write their refs in merged = sorted order.
-// Replaces the fine partition, the packed-result round trip, the widen / scan kernels and pass 2.
-// ---------------------------------------------------------------------------------------------
-// split(d) in [L, H] (inclusive) by an NL-ary search on lanes [lane0, lane0 + NL) of the wave (hl = the
-// lane's index in that group). pred(a) = A[a] precedes B[d-1-a] (A first on equal keys) is monotone
-// (true below the split), so the true probes of a round are a prefix of the group.
-template <int NL>
-__device__ __forceinline__ uint64_t split_search(const DiffSide &A, const DiffSide &B, uint64_t d, uint64_t L,
-                                                 uint64_t H, uint32_t hl, uint32_t lane0) {
-    while (H > L) {
-        const uint64_t w = H - L;
-        const bool fine = w <= (uint64_t)NL;
-        const uint64_t p = fine ? L + hl : L + (w * (hl + 1)) / (NL + 1);
-        bool pr = false;
-        if (!fine || hl < w) {
-            const uint64_t jb = d - 1 - p;
-            pr = cmp_merge(A, p, A.pfx[p], B, jb, B.pfx[jb]) <= 0;
-        }
-        const uint64_t bal = __ballot(pr);
-        uint32_t cnt;
-        if constexpr (NL == 64) cnt = (uint32_t)__popcll(bal);
-        else cnt = (uint32_t)__popcll((bal >> lane0) & ((1ull << NL) - 1));
-        if (fine) {
-            L += cnt;
-            H = L;
-        } else {
-            const uint64_t nl = cnt ? L + (w * cnt) / (NL + 1) + 1 : L;
-            const uint64_t nh = cnt < (uint32_t)NL ? L + (w * (cnt + 1)) / (NL + 1) : H;
-            L = nl;
-            H = nh;
-        }
-    }
-    return L;
-}
-
-// coarse[q] = split of tile 64 q (q < nc), coarse[nc] = A.n (the end). One wave per entry.
-__global__ __launch_bounds__(256) void k_diff_coarse(DiffSide A, DiffSide B, uint64_t nc, uint64_t *__restrict__ coarse) {
-    const uint64_t q = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (q > nc) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t M = A.n + B.n;
-    uint64_t d = q * PART_STRIDE * WTILE;
-    if (d > M || q == nc) d = M;
-    const uint64_t L = d > B.n ? d - B.n : 0, H = d < A.n ? d : A.n;
-    const uint64_t r = split_search<64>(A, B, d, L, H, lane, 0);
-    if (lane == 0) coarse[q] = r;
-}
-
-// split of tile tt (<= nt) from the coarse splits: exact at multiples of PART_STRIDE, else a search of
-// the bracket the coarse neighbours leave (as k_diff_partition_fine).
-__device__ __forceinline__ uint64_t fused_split(const DiffSide &A, const DiffSide &B, const uint64_t *coarse,
-                                                uint64_t nt, uint64_t tt, uint32_t hl, uint32_t lane0) {
-    const uint64_t M = A.n + B.n;
-    const uint64_t q = tt / PART_STRIDE, nc = (nt + PART_STRIDE - 1) / PART_STRIDE;
-    if (tt == nt) return coarse[nc];
-    if (tt % PART_STRIDE == 0) return coarse[q];
-    const uint64_t t0 = q * PART_STRIDE, t1 = t0 + PART_STRIDE < nt ? t0 + PART_STRIDE : nt;
-    const uint64_t d = tt * WTILE, d0 = t0 * WTILE, d1 = t1 * WTILE < M ? t1 * WTILE : M;
-    const uint64_t a0 = coarse[q], a1 = coarse[q + 1 <= nc ? q + 1 : nc];
-    uint64_t lo = a1 > d1 - d ? a1 - (d1 - d) : 0, hi = a0 + (d - d0);
-    if (lo < a0) lo = a0;
-    if (hi > a1) hi = a1;
-    if (d > B.n && lo < d - B.n) lo = d - B.n;
-    if (hi > A.n) hi = A.n;
-    if (hi > d) hi = d;
-    if (lo > hi) lo = hi;
-    // One window round around the linear interpolation of the coarse neighbours first: for
-    // near-identical replicas the guess is off by the few inserts / deletes inside the bracket, so the
-    // 32 probes straddle the split and the search ends after one dependent round instead of ~3 (the
-    // 32-ary search alone made pass 1 0.74 ms slower at 100M mixed). A miss narrows the bracket.
-    if (hi - lo > 32) {
-        const uint64_t g = a0 + (uint64_t)((double)(a1 - a0) * (double)(d - d0) / (double)(d1 - d0) + 0.5);
-        uint64_t s = g > lo + 16 ? g - 16 : lo;
-        if (s > hi - 32) s = hi - 32;
-        const uint64_t pp = s + hl, jb = d - 1 - pp;
-        const bool pr = cmp_merge(A, pp, A.pfx[pp], B, jb, B.pfx[jb]) <= 0;
-        const uint32_t cnt = (uint32_t)__popcll((__ballot(pr) >> lane0) & 0xFFFFFFFFull);
-        if (cnt > 0 && cnt < 32) return s + cnt;  // pred(s + cnt - 1) true, pred(s + cnt) false
-        if (cnt == 0) hi = s;                     // pred(s) false: split <= s
-        else lo = s + 32;                         // pred(s + 31) true: split >= s + 32
-    }
-    return split_search<32>(A, B, d, lo, hi, hl, lane0);
-}
-
-constexpr uint64_t DS_AGG = 1ull << 62, DS_INC = 2ull << 62;
-constexpr int DS_EPOCH_SHIFT = 40;
-constexpr uint64_t DS_VAL = (1ull << DS_EPOCH_SHIFT) - 1;
-constexpr uint64_t DS_EPOCH = (1ull << 22) - 1;
-constexpr uint32_t DS_SPIN_LIMIT = 1u << 22;
-
-constexpr int DF_WAVES = 8;  // tiles per workgroup of the single-pass form
-
-// Decoupled look-back by one wave: 64 predecessors' status words per round (lane q reads b-1-q). The
-// nearest inclusive word ends the walk; aggregates before it (and before any not-yet-published word) are
-// summed. Returns the exclusive prefix, or sets *gave_up after DS_SPIN_LIMIT empty rounds.
-__device__ __forceinline__ uint64_t df_lookback(uint64_t *status, uint64_t b, uint64_t tag, uint32_t lane,
-                                                bool *gave_up) {
-    uint64_t excl = 0;
-    int64_t j = (int64_t)b - 1;
-    uint32_t spins = 0;
-    while (j >= 0) {
-        const int64_t idx = j - (int64_t)lane;
-        const uint64_t x = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                    : (DS_INC | tag);  // before workgroup 0: an inclusive zero
-        const bool ready = (x & (DS_EPOCH << DS_EPOCH_SHIFT)) == tag && (x >> 62) != 0;
-        const bool inc = ready && (x >> 62) == 2;
-        const uint64_t nr = __ballot(!ready), im = __ballot(inc);
-        const uint32_t first_nr = nr ? (uint32_t)__builtin_ctzll(nr) : 64u;
-        const uint32_t first_inc = im ? (uint32_t)__builtin_ctzll(im) : 64u;
-        const bool done = first_inc < first_nr;
-        const uint32_t take = done ? first_inc + 1 : first_nr;  // lanes [0, take) are summed
-        uint64_t v = lane < take ? (x & DS_VAL) : 0ull;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += shfl_u64(v, (int)(lane ^ (uint32_t)o));
-        excl += v;
-        if (done) break;
-        j -= take;
-        if (take == 0) {
-            if (++spins > DS_SPIN_LIMIT) {
-                *gave_up = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    return excl;
-}
-
-__global__ __launch_bounds__(64 * DF_WAVES) void k_diff_fused(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
-                                                              uint64_t nt, uint64_t *__restrict__ status, uint32_t epoch,
-                                                              uint64_t *__restrict__ refs, uint64_t *__restrict__ out) {
-    __shared__ uint64_t lds[DF_WAVES * (WTILE + 2)];
-    __shared__ uint32_t wcnt[DF_WAVES];
-    __shared__ uint64_t wg_excl;
-    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t t = (uint64_t)blockIdx.x * DF_WAVES + wave;
-    const uint64_t M = A.n + B.n;
-    uint32_t pk = 0, total = 0;
-    TileCtx c{};
-    if (t < nt) {  // wave-uniform
-        const uint64_t tt = t + (lane >> 5);  // lanes 0-31: split of tile t; lanes 32-63: of tile t + 1
-        const uint64_t sp = fused_split(A, B, coarse, nt, tt, lane & 31, lane & 32);
-        c.d0 = t * WTILE;
-        const uint64_t d1 = c.d0 + WTILE < M ? c.d0 + WTILE : M;
-        c.a0 = shfl_u64(sp, 0);
-        c.a1 = shfl_u64(sp, 32);
-        c.b0 = c.d0 - c.a0;
-        c.b1 = d1 - c.a1;
-        pk = diff_tile(A, B, c, lane, lds + wave * (WTILE + 2), &total);
-    }
-    if (lane == 0) wcnt[wave] = total;
-    __syncthreads();
-    if (wave == 0) {
-        uint64_t agg = 0;
-#pragma unroll
-        for (int w = 0; w < DF_WAVES; ++w) agg += wcnt[w];
-        const uint64_t tag = (uint64_t)(epoch & DS_EPOCH) << DS_EPOCH_SHIFT;
-        const uint64_t b = blockIdx.x;
-        uint64_t excl = 0;
-        if (b == 0) {
-            if (lane == 0) __hip_atomic_store(&status[0], DS_INC | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0) __hip_atomic_store(&status[b], DS_AGG | tag | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            bool gave_up = false;
-            excl = df_lookback(status, b, tag, lane, &gave_up);
-            if (lane == 0) {
-                if (gave_up) __hip_atomic_store(&out[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&status[b], DS_INC | tag | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (lane == 0) {
-            wg_excl = excl;
-            if (b == gridDim.x - 1) out[0] = excl + agg;
-        }
-    }
-    __syncthreads();
-    if (t >= nt) return;
-    // refs of this tile's divergent keys at their global positions (pass 2 of the multi-pass form)
-    uint64_t base = wg_excl;
-    for (uint32_t w = 0; w < wave; ++w) base += wcnt[w];
-    const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
-    const uint32_t cnt = __popc(div);
-    uint64_t off = base + (wave_incl_scan<uint32_t>(cnt) - cnt);
-    if (!div) return;
-    const uint64_t dl = (uint64_t)lane * DI;
-    uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
-    for (int s = 0; s < DI; ++s) {
-        const bool fa = (fromA >> s) & 1u;
-        const uint64_t ref = fa ? i : (j | (1ull << 63));
-        if (fa) ++i; else ++j;
-        if ((div >> s) & 1u) refs[off++] = ref;
-    }
-}
-
-// Pass 1 of the default multi-pass form (round 3): the wave finds its tile's splits itself (32-ary
-// searches between the 64-ary coarse splits, no fine-partition kernel), publishes split[t] (and
-// split[nt]) for pass 2, and writes its divergent count as u64 (the scan's input: no widen kernel).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_diff_pass1s(DiffSide A, DiffSide B, const uint64_t *__restrict__ coarse,
-                                                     uint64_t nt, uint64_t *__restrict__ split,
-                                                     uint32_t *__restrict__ packed, uint64_t *__restrict__ tilecnt) {
-    __shared__ uint64_t lds[4 * (WTILE + 2)];
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= nt) return;  // wave-uniform
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t M = A.n + B.n;
-    const uint64_t tt = t + (lane >> 5);
-    const uint64_t sp = fused_split(A, B, coarse, nt, tt, lane & 31, lane & 32);
-    TileCtx c;
-    c.d0 = t * WTILE;
-    const uint64_t d1 = c.d0 + WTILE < M ? c.d0 + WTILE : M;
-    c.a0 = shfl_u64(sp, 0);
-    c.a1 = shfl_u64(sp, 32);
-    c.b0 = c.d0 - c.a0;
-    c.b1 = d1 - c.a1;
-    uint32_t total = 0;
-    const uint32_t pk = diff_tile(A, B, c, lane, lds + (threadIdx.x >> 6) * (WTILE + 2), &total);
-    if (lane == 0) {
-        tilecnt[t] = total;
-        split[t] = c.a0;
-        if (t + 1 == nt) split[nt] = c.a1;
-    }
-    packed[t * 64 + lane] = pk;
-}
-
 // Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
 __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, const uint32_t *__restrict__ packed,
@@ -1126,20 +897,8 @@ size_t diff_scratch_bytes(uint64_t M) {
     b += (nt + 2) * sizeof(uint32_t);             // tile counts
     b += (nt + 2) * sizeof(uint64_t);             // tile offsets
     b += scan_scratch_bytes(nt) + 1024;
-    b += (ceil_div(nt, PART_STRIDE) + 2) * sizeof(uint64_t) + 256;  // coarse splits (k_diff_pass1s form)
     b += defer_cap(M) * sizeof(uint64_t) + 512;                     // deferred key checks + their count
     return b;
-}
-
-// MKV_DIFF_PART (A/B knob): 0 (default) = binary-search partition + fine partition kernels, then pass 1;
-// 1 = 64-ary coarse splits + in-pass tile splits (k_diff_pass1s): the splits lengthen every wave's
-// dependency chain (100M mixed: pass1s 1.85 ms vs 1.70 ms for pass 1 + 0.08 ms of partition kernels).
-static int diff_part_variant() {
-    static const int v = [] {
-        const char *e = getenv("MKV_DIFF_PART");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
 }
 
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
@@ -1161,23 +920,10 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
     uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     void *sc = carve(scan_scratch_bytes(nt));
-    const uint64_t nc0 = ceil_div(nt, PART_STRIDE);
-    uint64_t *coarse0 = reinterpret_cast<uint64_t *>(carve((nc0 + 2) * sizeof(uint64_t)));
     DeferList V{reinterpret_cast<uint64_t *>(carve(defer_cap(M) * sizeof(uint64_t))),
                 reinterpret_cast<uint32_t *>(carve(256)), (uint32_t)defer_cap(M)};
     hipLaunchKernelGGL(k_diff_defer_reset, dim3(1), dim3(64), 0, st, V.count, count + 1);
     const dim3 wg((uint32_t)ceil_div(nt, 4));
-    if (diff_part_variant() == 1) {
-        const uint64_t nc = nc0;
-        uint64_t *coarse = coarse0;
-        hipLaunchKernelGGL(k_diff_coarse, dim3((uint32_t)ceil_div(nc + 1, 4)), dim3(256), 0, st, A, B, nc, coarse);
-        hipLaunchKernelGGL(k_diff_pass1s, wg, dim3(256), 0, st, A, B, coarse, nt, split, packed, tileoff);
-        MKV_LAUNCH_CHECK();
-        exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
-        hipLaunchKernelGGL(k_diff_pass2, wg, dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs);
-        MKV_LAUNCH_CHECK();
-        return;
-    }
     hipLaunchKernelGGL(k_diff_partition, grid1d(ceil_div(nt, PART_STRIDE) + 1), dim3(256), 0, st, A, B, nt, split);
     hipLaunchKernelGGL(k_diff_partition_fine, grid1d(nt), dim3(256), 0, st, A, B, nt, split);
     if (defer)
@@ -1191,26 +937,6 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     if (defer)
         hipLaunchKernelGGL(k_diff_verify, dim3((uint32_t)std::min<uint64_t>(ceil_div(defer_cap(M), 256), 1024)),
                            dim3(256), 0, st, A, B, V, count + 1);
-    MKV_LAUNCH_CHECK();
-}
-
-size_t diff_fused_status_words(uint64_t M) { return ceil_div(ceil_div(M ? M : 1, WTILE), DF_WAVES) + 4; }
-size_t diff_fused_scratch_bytes(uint64_t M) {
-    const uint64_t nt = ceil_div(M ? M : 1, WTILE);
-    return (ceil_div(nt, PART_STRIDE) + 2) * sizeof(uint64_t);
-}
-
-void launch_diff_fused(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *status, uint32_t epoch,
-                       uint64_t *refs, uint64_t *out2, hipStream_t st) {
-    const uint64_t M = A.n + B.n;
-    MKV_HIP(hipMemsetAsync(out2, 0, 2 * sizeof(uint64_t), st));
-    if (M == 0) return;
-    const uint64_t nt = ceil_div(M, WTILE);
-    const uint64_t nc = ceil_div(nt, PART_STRIDE);
-    uint64_t *coarse = reinterpret_cast<uint64_t *>(scratch);
-    hipLaunchKernelGGL(k_diff_coarse, dim3((uint32_t)ceil_div(nc + 1, 4)), dim3(256), 0, st, A, B, nc, coarse);
-    hipLaunchKernelGGL(k_diff_fused, dim3((uint32_t)ceil_div(nt, DF_WAVES)), dim3(64 * DF_WAVES), 0, st, A, B, coarse, nt,
-                       status, epoch, refs, out2);
     MKV_LAUNCH_CHECK();
 }
 

@@ -1,0 +1,411 @@
+// k_ragged.hip — Kernel A for store-shaped records: R1 + R2 (merkle.rs:7-16, :45-49) for any key / value
+// lengths at any byte offsets, the records a real SYNC snapshot hands over (sync.rs:109-115 hashes
+// arbitrary &str pairs).
+//
+// Work distribution: lane refill. A wave keeps one record per lane and runs one SHA-256 compression per
+// step; a lane whose record ends takes the next record of the wave's queue (ballot + mbcnt over the lanes
+// that need one), so records of 1..n blocks mix freely at full wave width with no bucketing pass. The
+// queue hands out 64-record chunks from a device counter (RG_GRAIN per atomic). Everything a step needs
+// is loaded one step ahead: the next record's offsets (koff/voff pairs) while the current block is
+// compressed, and the next block's source dwords likewise.
+//
+// Message words. Block `blk` of a record covers stream words 16 blk .. 16 blk + 15 of
+//   u32_be(k) || key || u32_be(v) || value || 0x80 || 0.. || u64_be(8L)
+// The key occupies stream words 1 .. b1 (b1 = (4 + k) / 4; word b1 also carries the head of u32_be(v)),
+// the value words b1 + 1 .. b3 (b3 = L / 4; word b1 + 1 starts with the tail of u32_be(v), word b3 ends
+// with 0x80). Per lane the block is assembled in a private 16-dword LDS slot from three 16-word RUNS
+// whose positions depend on the lane's record:
+//   key run   — 16 key words ENDING at position tb1 = b1 - 16 blk (or the whole block when the key goes
+//               on): its last word is word b1 at a static register index, spliced with the head of
+//               u32_be(v) in registers;
+//   value run — 16 value words STARTING at tb1 + 1: its first word (b1 + 1) is spliced with the tail of
+//               u32_be(v), again at a static index;
+//   zero run  — 16 zeros starting after word b3;
+// then one read-modify-write puts 0x80 into word b3, and the first / last block get u32_be(k) / 8L.
+// Runs are written at a dynamic base with static offsets (ds_write2_b32), so every source word costs one
+// v_perm_b32 (byte-swap + byte offset from two aligned dwords) and no per-word compare. Positions outside
+// the slot land in trash dwords: a lane's slot is followed by 20 dwords shared with the next lane's
+// leading trash (the key run reaches 15 below, the value / zero runs 15 above); nobody reads them.
+// Lane stride 36 dwords: the ds_read_b128 lane groups hit distinct banks (36 / 4 = 9 is odd).
+#include "common.hpp"
+#include "kernels.hpp"
+#include "leaf.hpp"
+#include "sha256.hpp"
+
+namespace mkv {
+
+namespace {
+
+constexpr int RG_WAVES = 4;                             // waves per workgroup
+constexpr uint32_t RG_STRIDE = 36;                      // dwords per lane
+constexpr uint32_t RG_FRONT = 16;                       // trash below lane 0's slot
+constexpr uint32_t RG_WAVE_DW = RG_FRONT + 64 * RG_STRIDE;  // lane 63 reaches dword 16 + 63 x 36 + 30
+static_assert(RG_FRONT + 63 * RG_STRIDE + 31 <= RG_WAVE_DW, "lane 63's trash fits the wave region");
+static_assert(RG_STRIDE >= 31 && (RG_STRIDE / 4) % 2 == 1, "trash shared with neighbours; conflict-free reads");
+constexpr uint32_t RG_GRAIN = 4;                        // virtual chunks per hand-out atomic
+constexpr uint32_t RG_INV = 0xFFFFFFFFu;
+#ifndef MKV_RAGGED_WGS
+#define MKV_RAGGED_WGS 3                                // workgroups per CU (persistent grid)
+#endif
+
+typedef uint32_t rg4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// 17 dwords at base + a (base and a 4-B aligned; gfx950 serves 16-B loads at 4-B alignment). Addresses
+// stay pointer arithmetic on the kernel's blob arguments so the loads are global_load, not flat_load
+// (a flat load also counts in lgkmcnt: every LDS wait would wait for it).
+__device__ __forceinline__ void rg_ld17(const uint8_t *base, int64_t a, uint32_t d[17]) {
+    const rg4 *q = reinterpret_cast<const rg4 *>(base + a);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const rg4 x = q[g];
+        d[4 * g] = x.x;
+        d[4 * g + 1] = x.y;
+        d[4 * g + 2] = x.z;
+        d[4 * g + 3] = x.w;
+    }
+    d[16] = reinterpret_cast<const uint32_t *>(base + a)[16];
+}
+// The same, every dword outside [lo, hi) read as zero (records within ~128 B of a blob end): each load
+// goes to a clamped in-range address (lo is a readable dword of a non-empty blob; an empty blob is never
+// read), its value is dropped when the dword is outside.
+__device__ __forceinline__ void rg_ld17_checked(const uint8_t *base, int64_t a, int64_t lo, int64_t hi,
+                                                uint32_t d[17]) {
+    if (lo >= hi) {
+#pragma unroll
+        for (int j = 0; j < 17; ++j) d[j] = 0u;
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 17; ++j) {
+        const int64_t p = a + 4 * j;
+        const bool in = p >= lo && p + 4 <= hi;
+        const uint32_t x = *reinterpret_cast<const uint32_t *>(base + (in ? p : lo));
+        d[j] = in ? x : 0u;
+    }
+}
+
+// Big-endian word of the 4 bytes at byte offset sel (0..3, encoded as a v_perm selector) of (lo, hi).
+__device__ __forceinline__ uint32_t rg_be(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// One lane's record: addresses and the constants of its boundary words.
+struct RgRec {
+    int64_t ka, va;       // floor4(key start), floor4(value start - (k & 3)) as offsets from the dword-aligned
+                          // blob bases (value words align to stream words)
+    uint32_t ksel, vsel;  // v_perm selectors of the two sources' byte offsets
+    uint32_t k, L, b1, b3, nb, blk, r;
+    uint32_t hc;          // head mask of word b1's key bytes (k & 3 of them)
+    uint32_t vhl, vtl;    // u32_be(v) split across words b1 / b1 + 1
+    uint32_t he, term;    // word b3: kept bytes (L & 3), 0x80 terminator
+    bool live, safe;
+};
+
+// kmis / vmis: byte misalignment of the key / value blob pointers (the bases are the blobs rounded down to
+// a dword); klo .. vhi: the blobs' dword ranges as offsets from those bases.
+__device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint64_t k1, uint64_t v0, uint64_t v1, uint32_t r,
+                                        uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi, int64_t vlo,
+                                        int64_t vhi) {
+    const uint32_t k = (uint32_t)(k1 - k0), v = (uint32_t)(v1 - v0);
+    const uint32_t c4 = k & 3;
+    R.k = k;
+    R.L = 8 + k + v;
+    R.nb = (R.L + 72) >> 6;
+    R.b1 = (4 + k) >> 2;
+    R.b3 = R.L >> 2;
+    R.blk = 0;
+    R.r = r;
+    const int64_t kp = (int64_t)(kmis + k0), vq = (int64_t)(vmis + v0) - c4;  // vq < 0: unsafe (first record)
+    R.ka = kp & ~int64_t(3);
+    R.va = vq & ~int64_t(3);
+    R.ksel = 0x00010203u + (uint32_t)(kp & 3) * 0x01010101u;
+    R.vsel = 0x00010203u + (uint32_t)(vq & 3) * 0x01010101u;
+    R.hc = ~(0xFFFFFFFFu >> (8 * c4));
+    R.vhl = v >> (8 * c4);
+    R.vtl = v << ((32 - 8 * c4) & 31);  // only its head c4 bytes are used (hc)
+    const uint32_t e4 = R.L & 3;
+    R.he = ~(0xFFFFFFFFu >> (8 * e4));
+    R.term = 0x80000000u >> (8 * e4);
+    // every source dword a block can load (key run: [ka - 60, ka + 4 b1 + 4], value run:
+    // [va, va + 4 (b3 - b1) + 64)) lies inside the blobs' dword ranges
+    R.safe = R.ka >= klo + 64 && R.ka + 4 * (int64_t)R.b1 + 64 <= khi && R.va >= vlo &&
+             R.va + 4 * (int64_t)(R.b3 - R.b1) + 128 <= vhi;
+    R.live = true;
+}
+
+// The block's positions of the boundary words (block-relative, may lie outside 0..15).
+struct RgPos {
+    int32_t tb1, tb3;
+    int32_t kend;   // key run ends here (min(tb1, 15))
+    int32_t vbeg;   // value run starts here (max(tb1 + 1, 0))
+    bool key_in, val_in;
+};
+__device__ __forceinline__ RgPos rg_pos(const RgRec &R) {
+    RgPos P;
+    P.tb1 = (int32_t)R.b1 - (int32_t)(16 * R.blk);
+    P.tb3 = (int32_t)R.b3 - (int32_t)(16 * R.blk);
+    P.kend = min(P.tb1, 15);
+    P.vbeg = max(P.tb1 + 1, 0);
+    P.key_in = R.live && P.tb1 >= 0;
+    P.val_in = R.live && P.tb1 <= 14 && P.tb3 >= 0;
+    return P;
+}
+
+// Source dwords of the lane's current (record, block): key run and value run.
+__device__ __forceinline__ void rg_fetch(const RgRec &R, bool all_safe, const uint8_t *kbase, const uint8_t *vbase,
+                                         int64_t klo, int64_t khi, int64_t vlo, int64_t vhi, uint32_t dk[17],
+                                         uint32_t dv[17]) {
+    const RgPos P = rg_pos(R);
+    const int64_t ak = R.ka + 4 * (int64_t)((int32_t)(16 * R.blk) + P.kend - 16);
+    const int64_t av = R.va + 4 * (int64_t)((int32_t)(16 * R.blk) + P.vbeg - (int32_t)R.b1 - 1);
+    if (all_safe) {
+        if (P.key_in) rg_ld17(kbase, ak, dk);
+        if (P.val_in) rg_ld17(vbase, av, dv);
+    } else {
+        if (P.key_in) rg_ld17_checked(kbase, ak, klo, khi, dk);
+        if (P.val_in) rg_ld17_checked(vbase, av, vlo, vhi, dv);
+    }
+}
+
+// Virtual chunk id -> chunk: the chunks k_leaf_direct listed, then [B, nch).
+struct RgQueue {
+    uint32_t qc, qn, qpos;  // current / next chunk, records of qc handed out
+    uint32_t pv, pe;        // ids left in the current grab
+    uint32_t pnext;         // first id of the next grab (its atomic was issued when this grab opened)
+    uint32_t nv, nlist, B;
+};
+
+__device__ __forceinline__ uint32_t rg_grab(uint32_t *ctr, uint32_t lane) {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&ctr[CTR_RAGGED], RG_GRAIN);
+    return __builtin_amdgcn_readfirstlane(__shfl(b, 0));
+}
+
+__device__ __forceinline__ uint32_t rg_next_chunk(RgQueue &Q, const uint32_t *ctr, uint32_t *ctrw, uint32_t lane) {
+    if (Q.pv >= Q.pe) {
+        if (Q.pnext >= Q.nv) return RG_INV;  // nothing left anywhere: no further atomics
+        Q.pv = Q.pnext;
+        Q.pe = Q.pnext + RG_GRAIN;
+        Q.pnext = rg_grab(ctrw, lane);
+    }
+    const uint32_t v = Q.pv++;
+    if (v >= Q.nv) return RG_INV;
+    return v < Q.nlist ? __builtin_amdgcn_readfirstlane(ctr[CTR_LIST + v]) : Q.B + (v - Q.nlist);
+}
+
+template <bool SHORT>
+__global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_leaf_ragged(const uint8_t *__restrict__ kb,
+                                                              const uint64_t *__restrict__ koff,
+                                                              const uint8_t *__restrict__ vb,
+                                                              const uint64_t *__restrict__ voff, uint64_t n,
+                                                              uint8_t *__restrict__ out, uint32_t *__restrict__ ctr) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[RG_WAVES * RG_WAVE_DW];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t *lb = lds_all + wave * RG_WAVE_DW + RG_FRONT + lane * RG_STRIDE;  // this lane's block slot
+
+    const uint32_t nch = (uint32_t)((n + 63) / 64);
+    const uint32_t bp1 = ctr[CTR_BP1];
+    RgQueue Q;
+    Q.nlist = ctr[CTR_NLIST];
+    Q.B = bp1 ? bp1 - 1 : nch;
+    Q.nv = Q.nlist + (nch - Q.B);
+    if (Q.nv == 0) return;  // k_leaf_direct hashed every chunk
+
+    // dword-aligned blob bases; the blobs' byte ranges rounded out to whole dwords (as offsets from the
+    // bases): no source load leaves them
+    const uint32_t kmis = (uint32_t)(reinterpret_cast<uintptr_t>(kb) & 3), vmis = (uint32_t)(reinterpret_cast<uintptr_t>(vb) & 3);
+    const uint8_t *kbase = kb - kmis, *vbase = vb - vmis;
+    const int64_t klo = (int64_t)((kmis + koff[0]) & ~3ull), khi = (int64_t)((kmis + koff[n] + 3) & ~3ull);
+    const int64_t vlo = (int64_t)((vmis + voff[0]) & ~3ull), vhi = (int64_t)((vmis + voff[n] + 3) & ~3ull);
+
+    Q.pnext = rg_grab(ctr, lane);
+    Q.pv = Q.pe = 0;
+    Q.qc = rg_next_chunk(Q, ctr, ctr, lane);
+    if (Q.qc == RG_INV) return;
+    Q.qn = rg_next_chunk(Q, ctr, ctr, lane);
+    Q.qpos = 0;
+
+    // next record of this lane (offsets in flight one step ahead)
+    uint64_t nk0 = 0, nk1 = 0, nv0 = 0, nv1 = 0;
+    uint32_t nrec = 0;
+    bool nok = false;
+    auto refill = [&](bool need) {
+        const uint64_t m = __ballot(need);
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t pos = Q.qpos + rank;
+        const uint32_t ch = pos < 64 ? Q.qc : Q.qn;
+        const uint64_t rec = (uint64_t)ch * 64 + (pos & 63);
+        if (need) {
+            nok = ch != RG_INV && rec < n;
+            if (nok) {
+                nrec = (uint32_t)rec;
+                const rg4 *kq = reinterpret_cast<const rg4 *>(koff + rec);  // koff[rec], koff[rec + 1]
+                const rg4 *vq = reinterpret_cast<const rg4 *>(voff + rec);
+                const rg4 a = *kq, b = *vq;
+                nk0 = ((uint64_t)a.y << 32) | a.x;
+                nk1 = ((uint64_t)a.w << 32) | a.z;
+                nv0 = ((uint64_t)b.y << 32) | b.x;
+                nv1 = ((uint64_t)b.w << 32) | b.z;
+            }
+        }
+        if (Q.qc != RG_INV) {
+            Q.qpos += cnt;
+            if (Q.qpos >= 64) {
+                Q.qpos -= 64;
+                Q.qc = Q.qn;
+                Q.qn = Q.qc == RG_INV ? RG_INV : rg_next_chunk(Q, ctr, ctr, lane);
+            }
+        }
+    };
+
+    RgRec R;
+    R.live = false;
+    R.safe = true;
+    R.k = R.L = R.b1 = R.b3 = R.nb = R.blk = R.r = 0;
+    R.ka = R.va = 0;
+    R.ksel = R.vsel = R.hc = R.vhl = R.vtl = R.he = R.term = 0;
+    refill(true);
+    if (nok) rg_take(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi);
+    nok = false;
+    refill(true);
+
+    uint32_t dk[17], dv[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) dk[j] = dv[j] = 0;
+    rg_fetch(R, __all(R.safe || !R.live), kbase, vbase, klo, khi, vlo, vhi, dk, dv);
+    uint32_t st[8];
+    sha_init(st);
+
+    while (__any(R.live || nok)) {
+        // ---- assemble this step's block in the lane's LDS slot ----
+        uint32_t w[16];
+        {
+            const RgPos P = rg_pos(R);
+            uint32_t kr[16], vr[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) kr[m] = rg_be(dk[m + 1], dk[m], R.ksel);
+            if (P.tb1 <= 15) kr[15] = (R.hc & kr[15]) | (~R.hc & R.vhl);  // word b1: key tail | head of u32_be(v)
+#pragma unroll
+            for (int m = 0; m < 16; ++m) vr[m] = rg_be(dv[m + 1], dv[m], R.vsel);
+            if (P.tb1 >= -1) vr[0] = (R.hc & R.vtl) | (~R.hc & vr[0]);  // word b1 + 1: tail of u32_be(v) | value
+            if (P.key_in) {
+                uint32_t *p = lb + (P.kend - 15);
+#pragma unroll
+                for (int m = 0; m < 16; ++m) p[m] = kr[m];
+            }
+            if (P.val_in) {
+                uint32_t *p = lb + P.vbeg;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) p[m] = vr[m];
+            }
+            const int32_t z = min(max(P.tb3 + 1, 0), 16);
+            if (R.live && z <= 15) {
+                uint32_t *p = lb + z;
+#pragma unroll
+                for (int m = 0; m < 16; ++m) p[m] = 0u;
+            }
+            if (R.live && P.tb3 >= 0 && P.tb3 <= 15) {
+                const uint32_t x = lb[P.tb3];
+                lb[P.tb3] = (x & R.he) | R.term;
+            }
+            if (R.live && R.blk == 0) lb[0] = R.k;
+            if (R.live && R.blk + 1 == R.nb) {  // 64-bit bit length 8L
+                lb[14] = R.L >> 29;
+                lb[15] = R.L << 3;
+            }
+            const uint4 *l4 = reinterpret_cast<const uint4 *>(lb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint4 x = l4[j];
+                w[4 * j] = x.x;
+                w[4 * j + 1] = x.y;
+                w[4 * j + 2] = x.z;
+                w[4 * j + 3] = x.w;
+            }
+        }
+        // ---- advance: next block, or the next record ----
+        const bool was_live = R.live;
+        const bool fin = R.live && R.blk + 1 == R.nb;
+        const uint32_t rfin = R.r;
+        if (R.live && !fin) {
+            ++R.blk;
+        } else {
+            if (nok) rg_take(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi);
+            else R.live = false;
+            nok = false;
+        }
+        refill(!nok);
+        rg_fetch(R, __all(R.safe || !R.live), kbase, vbase, klo, khi, vlo, vhi, dk, dv);  // in flight during the rounds
+        // ---- compress ----
+        sha_compress<SHORT>(st, w);
+        if (fin) store_digest(out + 32 * (uint64_t)rfin, st);
+        if (fin || !was_live) sha_init(st);
+    }
+}
+
+// Key-ownership copy of what the fixed-shape kernel left to the ragged stage: the records of chunks
+// [B, nch) (one contiguous byte range) and of the listed chunks, at their source byte offsets in 16-B
+// granules (neighbouring ranges may share a granule: same bytes), plus their offsets. Runs on the aux
+// stream beside the ragged hash (HBM-bound copy next to VALU-bound hashing); does nothing when
+// k_leaf_direct hashed everything.
+__global__ __launch_bounds__(256) void k_keycopy_rest(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                     uint64_t n, const uint32_t *__restrict__ ctr, KeyOut KO) {
+    const uint32_t bp1 = ctr[CTR_BP1];
+    if (!bp1) return;
+    const uint64_t nch = (n + 63) / 64;
+    const uint64_t B = bp1 - 1, nlist = ctr[CTR_NLIST];
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    auto copy_span = [&](uint64_t r0, uint64_t r1, uint64_t t0, uint64_t step) {  // records [r0, r1)
+        if (KO.kdst) {
+            const uint64_t g0 = koff[r0] & ~15ull, g1 = (koff[r1] + 15) & ~15ull;
+            if (g1 <= KO.kcap)
+                for (uint64_t g = g0 + 16 * t0; g < g1; g += 16 * step)
+                    *reinterpret_cast<uint4 *>(KO.kdst + g) = *reinterpret_cast<const uint4 *>(kb + g);
+        }
+        if (KO.odst)
+            for (uint64_t r = r0 + t0; r <= r1; r += step) KO.odst[r] = koff[r];  // r1's offset too (= next start)
+    };
+    if (blockIdx.y == 0) {
+        if (B < nch) copy_span(B * 64, n, t, stride);
+    } else {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint64_t wv = t / 64, nw = stride / 64;
+        for (uint64_t i = wv; i < nlist; i += nw) {
+            const uint64_t c = ctr[CTR_LIST + i];
+            copy_span(c * 64, std::min<uint64_t>(c * 64 + 64, n), lane, 64);
+        }
+    }
+}
+
+int device_cus() {
+    static int c = [] {
+        int dev = 0, x = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&x, hipDeviceAttributeMultiprocessorCount, dev);
+        return x > 0 ? x : 256;
+    }();
+    return c;
+}
+
+}  // namespace
+
+void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                        uint8_t *out, uint32_t *ctr, hipStream_t st) {
+    if (!n) return;
+    const uint64_t grid = std::min<uint64_t>((uint64_t)device_cus() * MKV_RAGGED_WGS, ceil_div(ceil_div(n, 64), RG_WAVES));
+    hipLaunchKernelGGL(k_leaf_ragged<false>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
+                       kb, koff, vb, voff, n, out, ctr);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_keycopy_rest(const uint8_t *kb, const uint64_t *koff, uint64_t n, const uint32_t *ctr, uint8_t *kdst,
+                         uint64_t kcap, uint64_t *odst, hipStream_t st) {
+    if (!n || (!kdst && !odst)) return;
+    const KeyOut KO{kdst, odst, kcap};
+    hipLaunchKernelGGL(k_keycopy_rest, dim3(1024, 2), dim3(256), 0, st, kb, koff, n, ctr, KO);
+    MKV_LAUNCH_CHECK();
+}
+
+}  // namespace mkv

@@ -177,6 +177,11 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
         __syncthreads();
         if (!last) return;
         __threadfence();
+    } else {
+        // one tile: phase 2 still reads level nf back from HBM, so every thread's stores of it must have
+        // landed (lds_barrier waits for LDS operations only)
+        __threadfence();
+        __syncthreads();
     }
     // level nf (owned nodes [a, a + c), c <= RD_TILE) into LDS as BE words, read coherently
     {
@@ -408,38 +413,21 @@ __global__ __launch_bounds__(64) void k_seam_combine(const SeamEntry *__restrict
 
 void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
-    // Few tiles = latency-bound (each fused level waits one full node hash): use the short dependency
-    // chain there; many tiles = throughput-bound: fewer instructions win (profiles/r01_valu_microbench.md).
-    const bool latency_bound = p.ntiles < 256;
-    const int v = sha_variant();
-    static const int thr = [] {
-        const char *e = getenv("MKV_RD_THREADS");  // A/B knob: 512 (one parent per thread) or 256
-        return e && atoi(e) == 256 ? 256 : 512;
-    }();
-    if (v == 0 || (v == 1 && !latency_bound)) {
-        if (thr == 256)
-            hipLaunchKernelGGL((k_reduce_fused<false, 256>), dim3((uint32_t)p.ntiles), dim3(256), 0, st, p);
-        else
-            hipLaunchKernelGGL((k_reduce_fused<false, 512>), dim3((uint32_t)p.ntiles), dim3(512), 0, st, p);
-    } else {
-        hipLaunchKernelGGL((k_reduce_fused<true, 512>), dim3((uint32_t)p.ntiles), dim3(512), 0, st, p);
-    }
+    // Few tiles = latency-bound (each fused level waits one full node hash): the short dependency chain
+    // there; many tiles = throughput-bound: fewer instructions win (profiles/r01_valu_microbench.md).
+    if (p.ntiles < 256)
+        hipLaunchKernelGGL((k_reduce_fused<true, RD_TILE>), dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+    else
+        hipLaunchKernelGGL((k_reduce_fused<false, RD_TILE>), dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 
 void launch_reduce_top(const TopPlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
-    // MKV_TOP_SHA (A/B knob): 0 (default) plain rounds, 1 short-chain rounds. One wave per SIMD is
-    // bound by its own issue rate (~4 cycles per VALU instruction), not by the round's dependency
-    // chain, so the form with fewer instructions wins even here (10M build: 110 vs 116 us).
-    static const int form = [] {
-        const char *e = getenv("MKV_TOP_SHA");
-        return e ? atoi(e) : 0;
-    }();
-    if (form)
-        hipLaunchKernelGGL(k_reduce_top<true>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
-    else
-        hipLaunchKernelGGL(k_reduce_top<false>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+    // Plain rounds: one wave per SIMD is bound by its own issue rate (~4 cycles per VALU instruction), not
+    // by the round's dependency chain, so the form with fewer instructions wins even here (10M build: 110
+    // vs 116 us for the short-chain form).
+    hipLaunchKernelGGL(k_reduce_top<false>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 

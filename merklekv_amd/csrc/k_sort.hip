@@ -32,15 +32,10 @@ constexpr int SC_THREADS = 256;
 constexpr int SC_IPT = 8;
 constexpr int SC_TILE = SC_THREADS * SC_IPT;
 
-// Issue priority of the ordering kernels against co-resident leaf-hash waves (MKV_SORT_PRIO, default 3):
-// a uniform scalar load + branch at kernel entry, since s_setprio takes an immediate.
-__device__ int g_sort_prio = 3;
-__device__ __forceinline__ void sort_prio() {
-    const int p = __builtin_amdgcn_readfirstlane(g_sort_prio);
-    if (p >= 3) __builtin_amdgcn_s_setprio(3);
-    else if (p == 2) __builtin_amdgcn_s_setprio(2);
-    else if (p == 1) __builtin_amdgcn_s_setprio(1);
-}
+// Issue priority of the ordering kernels against co-resident leaf-hash waves: the highest, 3 (at 0, the
+// leaf hash's, the co-running sort starves: 1.56 vs 0.92 ms beside the leaf hash, build 2.26-2.49 vs
+// 2.17-2.22 ms/step).
+__device__ __forceinline__ void sort_prio() { __builtin_amdgcn_s_setprio(3); }
 
 __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                  uint64_t n, uint64_t *__restrict__ pfx, uint32_t *__restrict__ idx) {
@@ -728,11 +723,6 @@ __global__ __launch_bounds__(256) void k_rank_selftest(uint32_t trials, uint32_t
 static bool lds_rank_ok(hipStream_t st) {
     static int ok = -1;
     if (ok >= 0) return ok == 1;
-    const char *e = getenv("MKV_SORT_RANK");  // "ballot" forces the ballot ranking
-    if (e && std::string(e) == "ballot") {
-        ok = 0;
-        return false;
-    }
     uint32_t *bad = nullptr;
     uint32_t hbad = 1;
     if (hipMalloc(&bad, 4) == hipSuccess) {
@@ -745,39 +735,18 @@ static bool lds_rank_ok(hipStream_t st) {
     return ok == 1;
 }
 
-// Items per thread of the tree builds' prefix-sort passes (MKV_SORT_IPT 16 / 24 / 32; default 24: 6,144
-// pairs per tile through the half-LDS reorder, ~53 KiB — the same LDS footprint as the 4,096-pair tile
-// with separate key and value tiles, 1.5x the pairs per look-back and 1.5x longer digit runs per write:
-// the build's ordering stage 1.27 -> 1.11 ms beside the leaf hash; 32 no longer fits beside it).
-// Half-LDS tiles of 12 / 16 / 20 items ("12h" / "16h" / "20h"; 30-46 KiB) fit beside three leaf-hash
-// workgroups per CU (A/B knob with MKV_LEAF_WGS=3). Returned as -ipt for the half-LDS form of 12..20.
-static int sort_ipt() {
-    static const int v = [] {
-        const char *e = getenv("MKV_SORT_IPT");
-        if (!e) return 24;
-        const int x = atoi(e);
-        if (std::strchr(e, 'h') && (x == 12 || x == 16 || x == 20)) return -x;
-        return (x == 24 || x == 32) ? x : 16;
-    }();
-    return v;
-}
-
-static void init_sort_prio() {
-    static bool done = [] {
-        const char *e = getenv("MKV_SORT_PRIO");
-        if (e) {
-            const int v = atoi(e);
-            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_prio), &v, sizeof(int));
-        }
-        return true;
-    }();
-    (void)done;
-}
+// Items per thread of the tree builds' prefix-sort passes: 24 (6,144 pairs per tile through the half-LDS
+// reorder, ~53 KiB — the LDS footprint of the 4,096-pair tile with separate key and value tiles, 1.5x the
+// pairs per look-back and 1.5x longer digit runs per write: the build's ordering stage 1.27 -> 1.11 ms
+// beside the leaf hash; 32 no longer fits beside it). 12 / 16 / 20 (30-46 KiB) fit beside three leaf-hash
+// workgroups per CU.
+#ifndef MKV_SORT_IPT
+#define MKV_SORT_IPT 24
+#endif
 
 void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, uint32_t *idx,
                      hipStream_t st) {
     if (!n) return;
-    init_sort_prio();
     hipLaunchKernelGGL(k_prefix64, grid1d(n), dim3(256), 0, st, kb, koff, n, pfx, idx);
     MKV_LAUNCH_CHECK();
 }
@@ -785,7 +754,7 @@ void launch_prefix64(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64
 size_t scan_scratch_bytes(uint64_t n) { return (ceil_div(n ? n : 1, SC_TILE) + 16) * sizeof(uint64_t); }
 
 size_t radix_scratch_bytes(uint64_t n) {
-    // look-back words for the smallest tile any pass may use (12 items per thread, sort_ipt)
+    // look-back words for the smallest tile any pass may use (12 items per thread)
     const uint64_t nb = ceil_div(n ? n : 1, (uint64_t)RS_THREADS * 12);
     // digit counts (8 x 256) + control words (8 passes x 4) + look-back words (8 passes x tiles x 256)
     return (8 * 256 + 64 + 8ull * nb * 256) * sizeof(uint32_t) + 1024 + scan_scratch_bytes(n);
@@ -855,7 +824,6 @@ void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const
 
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
                         hipStream_t st, uint64_t off, bool lcp) {
-    init_sort_prio();
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) return;
@@ -890,9 +858,7 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
         return false;
     }
     if (n >= (1ull << 30)) throw Error(ST_EINVAL, "radix sort: more than 2^30 - 1 keys per device");
-    const int ipt_sel = sort_ipt();
-    const int ipt = ipt_sel < 0 ? -ipt_sel : ipt_sel;
-    const uint32_t nb = (uint32_t)ceil_div(n, (uint64_t)RS_THREADS * ipt);
+    const uint32_t nb = (uint32_t)ceil_div(n, (uint64_t)RS_THREADS * MKV_SORT_IPT);
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *ctl = counts + 8 * 256;
     uint32_t *lookback = ctl + 64;
@@ -907,24 +873,9 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
         if (!((digit_mask >> p) & 1u)) continue;
         const bool lr = lds_rank_ok(st);
         uint32_t *lb = lookback + (size_t)q * nb * 256;
-        if (lr && ipt_sel < 0 && ipt == 12)
-            hipLaunchKernelGGL((k_os_pass<true, true, 12>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
-        else if (lr && ipt_sel < 0 && ipt == 16)
-            hipLaunchKernelGGL((k_os_pass<true, true, 16>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
-        else if (lr && ipt_sel < 0 && ipt == 20)
-            hipLaunchKernelGGL((k_os_pass<true, true, 20>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
-        else if (lr && ipt == 32)
-            hipLaunchKernelGGL((k_os_pass<true, true, 32>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
-        else if (lr && ipt == 24)
-            hipLaunchKernelGGL((k_os_pass<true, true, 24>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
-        else if (lr)
-            hipLaunchKernelGGL((k_os_pass<true, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
+        if (lr)
+            hipLaunchKernelGGL((k_os_pass<true, true, MKV_SORT_IPT>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
+                               8 * p, counts + 256 * p, lb, ctl + 4 * p);
         else
             hipLaunchKernelGGL((k_os_pass<false, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
                                counts + 256 * p, lb, ctl + 4 * p);

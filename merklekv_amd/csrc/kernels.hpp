@@ -17,17 +17,28 @@ struct LeafBatches {
     uint64_t base[LEAF_MULTI_MAX];  // batch b's digests at out + 32 x base[b]
 };
 void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uint8_t *out, hipStream_t st);
-// Words of the leaf hash's device counter block (ctr): chunk hand-out counter + listed-chunk count + list.
+// Words of the leaf stage's device counter block (ctr, leaf.hpp): chunk hand-out counters and the list of
+// chunks the fixed-shape kernel leaves to the ragged one.
 size_t leaf_ctr_words(uint64_t n);
-// ctr: optional device counter block (leaf_ctr_words(n) words) for the persistent kernels' chunk
-// hand-out and the list of chunks k_leaf_direct leaves to k_leaf_list; zeroed by the launch. Without it
-// the launch takes the static round-robin k_leaf_persist.
-// kcopy/kcap/ocopy: optional fused key-ownership copy (keys at the same byte offsets into kcopy, at most
-// kcap bytes; offsets[0..n] into ocopy). Returns true when the key copy was fused (persistent kernels and
-// kb 16-B aligned; offsets are copied whenever ocopy is given to a persistent kernel).
-bool launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                      uint8_t *out_digests, hipStream_t st, uint32_t *ctr = nullptr, uint8_t *kcopy = nullptr,
-                      uint64_t kcap = 0, uint64_t *ocopy = nullptr);
+// The fixed-shape kernel (k_leaf_direct): zeroes the counter head, hashes every chunk of the configs'
+// 32/100-B shape until it meets another shape (then it stops and hands the rest over). kcopy/kcap/ocopy:
+// optional fused key-ownership copy (keys at the same byte offsets into kcopy, at most kcap bytes;
+// offsets into ocopy). Returns true when the key copy was fused (kb 16-B aligned); the records left to
+// the ragged stage are then copied by launch_keycopy_rest.
+bool launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st, uint8_t *kcopy, uint64_t kcap,
+                       uint64_t *ocopy);
+// Every chunk launch_leaf_fixed left (k_ragged.hip: any key / value lengths and alignments). Same stream,
+// after launch_leaf_fixed.
+void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                        uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
+// Key-ownership copy of the records the fixed-shape kernel left (no-op when it hashed everything); any
+// stream ordered after launch_leaf_fixed.
+void launch_keycopy_rest(const uint8_t *kb, const uint64_t *koff, uint64_t n, const uint32_t *ctr, uint8_t *kdst,
+                         uint64_t kcap, uint64_t *odst, hipStream_t st);
+// Both kernels, no key copy (staged inputs, update batches).
+void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                      uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
 
 // ---- Kernel C: ordering (k_sort.hip) ----
 // pfx[i] = big-endian first 8 key bytes, zero padded (key i of kb/koff); idx[i] = i
@@ -181,13 +192,6 @@ size_t diff_scratch_bytes(uint64_t nmerged);
 // then not valid and the caller runs launch_diff again with defer = false (exact for any key sets).
 void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *refs, uint64_t *count,
                  hipStream_t st, bool defer = true);
-// Single-pass merge-join (k_diff_coarse + k_diff_fused): refs in sorted order, out2[0] = count,
-// out2[1] != 0 if a look-back gave up (then re-run launch_diff). status: diff_fused_status_words(M)
-// u64, zeroed when allocated; epoch: 1 + a per-call counter (mod 2^22, never 0) so it is never cleared.
-size_t diff_fused_status_words(uint64_t nmerged);
-size_t diff_fused_scratch_bytes(uint64_t nmerged);
-void launch_diff_fused(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *status, uint32_t epoch,
-                       uint64_t *refs, uint64_t *out2, hipStream_t st);
 // Top-down diff for trees with equal leaf counts (identical level shapes).
 // fin/fout: local indices; a_par/a_child: global index of local 0 at the parent/child level; r0/r1:
 // extra child-level candidates (owned nodes with an unowned parent; UINT64_MAX = none).

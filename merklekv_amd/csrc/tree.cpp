@@ -24,11 +24,6 @@ using namespace mkv;
 
 static thread_local std::string g_err;
 
-static int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
 // Host-side phase trace of the last API call on this thread (mkv_debug_trace): labelled timestamps
 // (µs since the call started) at the call's blocking points, so a slow call names where its host time
 // went (a device wait, a readback, a copy) next to the device time the HIP events report.
@@ -52,14 +47,6 @@ struct HostTrace {
 thread_local HostTrace g_trace;
 }  // namespace
 #define HTRACE(l) g_trace.mark(l)
-
-int mkv::sha_variant() {
-    static const int v = [] {
-        const char *e = getenv("MKV_SHA_VARIANT");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
 
 namespace {
 
@@ -194,7 +181,7 @@ struct mkv_tree {
     int dev = 0;
     hipStream_t st = nullptr;   // main stream: leaf hashing, digest gather, reduction, diff
     hipStream_t st2 = nullptr;  // aux stream: key ownership copy, prefix sort, ties, dedup (overlaps st)
-    hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr;
+    hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr, ev_leaf = nullptr;
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
@@ -226,8 +213,6 @@ struct mkv_tree {
     // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
     std::vector<std::pair<uint32_t, uint32_t>> walk_jumps;
     uint32_t walk_L = 0, walk_k = 0;
-    DevBuf d_status;   // k_diff_fused's look-back status words (zeroed when allocated; epoch-tagged)
-    uint32_t diff_epoch = 0;
     DevBuf r_chunk, r_chunk2, r_kidx, r_kidx2, r_permact, r_head, r_gexcl, r_key2, r_key22;
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf leaf_ctr;  // dynamic chunk counter of the leaf hash
@@ -235,6 +220,7 @@ struct mkv_tree {
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf td_bm, td_bc;            // divergent-position bitmap (all-zero between calls) + block counts
     uint64_t tail_cap_m = 0, tail_cap_b = 0;  // one-wait top-down tail: key-list capacity (keys, bytes)
+    std::shared_ptr<PinnedBlock> tail_blk;      // its staging block (reused while no result holds it)
     uint64_t td_bm_words = 0;       // words of td_bm known to be zero
     DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
     DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
@@ -688,37 +674,6 @@ uint64_t total_nodes(const mkv_tree *t) {
     return s;
 }
 
-// MKV_DIFF_FUSED (A/B knob): 1 = single-pass merge-join (k_diff_fused: decoupled look-back), 0 (default) =
-// multi-pass. Measured (100M mixed): 4.06 ms for the single pass vs 1.84 ms for pass 1 of the multi-pass
-// form — 170 VGPRs leave one 8-wave workgroup per CU, and its look-back wave idles the other seven.
-static bool fused_diff_enabled() {
-    static const bool v = [] {
-        const char *e = getenv("MKV_DIFF_FUSED");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return v;
-}
-
-// MKV_DIFF_DEFER (A/B knob): 1 (default) = the merge-join's aligned tiles defer their key checks to
-// k_diff_verify; 0 = checked inline in pass 1 (round 2).
-static bool defer_enabled() {
-    static const bool v = [] {
-        const char *e = getenv("MKV_DIFF_DEFER");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
-// MKV_TOP_REDUCE (A/B knob): 1 (default) = the tree's top levels in one k_reduce_top launch, 0 = the
-// round-2 per-4-level launches all the way up.
-static bool top_reduce_enabled() {
-    static const bool v = [] {
-        const char *e = getenv("MKV_TOP_REDUCE");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return v;
-}
-
 // gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch. Leaves whose
 // parent is not owned (at most the first and the last of a shard) are gathered directly; a plan without
 // an owned level-1 node (single leaf, or a one-leaf shard) gathers everything directly.
@@ -747,7 +702,7 @@ void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, co
         // with owned nodes (a shard stops at its last owned level; the seam combine does the rest).
         size_t nown = 0;
         while (nown < remaining && t->lev_cnt[l + 1 + nown] > 0) ++nown;
-        if (ntiles <= RD_TOP_TILES && nown <= (size_t)TOP_MAX_LEVELS && top_reduce_enabled()) {
+        if (ntiles <= RD_TOP_TILES && nown <= (size_t)TOP_MAX_LEVELS) {
             const bool fresh = t->rd_arrive.p == nullptr;
             uint32_t *arrive = ens<uint32_t>(t->rd_arrive, 16);
             if (fresh) MKV_HIP(hipMemsetAsync(arrive, 0, 64, t->st));
@@ -874,11 +829,9 @@ void refine_ties(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t 
 // next to nothing, so 10M base64 keys take 5 passes and ~46K ties instead of 6 passes and ~730 ties:
 // ordering stage 1.10 -> 1.00 ms beside the leaf hash.) Returns the digit mask; *lo_bit = lowest sorted bit.
 uint32_t choose_prefix_digits(const uint32_t *counts, uint64_t n, int *lo_bit) {
-    // margin bits beyond log2(n): fewer radix passes vs more prefix ties for the refinement
-    static const double margin = [] {
-        const char *e = getenv("MKV_SORT_MARGIN");
-        return e ? atof(e) : 6.0;
-    }();
+    // margin bits beyond log2(n): fewer radix passes vs more prefix ties for the refinement (6: 5 passes
+    // + ~46K ties at 10M base64 keys beat 6 passes + ~730 ties; 3 / 0 and 11 / 14 measured slower)
+    constexpr double margin = 6.0;
     const double need = std::log2((double)(n > 1 ? n : 2)) + margin;
     double cum = 0;
     int p0 = 0;
@@ -1040,6 +993,13 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
     // a readback there would hold the host until the gather finishes and delay the reduce launches)
     const uint64_t kbytes = staged_inputs ? staged_kbytes : (n_in ? d2h_u64(t, koff + n_in, st) : 0);
+    const bool keys_done = !staged_inputs && fused_kcap && kbytes + 16 <= fused_kcap;
+    if (keys_done || (!staged_inputs && fused_koff)) {
+        // the records the fixed-shape kernel left to the ragged one: copied here, beside the ragged hash
+        MKV_HIP(hipStreamWaitEvent(st, t->ev_leaf, 0));
+        launch_keycopy_rest(kb, koff, n_in, t->leaf_ctr.as<uint32_t>(), keys_done ? t->kb.as<uint8_t>() : nullptr,
+                            fused_kcap, fused_koff ? t->koff.as<uint64_t>() : nullptr, st);
+    }
     // The reduction on st needs only the sorted order: join here, before the key copy.
     MKV_HIP(hipEventRecord(t->ev_join, st));
     MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
@@ -1053,7 +1013,6 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
         swap_buf(t->kb, t->s_kb);
         swap_buf(t->koff, t->s_koff);
     } else {
-        const bool keys_done = fused_kcap && kbytes + 16 <= fused_kcap;
         uint8_t *dkb = ens<uint8_t>(t->kb, kbytes + 16);  // (a regrowth syncs the device first)
         uint64_t *dko = ens<uint64_t>(t->koff, n_in + 1);
         if (!keys_done || !fused_koff) {
@@ -1244,24 +1203,12 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess) {
             int lo = 0, hi = 0;  // aux (ordering) stream at the highest priority: its WGs dispatch first
             (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            const int sort_cus = env_int("MKV_SORT_CUS", 0);  // A/B knob: confine the ordering kernels to N CUs
-            if (sort_cus > 0) {
-                int ncu = 0;
-                (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, hip_device);
-                std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-                const int k = std::min(sort_cus, ncu);
-                for (int i = 0; i < k; ++i) {  // spread over the chip (every ncu/k-th CU)
-                    const int cu = (int)((int64_t)i * ncu / k);
-                    mask[cu / 32] |= 1u << (cu % 32);
-                }
-                e2 = hipExtStreamCreateWithCUMask(&t->st2, (uint32_t)mask.size(), mask.data());
-            } else {
-                e2 = hipStreamCreateWithPriority(&t->st2, hipStreamNonBlocking, hi);
-            }
+            e2 = hipStreamCreateWithPriority(&t->st2, hipStreamNonBlocking, hi);
         }
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_wait, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_leaf, hipEventDisableTiming);
         if (e2 != hipSuccess) {
             mkv_tree_destroy(t);
             throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
@@ -1280,6 +1227,7 @@ void mkv_tree_destroy(mkv_tree *t) {
     if (t->ev_in) (void)hipEventDestroy(t->ev_in);
     if (t->ev_join) (void)hipEventDestroy(t->ev_join);
     if (t->ev_wait) (void)hipEventDestroy(t->ev_wait);
+    if (t->ev_leaf) (void)hipEventDestroy(t->ev_leaf);
     if (t->st2) (void)hipStreamDestroy(t->st2);
     for (auto &p : t->evpool) {
         (void)hipEventDestroy(p.a);
@@ -1379,9 +1327,11 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
     });
 }
 
-// The leaf hash of a build. Borrowed device inputs (!staged): it also copies the keys (and offsets) into
-// the tree's own buffers when the capacity of an earlier build suffices (*kcap / *ko_fused say what was
-// fused; otherwise sort_dedup_gather copies them).
+// The leaf stage of a build: the fixed-shape kernel, then the ragged kernel for whatever it left. Borrowed
+// device inputs (!staged): the fixed-shape kernel also copies the keys (and offsets) into the tree's own
+// buffers when the capacity of an earlier build suffices (*kcap / *ko_fused say what was fused; the
+// records it left are copied by launch_keycopy_rest in sort_dedup_gather; otherwise sort_dedup_gather
+// copies everything).
 static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
                                   const uint64_t *voff, uint64_t n, uint8_t *dig, bool staged, uint64_t *kcap,
                                   bool *ko_fused) {
@@ -1391,14 +1341,14 @@ static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t
     if (!staged) {
         *kcap = t->kb.p ? t->kb.cap : 0;
         *ko_fused = t->koff.p && t->koff.cap >= (n + 1) * 8;
-        if (!launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ctr, t->kb.as<uint8_t>(), *kcap,
-                              *ko_fused ? t->koff.as<uint64_t>() : nullptr)) {
+        if (!launch_leaf_fixed(kb, koff, vb, voff, n, dig, ctr, t->st, t->kb.as<uint8_t>(), *kcap,
+                               *ko_fused ? t->koff.as<uint64_t>() : nullptr))
             *kcap = 0;
-            *ko_fused = false;  // offsets are copied only together with the persistent kernels
-        }
+        MKV_HIP(hipEventRecord(t->ev_leaf, t->st));  // the hand-off state k_keycopy_rest reads
     } else {
-        launch_leaf_hash(kb, koff, vb, voff, n, dig, t->st, ctr);
+        launch_leaf_fixed(kb, koff, vb, voff, n, dig, ctr, t->st, nullptr, 0, nullptr);
     }
+    launch_leaf_ragged(kb, koff, vb, voff, n, dig, ctr, t->st);
 }
 
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
@@ -1476,14 +1426,6 @@ mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
 
 static DiffSide side_of(const mkv_tree *t);
 
-static bool merge_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("MKV_UPDATE_MERGE");  // A/B knob: 0 = re-sort everything
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // Key-set-changing batch on a non-empty unsharded tree: only the batch is sorted (last
 // write per key wins, tombstones kept as flags), then merged with the tree's sorted leaves (Kernel E
 // merge: replaced / removed leaves drop out, existing digests are reused, never re-hashed), and the
@@ -1514,7 +1456,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
         bdig = ens<uint8_t>(t->u_dig, nb * 32);
         size_t pl = prof_begin(t, "leaf_hash");
         launch_leaf_hash(t->u_kb.as<uint8_t>(), t->u_koff.as<uint64_t>(), t->u_vb.as<uint8_t>(),
-                         t->u_voff.as<uint64_t>(), nb, bdig, t->st);
+                         t->u_voff.as<uint64_t>(), nb, bdig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(nb)), t->st);
         prof_end(t, pl);
     }
     const SortedSet B = sort_unique(t, t->u_kb.as<uint8_t>(), t->u_koff.as<uint64_t>(), nb, tomb, false);
@@ -1572,7 +1514,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
 }
 
 static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *values, const uint8_t *is_remove) {
-    if (t->n > 0 && !t->sharded && !t->prepared && merge_enabled()) {
+    if (t->n > 0 && !t->sharded && !t->prepared) {
         merge_batch(t, keys, values, is_remove);
         return;
     }
@@ -1584,7 +1526,8 @@ static void apply_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     if (values && keys.n) {
         size_t pl = prof_begin(t, "leaf_hash");
         launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>() + m, t->s_vb.as<uint8_t>(),
-                         t->s_voff.as<uint64_t>(), keys.n, t->s_dig.as<uint8_t>() + 32 * m, t->st);
+                         t->s_voff.as<uint64_t>(), keys.n, t->s_dig.as<uint8_t>() + 32 * m,
+                         ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(keys.n)), t->st);
         prof_end(t, pl);
     }
     sort_dedup_gather(t, t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), tot, t->in_tomb, true, kbytes, true);
@@ -1643,7 +1586,7 @@ static DirtyTree dirty_prepare(mkv_tree *t, const DirtyBatch &b) {
     const uint64_t *ps = locate_samples_of(t, st, &ns);
     launch_locate(b.kb, b.koff, m, side_of(t), ps, ns, pos, idx, cnt + L + 1, st);
     uint8_t *bdig = ens<uint8_t>(t->u_dig, m * 32);
-    launch_leaf_hash(b.kb, b.koff, b.vb, b.voff, m, bdig, st);
+    launch_leaf_hash(b.kb, b.koff, b.vb, b.voff, m, bdig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(m)), st);
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
     const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, m, 0, std::max(8, bits_for(t->n)), radix, st);
     uint32_t *l0 = ens<uint32_t>(t->u_l0, m + 1), *l1 = ens<uint32_t>(t->u_l1, m + 1);
@@ -1776,25 +1719,17 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         size_t ltop = 0;
         // The fused top runs in one workgroup per tree: a level of more than ~1K dirty nodes takes it
         // several serial hash rounds on one CU (4,096 nodes: ~70 us), while a per-level launch spreads
-        // them over the chip; so the per-level launches continue down to MKV_DIRTY_TOP (default 1,024)
+        // them over the chip; so the per-level launches continue down to 1,024
         // entries (configs[4]: fused top 227 -> ~110 us per step).
-        static const uint64_t top_switch = [] {
-            const char *e = getenv("MKV_DIRTY_TOP");
-            const long v = e ? atol(e) : 1024;
-            return (uint64_t)std::min<long>(std::max<long>(v, 1), (long)DIRTY_TOP_CAP);
-        }();
+        constexpr uint64_t top_switch = 1024;
         while (ltop < L && std::min<uint64_t>(mmax, t0->lev_cnt[ltop]) > top_switch) ++ltop;
         // Large batches: entries do not clear their children's dirty bits (two device atomics per entry
         // and level, serialised per address); the bitmap is cleared by one memset before the next update
         // instead (nn / 8 bytes). Taken when the batches hold at least one key per 4,096 bitmap bits
-        // (configs[4]: update 2.18 -> 2.04 ms); MKV_DIRTY_KEEP_BITS=0/1 forces either form.
-        static const int keep_env = [] {
-            const char *e = getenv("MKV_DIRTY_KEEP_BITS");
-            return e ? atoi(e) : -1;
-        }();
+        // (configs[4]: update 2.18 -> 2.04 ms).
         uint64_t msum = 0;
         for (size_t q = 0; q < g.size(); ++q) msum += bs[g[q]].m;
-        const bool keep_bits = keep_env >= 0 ? keep_env == 1 : msum * 4096 >= total_nodes(t0);
+        const bool keep_bits = msum * 4096 >= total_nodes(t0);
         if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
         const size_t pclimb = prof_begin(t0, "climb", st);
         for (size_t l = 0; l < ltop; ++l) {
@@ -2207,30 +2142,6 @@ static bool same_plan(const mkv_tree *a, const mkv_tree *b) {
 
 constexpr size_t TD_CHECK_LEVEL = 4;
 
-static bool topdown_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("MKV_DIFF_TOPDOWN");  // A/B measurement knob: 0 = always merge-join
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-static bool jumps_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("MKV_TD_JUMP");  // A/B knob: 0 = one launch per level
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
-static bool fine_jumps() {
-    static const bool on = [] {
-        const char *e = getenv("MKV_TD_FINE");  // A/B knob: 0 = 4-level jumps down to the leaves (batched walk)
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // Levels the jumping walk lands on: the top level, then every multiple of 4 below it down to 0.
 // fine: below level 8 every multiple of 2 instead. A jump of k levels reads 2^k digests per frontier
 // node; near the leaves of a dense diff the frontier holds about one node per divergent leaf, so
@@ -2265,7 +2176,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
-    if (!a->sharded && !b->sharded && L > 1 && jumps_enabled()) {
+    if (!a->sharded && !b->sharded && L > 1) {
         // Unsharded: seed with the root, then jump 4 levels per launch (landing on level 4 for the
         // key-shift check and on level 0).
         launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
@@ -2333,14 +2244,6 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     return true;
 }
 
-static bool onewait_enabled() {
-    static const bool on = [] {
-        const char *e = getenv("MKV_DIFF_ONEWAIT");  // A/B knob: 0 = the round-2 walk with 4 host waits
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 // Unsharded top-down pair diff queued whole before ONE host wait (round 3): the jumping walk, the level-4
 // abort test on the device (k_td_gate), the divergent positions (bitmap, device count) written straight
 // into refs, the leaf-key check, key lengths, scan, key gather and the copy into a mapped pinned block
@@ -2348,6 +2251,9 @@ static bool onewait_enabled() {
 // walk was abandoned: merge-join) or 2 (the list outgrew the pinned capacity: refs hold *m_out sorted
 // positions; the caller copies them with keylist_from_refs). Round 2 waited four times: level-4 count,
 // leaf count, key bytes, result.
+constexpr uint64_t TAIL_MIN_KEYS = 4096;        // smallest staging capacity of the one-wait diff (keys)
+constexpr uint64_t TAIL_COPY_MAX = 1ull << 20;  // results up to 1 MiB are copied out of the staging block
+
 static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, const DiffSide &A,
                                          const DiffSide &B, uint64_t *refs, int *fallback, uint64_t *m_out) {
     *fallback = 0;
@@ -2360,7 +2266,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 2);
     uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2);
     if (!t->tail_cap_m) {
-        t->tail_cap_m = std::max<uint64_t>(65536, n / 256);
+        t->tail_cap_m = std::max<uint64_t>(TAIL_MIN_KEYS, n / 1024);
         t->tail_cap_b = 48 * t->tail_cap_m;
     }
     const uint64_t cap_m = t->tail_cap_m, cap_b = t->tail_cap_b;
@@ -2372,7 +2278,10 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     void *scr = t->d_diffscr.ensure(scan_scratch_bytes(cap_m + 1));
     uint8_t *kout = ens<uint8_t>(t->d_out, cap_b + 16);
     const uint64_t kpos = (8 * (cap_m + 1) + 15) & ~uint64_t(15);
-    auto blk = std::make_shared<PinnedBlock>(kpos + cap_b + 16);
+    // the staging block is the tree's own, reused call to call unless an earlier result still holds it
+    if (!t->tail_blk || t->tail_blk.use_count() > 1 || t->tail_blk->cap < kpos + cap_b + 16)
+        t->tail_blk = std::make_shared<PinnedBlock>(kpos + cap_b + 16);
+    std::shared_ptr<PinnedBlock> blk = t->tail_blk;
     const size_t pd = prof_begin(t, "diff");  // the queued device work (the wait excluded)
     MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
     launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
@@ -2419,12 +2328,30 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         *m_out = m;
         return nullptr;
     }
+    // capacity follows the results: halve towards twice this call's size (a burst of large diffs does not
+    // keep every later staging block large)
+    t->tail_cap_m = std::max<uint64_t>({TAIL_MIN_KEYS, 2 * m, cap_m / 2});
+    t->tail_cap_b = std::max<uint64_t>({48 * TAIL_MIN_KEYS, 2 * bytes, cap_b / 2});
     auto *l = new mkv_keylist();
     l->n = m;
     if (m) {
-        l->blk = blk;
-        l->offsets = reinterpret_cast<const uint64_t *>(blk->p);
-        l->bytes = blk->p + kpos;
+        const uint64_t used = 8 * (m + 1) + bytes;
+        if (used <= TAIL_COPY_MAX && 8 * used <= blk->cap) {
+            // a small result in a large staging block: the list gets a block of its own size (a caller that
+            // keeps many results alive must not pin a capacity-sized block for each), the tree keeps the
+            // staging block for its next call
+            auto own = std::make_shared<PinnedBlock>(used + 16);
+            std::memcpy(own->p, blk->p, 8 * (m + 1));
+            std::memcpy(own->p + 8 * (m + 1), blk->p + kpos, bytes);
+            l->blk = own;
+            l->offsets = reinterpret_cast<const uint64_t *>(own->p);
+            l->bytes = own->p + 8 * (m + 1);
+        } else {
+            l->blk = blk;  // a large result: handed over whole; the next call stages into a fresh block
+            t->tail_blk.reset();
+            l->offsets = reinterpret_cast<const uint64_t *>(blk->p);
+            l->bytes = blk->p + kpos;
+        }
     }
     return l;
 }
@@ -2481,6 +2408,7 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
 
 static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     mkv_tree *t = const_cast<mkv_tree *>(a);
+    t->walk_L = 0;  // td_cnt is about to hold a pair walk's counters: no batched-walk stats any more
     // b's last work must be complete before a's stream reads it
     wait_idle(b->st);
     HTRACE("diff-start");
@@ -2490,15 +2418,15 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     uint64_t m = 0;
     bool done = false;
     const uint64_t nwords = (A.n + 31) / 32;
-    if (A.n > 0 && same_plan(a, b) && topdown_enabled() && onewait_enabled() && !a->sharded && !b->sharded &&
-        a->lev_S.size() > 1 && jumps_enabled() && ceil_div(nwords, 1024) <= 8192) {
+    if (A.n > 0 && same_plan(a, b) && !a->sharded && !b->sharded && a->lev_S.size() > 1 &&
+        ceil_div(nwords, 1024) <= 8192) {
         int fb = 0;
         mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);
         HTRACE("topdown-done");
         if (l) return l;
         if (fb == 2) return keylist_from_refs(t, refs, m, A, B);
         m = 0;  // key sets differ (or the walk was abandoned): the merge-join below
-    } else if (A.n > 0 && same_plan(a, b) && topdown_enabled()) {
+    } else if (A.n > 0 && same_plan(a, b)) {
         // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
         size_t pd = prof_begin(t, "diff");
         const uint32_t *nbad = nullptr;
@@ -2516,38 +2444,17 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     if (!done) {
         size_t pd = prof_begin(t, "diff");
         uint64_t *cnt = ens<uint64_t>(t->s_misc, 64);
-        bool ran = false;
-        if (fused_diff_enabled()) {
-            void *scr = t->d_diffscr.ensure(diff_fused_scratch_bytes(M));
-            const size_t sw = diff_fused_status_words(M);
-            const bool fresh = t->d_status.cap < 8 * sw || !t->d_status.p;
-            uint64_t *status = ens<uint64_t>(t->d_status, sw);
-            // epochs 1 .. 2^22 - 1 (never the zeroed tag); a wrap clears the words an older call left
-            if (fresh || ++t->diff_epoch >= (1u << 22)) {
-                MKV_HIP(hipMemsetAsync(status, 0, t->d_status.cap, t->st));
-                t->diff_epoch = 1;
-            }
-            launch_diff_fused(A, B, scr, status, t->diff_epoch, refs, cnt, t->st);
+        void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
+        launch_diff(A, B, scr, refs, cnt, t->st, true);
+        prof_end(t, pd);
+        small_d2h(t, t->h_small, cnt, 16, t->st);  // count + deferred-check verdict
+        wait_stream(t, t->st);
+        m = t->h_small[0];
+        if (t->h_small[1]) {  // equal prefixes with different keys (or too many checks): exact rerun
+            pd = prof_begin(t, "diff");
+            launch_diff(A, B, scr, refs, cnt, t->st, false);
             prof_end(t, pd);
-            small_d2h(t, t->h_small, cnt, 16, t->st);
-            wait_stream(t, t->st);
-            m = t->h_small[0];
-            ran = t->h_small[1] == 0;  // else a look-back gave up: the multi-pass form below
-            if (!ran) pd = prof_begin(t, "diff");
-        }
-        if (!ran) {
-            void *scr = t->d_diffscr.ensure(diff_scratch_bytes(M));
-            launch_diff(A, B, scr, refs, cnt, t->st, defer_enabled());
-            prof_end(t, pd);
-            small_d2h(t, t->h_small, cnt, 16, t->st);  // count + deferred-check verdict
-            wait_stream(t, t->st);
-            m = t->h_small[0];
-            if (t->h_small[1]) {  // equal prefixes with different keys (or too many checks): exact rerun
-                pd = prof_begin(t, "diff");
-                launch_diff(A, B, scr, refs, cnt, t->st, false);
-                prof_end(t, pd);
-                m = d2h_u64(t, cnt);
-            }
+            m = d2h_u64(t, cnt);
         }
     }
     return keylist_from_refs(t, refs, m, A, B);
@@ -2576,11 +2483,11 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     t->walk_L = (uint32_t)L;
     t->walk_k = k;
     const size_t pwalk = prof_begin(t, "walk");
-    if (!sharded && L > 1 && jumps_enabled()) {  // seed with every variant's root, then jump 4 levels per launch
+    if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
         launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
                                    fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
         std::swap(fin, fout);
-        const std::vector<size_t> T = jump_targets(L, fine_jumps());
+        const std::vector<size_t> T = jump_targets(L, true);
         for (size_t q = 1; q < T.size(); ++q) {
             const size_t l = T[q - 1], lt = T[q];
             const int kk = (int)(l - lt);
@@ -2703,7 +2610,7 @@ mkv_status mkv_tree_diff_many(const mkv_tree *a, const mkv_tree *const *others, 
             for (uint32_t i = 0; i < k; ++i) wait_idle(others[i]->st);
             // candidates for the shared walk: same level plan and a clean key-set screen
             std::vector<uint32_t> cand;
-            if (a->n > 0 && topdown_enabled()) {
+            if (a->n > 0) {
                 for (uint32_t i = 0; i < k; ++i)
                     if (same_plan(a, others[i])) cand.push_back(i);
             }
@@ -3396,9 +3303,9 @@ mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint
             upload_blob(t, keys, t->s_kb, t->s_koff);
             upload_blob(t, values, t->s_vb, t->s_voff);
             uint8_t *dig = ens<uint8_t>(t->s_dig, (n ? n : 1) * 32);
-            // the build's leaf-hash path (k_leaf_direct + k_leaf_list for other shapes)
+            // the build's leaf stage (k_leaf_direct, then k_leaf_ragged for other shapes)
             launch_leaf_hash(t->s_kb.as<uint8_t>(), t->s_koff.as<uint64_t>(), t->s_vb.as<uint8_t>(),
-                             t->s_voff.as<uint64_t>(), n, dig, t->st, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)));
+                             t->s_voff.as<uint64_t>(), n, dig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)), t->st);
             if (n) MKV_HIP(hipMemcpyAsync(out, dig, 32 * n, hipMemcpyDeviceToHost, t->st));
             MKV_HIP(hipStreamSynchronize(t->st));
         } catch (...) {

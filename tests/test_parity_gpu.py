@@ -404,6 +404,36 @@ def test_topdown_value_only_vs_oracle(oracle_lib, n, stride):
     assert b.diff_keys_bytes(a) == want
 
 
+@pytest.mark.parametrize("n,klen,stride", [(400_000, 32, 48), (100_000, 200, 48)])
+def test_topdown_onewait_capacity_overflow_and_regrowth(oracle_lib, n, klen, stride):
+    """The one-wait top-down diff stages its key list in a capacity sized from earlier calls. First call on
+    a fresh handle: the list outgrows it (more keys than the capacity, or more key bytes: 200-B keys) and
+    the refs path copies it; the capacity grows, so the second call fits (a large result: the staging
+    block is handed over); a one-key diff then gets a right-sized copy. Every result equals the oracle's
+    (/root/reference/src/store/merkle.rs:171-196)."""
+    kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED + 9, 0, n, klen=klen, vlen=100)
+    vb2 = vb.copy().reshape(n, 100)
+    vb2[::stride, 7] ^= 1
+    vb2 = vb2.reshape(-1)
+    vb3 = vb.copy().reshape(n, 100)
+    vb3[n // 2, 0] ^= 1
+    vb3 = vb3.reshape(-1)
+    a, b, c = MerkleTree(), MerkleTree(), MerkleTree()
+    a.build((kb, ko), (vb, vo))
+    b.build((kb, ko), (vb2, vo))
+    c.build((kb, ko), (vb3, vo))
+    oa = oracle_lib.OracleTree.build(kb, ko, vb, vo)
+    want_b = oa.diff(oracle_lib.OracleTree.build(kb, ko, vb2, vo))
+    want_c = oa.diff(oracle_lib.OracleTree.build(kb, ko, vb3, vo))
+    assert len(want_b) == len(range(0, n, stride)) and len(want_c) == 1
+    first = a.diff_keys_bytes(b)   # overflow: copied from the refs
+    second = a.diff_keys_bytes(b)  # fits the grown capacity
+    small = a.diff_keys_bytes(c)   # right-sized copy of a one-key list
+    again = a.diff_keys_bytes(b)
+    assert first == want_b and second == want_b and again == want_b
+    assert small == want_c
+
+
 def test_topdown_positions_across_bitmap_blocks(oracle_lib):
     """Divergent leaves at chosen sorted positions: word / uint4 / 32768-leaf block edges, a dense run
     and the last leaf (the sorted-position compaction of the walk); repeated diffs on one handle, then a

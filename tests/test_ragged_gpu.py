@@ -1,6 +1,7 @@
-"""Ragged records: the bucketed LDS-materialising leaf kernel (k_leaf_ragged) against
-the C oracle — store-like key / value lengths at arbitrary byte offsets, every padding / window / class
-edge, blob bases at every byte alignment, and records far larger than one window.
+"""Ragged records: the lane-refill leaf kernel (k_leaf_ragged, csrc/k_ragged.hip) against the C oracle —
+store-like key / value lengths at arbitrary byte offsets, every padding / block / run edge, blob bases at
+every byte alignment, records of thousands of blocks beside one-block ones, fixed-shape chunks handed
+over by k_leaf_direct, and the key-ownership copy of the records the ragged stage hashed.
 Reference inputs are arbitrary &str pairs (/root/reference/src/store/merkle.rs:7-16, :45-49;
 /root/reference/src/sync.rs:109-115)."""
 import hashlib
@@ -65,9 +66,9 @@ def test_ragged_device_generator_matches_oracle():
 
 
 def _edge_records(rng):
-    """Lengths at every field / padding / window / class edge: total encodings L = 8 + k + v around
-    55/56 (1 -> 2 blocks), 183/184 (3 -> 4 blocks: the window edge), 375/376 (6 -> 7), 1975 (31 blocks),
-    1976+ (class 31 = 32 blocks and more), with every key length mod 4."""
+    """Lengths at every field / padding / block edge: total encodings L = 8 + k + v around 55/56 (1 -> 2
+    blocks), 119/120, 183/184, 247/248, 375/376, 1975/1976 and beyond, with every key length mod 4 and keys
+    that end in the first, second or a later block (the key run / value run splice positions)."""
     keys, vals = [], []
     for Lt in (8, 9, 12, 54, 55, 56, 57, 63, 64, 119, 120, 183, 184, 185, 247, 248, 375, 376, 377, 1975, 1976, 1977,
                2100, 5000):
@@ -83,7 +84,7 @@ def _edge_records(rng):
 def test_ragged_window_and_class_edges_vs_hashlib():
     rng = np.random.default_rng(11)
     keys, vals = _edge_records(rng)
-    # shuffled, so that 64-record chunks mix classes before the bucketing
+    # shuffled, so that lanes of one wave run records of very different block counts
     order = rng.permutation(len(keys))
     keys = [keys[i] for i in order]
     vals = [vals[i] for i in order]
@@ -140,3 +141,62 @@ def test_ragged_mixed_with_fixed_chunks_and_duplicates():
     t.build(keys, vals)
     assert t.get_root_hash() == o.root()
     assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
+
+
+def test_ragged_long_records_beside_short_ones_vs_hashlib():
+    """Lane refill: a few records of thousands of blocks (a 256 KiB value, a 12 KiB key) keep their lanes
+    busy while the other lanes of the wave take hundreds of one- to four-block records."""
+    rng = np.random.default_rng(23)
+    keys, vals = [], []
+    for i in range(3000):
+        if i % 997 == 5:
+            keys.append(rng.integers(0, 256, size=int(rng.integers(0, 12_000)), dtype=np.uint8).tobytes())
+            vals.append(rng.integers(0, 256, size=int(rng.integers(100_000, 262_144)), dtype=np.uint8).tobytes())
+        else:
+            keys.append(rng.integers(0, 256, size=int(rng.integers(0, 70)), dtype=np.uint8).tobytes())
+            vals.append(rng.integers(0, 256, size=int(rng.integers(0, 200)), dtype=np.uint8).tobytes())
+    got = leaf_digests(keys, vals)
+    for k, v, g in zip(keys, vals, got):
+        assert g == _enc_digest(k, v), (len(k), len(v))
+
+
+@pytest.mark.parametrize("layout", ["ragged", "fixed_then_ragged", "ragged_then_fixed"])
+def test_ragged_build_device_owns_its_keys(layout):
+    """build_device from borrowed device blobs: the tree keeps its own copy of the keys (the fixed-shape
+    kernel copies the chunks it hashes, k_keycopy_rest the ones it hands to the ragged stage), so after
+    the caller overwrites its buffers the sorted keys, a diff and a rebuilt root still equal the oracle's.
+    The second build reuses the first one's key buffer (the fused-copy path)."""
+    import torch
+    n = 64 * 300 + 17
+    fk, fko, fv, fvo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    rk, rko, rv, rvo = coracle.gen_records(DEFAULT_SEED, 10**6, n, klen=64, vlen=256, ragged=2)
+    split = {"ragged": 0, "fixed_then_ragged": 64 * 200 + 5, "ragged_then_fixed": 64 * 100}[layout]
+    keys, vals = [], []
+    for i in range(n):
+        fixed = (i < split) if layout == "fixed_then_ragged" else (layout == "ragged_then_fixed" and i >= split)
+        src = (fk, fko, fv, fvo) if fixed else (rk, rko, rv, rvo)
+        keys.append(src[0][int(src[1][i]):int(src[1][i + 1])].tobytes())
+        vals.append(src[2][int(src[3][i]):int(src[3][i + 1])].tobytes())
+    (pk, pko), (pv, pvo) = pack(keys), pack(vals)
+    o = coracle.OracleTree.build(pk, pko, pv, pvo)
+    dk = torch.from_numpy(pk.copy()).cuda()
+    dv = torch.from_numpy(pv.copy()).cuda()
+    dko = torch.from_numpy(pko.astype(np.int64)).cuda()
+    dvo = torch.from_numpy(pvo.astype(np.int64)).cuda()
+    torch.cuda.synchronize()
+    t = MerkleTree()
+    for _ in range(2):
+        t.build_device(dk.data_ptr(), dko.data_ptr(), dv.data_ptr(), dvo.data_ptr(), n)
+    dk.fill_(0x5A)
+    dko.fill_(0)
+    torch.cuda.synchronize()
+    assert t.get_root_hash() == o.root()
+    assert [k for k, _ in t.leaves()] == [k.decode("utf-8", "surrogateescape") for k, _ in o.leaves()]
+    # a replica with a few changed values: the diff names keys from the tree's own copy
+    vals2 = list(vals)
+    for i in range(0, n, 97):
+        vals2[i] = vals2[i] + b"!"
+    o2 = coracle.OracleTree.from_pairs(list(zip(keys, vals2)))
+    t2 = MerkleTree()
+    t2.build(keys, vals2)
+    assert t.diff_keys_bytes(t2) == o.diff(o2)
