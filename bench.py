@@ -742,6 +742,10 @@ def diff_modes(ctx, n, steps, warmup, gather=False):
                      "ms": el / steps * 1e3, "device_ms": dms / max(steps, 1),
                      "keys_per_s": union * steps / el,
                      "path": "top-down" if mode == "value_only" else "merge-join"}
+        if mode == "value_only":
+            res[mode]["roofline"] = topdown_roofline(A.walk_stats(), len(d), res[mode]["device_ms"])
+        else:
+            res[mode]["roofline"] = merge_roofline(n + new, res[mode]["device_ms"])
         if gather and ctx.dist is not None:
             # the global sorted list on every rank (sync.rs:67-83 consumes it whole): local diff +
             # all-gather-v of key lengths and bytes; this rank's slice must sit at its global offset
@@ -770,23 +774,48 @@ def diff_modes(ctx, n, steps, warmup, gather=False):
     return res
 
 
+def merge_roofline(union_keys_per_rank, device_ms):
+    """The merge-join diff (mixed divergence): 80 B per union key (8-B prefix + 32-B leaf digest, both
+    trees: SURVEY §8(d)) over the device time of the whole diff call; traffic = PMC HBM bytes of its
+    kernels from profiles/pmc_diff_merge.json when that file describes a diff of this size."""
+    achieved = DIFF_BYTES_PER_KEY * union_keys_per_rank / (device_ms * 1e-3) / 1e9
+    traffic, src = None, None
+    try:
+        pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_diff_merge.json")))
+        if pm.get("union_keys") == union_keys_per_rank:  # the PMC file is per rank
+            traffic, src = pm.get("hbm_bytes_per_diff"), pm.get("source")
+    except (OSError, ValueError):
+        pass
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+            "kernel": "k_diff_pass1 + k_diff_pass2 (merge-join)", "bytes_per_union_key": DIFF_BYTES_PER_KEY,
+            "algorithmic_bytes": DIFF_BYTES_PER_KEY * union_keys_per_rank, "device_ms": device_ms,
+            "note": "achieved = 80 B x union keys / device time of the whole diff call (partition, passes, "
+                    "verify, key gather)"}
+
+
+def topdown_roofline(ws, m, device_ms):
+    """The top-down walk (value-only divergence): the digest bytes the walk compared (mkv_tree_walk_stats:
+    2^k descendants x 32 B x both trees per expanded frontier node) plus the divergent leaves' tail (the
+    leaf-key check reads perm + two offsets + the key on both sides, the key gather reads the key and
+    offsets and writes the list: ~184 B per divergent key), over the device time of the call. The walk
+    is a chain of dependent launches, so it is latency- rather than bandwidth-bound."""
+    walk_bytes = ws.get("bytes", 0) if ws else 0
+    tail_bytes = 184 * m
+    algo = walk_bytes + tail_bytes
+    achieved = algo / (device_ms * 1e-3) / 1e9 if device_ms else None
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+            "kernel": "k_topdown_jump chain + bitmap positions + key tail", "walk_bytes": walk_bytes,
+            "walk_entries": ws.get("entries") if ws else None, "launches": ws.get("launches") if ws else None,
+            "tail_bytes": tail_bytes, "algorithmic_bytes": algo, "device_ms": device_ms,
+            "note": "latency-bound walk: %s dependent jump launches; frac reported against 8 TB/s anyway"
+                    % (ws.get("launches") if ws else "?")}
+
+
 def diff_roofline(res):
     m = res["mixed"]
-    achieved = DIFF_BYTES_PER_KEY * m["union_keys_per_rank"] / (m["device_ms"] * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_diff_merge.json")
-    try:
-        pm = json.load(open(pmc_path))
-        # the PMC file is per rank: it must describe this rank's diff (same union size)
-        if pm.get("union_keys") == m["union_keys_per_rank"]:
-            traffic = pm.get("hbm_bytes_per_diff")
-    except (OSError, ValueError):
-        pm = None
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "merge-join diff (mixed)",
-            "bytes_per_union_key": DIFF_BYTES_PER_KEY,
-            "note": "achieved = 80 B x union keys / device time of the whole diff call (partition, both passes, "
-                    "key gather); traffic = PMC HBM bytes of its merge-join kernels"}
+    return merge_roofline(m["union_keys_per_rank"], m["device_ms"])
 
 
 def wl_diff(ctx, args):

@@ -175,6 +175,54 @@ mkv_status mkv_shard_fringe_device(const mkv_tree *t, uint8_t *dout);
 mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32_t world, uint64_t stride_bytes,
                                     uint64_t global_n, uint8_t out32[32], int *has_root);
 
+/* ---------------- multi-GPU over a communicator: the collectives inside the library --------
+ * One process per GPU; rank r holds the records of key range r, ranges ordered by rank. The sharded entry
+ * points run the all-gathers themselves, so a host in any language (the reference's SyncManager is Rust,
+ * sync.rs:56-87) needs no collective layer of its own. Two communicator forms:
+ *   RCCL (xGMI): mkv_comm_unique_id on one rank, the 128 bytes shared out of band (TCP, a file, MPI),
+ *     then mkv_comm_init_rank on every rank (ncclCommInitRank). Payloads stay in device memory.
+ *   host: mkv_comm_create_host with the caller's all-gather (gloo, MPI, a test harness): fn gathers
+ *     `bytes` from every rank into recv in rank order (host memory) and returns 0.
+ * Replaces: the host-side count / fringe / key-list exchanges a caller had to write around
+ * mkv_shard_* (above); the reference itself has no sharding (one MerkleTree per node, merkle.rs:27-32). */
+typedef struct mkv_comm mkv_comm;
+#define MKV_COMM_ID_BYTES 128
+typedef int (*mkv_allgather_fn)(void *ctx, const void *send, void *recv, uint64_t bytes);
+mkv_status mkv_comm_unique_id(uint8_t id[MKV_COMM_ID_BYTES]);
+mkv_status mkv_comm_init_rank(const uint8_t id[MKV_COMM_ID_BYTES], int rank, int world, int hip_device, mkv_comm **out);
+mkv_status mkv_comm_create_host(int rank, int world, mkv_allgather_fn fn, void *ctx, mkv_comm **out);
+mkv_status mkv_comm_rank(const mkv_comm *c, int *rank, int *world);
+/* All-gather of `bytes` host bytes per rank through the communicator (recv: world x bytes, rank order);
+ * what the sharded entry points use for their metadata. Collective; needs no GPU in the host form. */
+mkv_status mkv_comm_all_gather(mkv_comm *c, const void *send, void *recv, uint64_t bytes);
+/* Per-kind collective timings since creation / the last reset: host wall seconds around each all-gather
+ * and the wait for its result, calls, payload bytes per rank. Kinds: */
+#define MKV_COLL_COUNTS 0 /* leaf counts (8 B) */
+#define MKV_COLL_RANGE 1  /* range check: first / last key per shard */
+#define MKV_COLL_FRINGE 2 /* seam fringes (k x MKV_FRINGE_BYTES) */
+#define MKV_COLL_DIFF 3   /* divergent-key all-gather-v (meta + padded blocks) */
+#define MKV_COLL_KINDS 4
+mkv_status mkv_comm_stats(mkv_comm *c, double secs[MKV_COLL_KINDS], uint64_t calls[MKV_COLL_KINDS],
+                          uint64_t bytes[MKV_COLL_KINDS], int reset);
+void mkv_comm_destroy(mkv_comm *c);
+/* Collective sharded build of this rank's records (device blobs when on_device != 0, else host blobs):
+ * hash + sort + dedup, all-gather of the leaf counts, range check when range_check != 0 (every shard's
+ * keys below the next non-empty shard's, else MKV_EINVAL; three more small all-gathers), in-shard
+ * reduction, fringe all-gather, device seam combine. Afterwards mkv_tree_root is the GLOBAL root on every
+ * rank, bit-exact with one tree over all records (merkle.rs:73-121). counts_out (optional, world
+ * entries): every rank's leaf count. */
+mkv_status mkv_sharded_build(mkv_tree *t, mkv_comm *c, mkv_blob keys, mkv_blob values, int on_device,
+                             int range_check, uint64_t *counts_out);
+/* Global root again after in-place updates of the shard (mkv_tree_upsert[_device] of keys in its range):
+ * fringe all-gather + seam combine (merkle.rs:52-56 then :65-67). _many: k replicas of one key range, ONE
+ * all-gather for all of them; roots = k x 32 bytes. */
+mkv_status mkv_sharded_root(mkv_tree *t, mkv_comm *c, uint8_t out32[32], int *has_root);
+mkv_status mkv_sharded_root_many(mkv_tree *const *ts, uint32_t k, mkv_comm *c, uint8_t *roots, int *has_root);
+/* diff_keys (merkle.rs:171-196) of two sharded trees over the same partition, as ONE sorted list on every
+ * rank — what SyncManager::sync_once consumes (sync.rs:67): local device diff, all-gather of (count,
+ * bytes), all-gather of [u32 lengths | key bytes] blocks. Rank order is key order. */
+mkv_status mkv_sharded_diff(const mkv_tree *a, const mkv_tree *b, mkv_comm *c, mkv_keylist **out);
+
 /* ---------------- redistribution of unpartitioned input ----------------
  * The sharded build needs rank r to hold every key of range r. Records that sit on the ranks in no key
  * order (a store snapshot per GPU, as sync.rs:104-143 collects one) are moved there with one all-to-all:
@@ -212,9 +260,10 @@ mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms,
 /* Synthetic records (same generator as oracle/merkle_oracle.c) written to device buffers:
  * kb >= n*klen, vb >= n*vlen, koff/voff n+1 entries. Synchronous. */
 /* Introspection (benches / tests): per-level dirty entry counts of the tree's last dirty-path update
- * (level 0 = changed leaves, level l > 0 = rehashed nodes), and the last batched top-down walk this tree
- * ran as the base (mkv_tree_diff_many): out[0] = frontier entries expanded, out[1] = digest bytes the walk
- * compared, out[2] = divergent leaf positions, out[3] = launches. Both synchronise the tree's stream. */
+ * (level 0 = changed leaves, level l > 0 = rehashed nodes), and the last top-down walk this tree ran as
+ * the base (a batched walk of mkv_tree_diff_many or an unsharded pair walk of mkv_tree_diff):
+ * out[0] = frontier entries expanded, out[1] = digest bytes the walk compared, out[2] = divergent leaf
+ * positions, out[3] = launches. Both synchronise the tree's stream. */
 mkv_status mkv_tree_update_counts(const mkv_tree *t, uint64_t *out, uint32_t cap, uint32_t *nlevels);
 mkv_status mkv_tree_walk_stats(const mkv_tree *t, uint64_t out[4]);
 mkv_status mkv_gen_records_device(int hip_device, uint64_t seed, uint64_t idx0, uint64_t n, uint32_t klen,

@@ -32,7 +32,14 @@ EXPORTS = [
     "mkv_tree_build_digests", "mkv_tree_hash_pattern", "mkv_shard_fringe_device", "mkv_shard_combine_device",
     "mkv_pool_trim", "mkv_pool_stats", "mkv_debug_trace",
     "mkv_route_sample", "mkv_route_splitters", "mkv_route_plan", "mkv_route_pack", "mkv_route_offsets",
+    "mkv_comm_unique_id", "mkv_comm_init_rank", "mkv_comm_create_host", "mkv_comm_rank", "mkv_comm_destroy",
+    "mkv_comm_stats", "mkv_comm_all_gather", "mkv_sharded_build", "mkv_sharded_root", "mkv_sharded_root_many", "mkv_sharded_diff",
 ]
+
+COMM_ID_BYTES = 128
+COLL_KINDS = ["counts_all_gather", "range_all_gather", "fringe_all_gather", "diff_all_gather_v"]  # MKV_COLL_*
+# int (*mkv_allgather_fn)(void *ctx, const void *send, void *recv, uint64_t bytes)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
 
 
 class MerkleError(RuntimeError):
@@ -110,6 +117,17 @@ def lib():
         "mkv_route_plan": ([vp, Blob, Blob, u32, vp, vp], i32),
         "mkv_route_pack": ([vp, Blob, Blob, vp, vp, vp, vp], i32),
         "mkv_route_offsets": ([vp, vp, u64, vp], i32),
+        "mkv_comm_unique_id": ([vp], i32),
+        "mkv_comm_init_rank": ([vp, i32, i32, i32, P(vp)], i32),
+        "mkv_comm_create_host": ([i32, i32, ALLGATHER_FN, vp, P(vp)], i32),
+        "mkv_comm_rank": ([vp, P(i32), P(i32)], i32),
+        "mkv_comm_destroy": ([vp], None),
+        "mkv_comm_stats": ([vp, vp, vp, vp, i32], i32),
+        "mkv_comm_all_gather": ([vp, vp, vp, u64], i32),
+        "mkv_sharded_build": ([vp, vp, Blob, Blob, i32, i32, vp], i32),
+        "mkv_sharded_root": ([vp, vp, vp, P(i32)], i32),
+        "mkv_sharded_root_many": ([P(vp), u32, vp, vp, vp], i32),
+        "mkv_sharded_diff": ([vp, vp, vp, P(vp)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -67,3 +67,15 @@ struct DevBuf {
 static inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 
 }  // namespace mkv
+
+struct mkv_keylist;
+struct mkv_tree;
+namespace mkv {
+// tree.cpp internals shared with comm.cpp: a library-owned key list (pinned host block) over host bytes
+// (offsets[0] == 0); the thread's mkv_last_error message; a tree's global leaf count (its shard plan's N,
+// or n when unsharded).
+mkv_keylist *keylist_from_host(const uint8_t *bytes, const uint64_t *offsets, uint64_t n);
+void set_last_error(const char *msg);
+uint64_t tree_global_n(const mkv_tree *t);
+
+}  // namespace mkv

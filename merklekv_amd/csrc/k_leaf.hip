@@ -289,41 +289,27 @@ __device__ __forceinline__ void load_words_a4(const uint8_t *p, uint32_t *w) {
     for (uint32_t i = NW / 4 * 4; i < NW; ++i) w[i] = reinterpret_cast<const uint32_t *>(p)[i];
 }
 
-template <uint32_t NW>
-__device__ __forceinline__ void store_words_a4(uint8_t *p, const uint32_t *w) {
-    u32x4_a4 *q = reinterpret_cast<u32x4_a4 *>(p);
-#pragma unroll
-    for (uint32_t i = 0; i < NW / 4; ++i) q[i] = u32x4_a4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
-#pragma unroll
-    for (uint32_t i = NW / 4 * 4; i < NW; ++i) reinterpret_cast<uint32_t *>(p)[i] = w[i];
-}
-
-constexpr uint32_t LEAF_GRAIN = 4;  // k_leaf_direct: chunks per hand-out atomic
 
 // Fixed-shape records (the configs' 32-B keys / 100-B values at 4-B alignment): each lane loads its own
 // record's 33 message words straight from HBM into VGPRs with 16-B loads at 4-B alignment (gfx950 serves
 // unaligned global loads; a wave's 64 records are contiguous, so it touches the cache lines a coalesced
 // copy would), byte-swaps them and runs the three compressions with the constant words folded at compile
-// time. No LDS: the ordering kernels co-running on the aux stream keep the CU's whole LDS. Chunks (64
-// records) come from a device counter, LEAF_GRAIN per atomic, so waves on CUs that also run ordering
-// workgroups simply take fewer. A chunk of any other shape ends the kernel's hand-out (leaf.hpp): one
-// atomicMax pushes the counter past every chunk, the wave lists the rest of its grab for k_leaf_ragged
-// and leaves; other waves finish their current grab and leave at their next one.
+// time. No LDS: the ordering kernels co-running on the aux stream keep the CU's whole LDS. Wave w starts
+// with chunk w, then takes LEAF_GRAIN chunks per atomic from a device counter, so waves on CUs that also
+// run ordering workgroups simply take fewer. A chunk of any other shape ends the wave's work: it leaves
+// that chunk and the rest of its range in its slot for k_leaf_ragged and raises the flag (leaf.hpp).
 template <bool SHORT, uint32_t K0, uint32_t V0>
 __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                     const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
-                                                    uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
-                                                    KeyOut KO) {
+                                                    uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ ctr) {
     using Sh = LeafShape<K0, V0>;
     constexpr uint32_t MW = Sh::kw + Sh::vw;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nch = (uint32_t)((n + 63) / 64);
-    while (true) {
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(&ctr[CTR_FIXED], LEAF_GRAIN);
-        b = __builtin_amdgcn_readfirstlane(__shfl(b, 0));
-        if (b >= nch) return;  // all handed out, or another wave stopped the hand-out (>= CTR_ABORT)
-        const uint32_t e = std::min<uint32_t>(b + LEAF_GRAIN, nch);
+    const uint32_t NW = gridDim.x * LEAF_WAVES;
+    const uint32_t w = blockIdx.x * LEAF_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t b = w, e = std::min<uint32_t>(w + 1, nch);
+    while (b < nch) {
         for (uint32_t c = b; c < e; ++c) {
             const uint64_t r = (uint64_t)c * 64 + lane;
             const bool valid = r < n;
@@ -333,12 +319,10 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
             const bool fixed =
                 __all(!valid || (kend - kbeg == K0 && vend - vbeg == V0 &&
                                  ((reinterpret_cast<uintptr_t>(kp) | reinterpret_cast<uintptr_t>(vp)) & 3) == 0));
-            if (!fixed) {
+            if (!fixed) {  // this chunk and the rest of the range go to the ragged stage
                 if (lane == 0) {
-                    const uint32_t old = atomicMax(&ctr[CTR_FIXED], CTR_ABORT);
-                    if (old < CTR_ABORT) ctr[CTR_BP1] = std::min(old, nch) + 1;  // exactly one wave sees it
-                    const uint32_t at = atomicAdd(&ctr[CTR_NLIST], e - c);
-                    for (uint32_t j = 0; j < e - c; ++j) ctr[CTR_LIST + at + j] = c + j;
+                    ctr[CTR_STOP] = 1u;  // read by the ragged stage after this kernel
+                    ctr[CTR_LIST + w] = (c << 5) | (e - c);
                 }
                 return;
             }
@@ -346,11 +330,6 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
             uint32_t m[MW];
             load_words_a4<Sh::kw>(kp, m);
             load_words_a4<Sh::vw>(vp, m + Sh::kw);
-            if (KO.kdst && kend <= KO.kcap) store_words_a4<Sh::kw>(KO.kdst + kbeg, m);
-            if (KO.odst) {
-                KO.odst[r] = kbeg;
-                if (r + 1 == n) KO.odst[n] = kend;
-            }
 #pragma unroll
             for (uint32_t i = 0; i < MW; ++i) m[i] = bswap32(m[i]);
             uint32_t st[8];
@@ -358,6 +337,13 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
             hash_regs_block<SHORT, K0, V0, 0>(m, st);
             store_digest(out + 32 * r, st);
         }
+        // next range. (No look at the stop flag here: an agent-scope load of it beside every grab doubled
+        // this kernel and slowed the co-running sort 3x; a wave simply stops at its own first chunk of
+        // another shape.)
+        uint32_t x = 0;
+        if (lane == 0) x = atomicAdd(&ctr[CTR_FIXED], LEAF_GRAIN);
+        b = NW + __builtin_amdgcn_readfirstlane(__shfl(x, 0));
+        e = std::min<uint32_t>(b + LEAF_GRAIN, nch);
     }
 }
 
@@ -380,29 +366,33 @@ void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uin
     MKV_LAUNCH_CHECK();
 }
 
-size_t leaf_ctr_words(uint64_t n) { return CTR_LIST + ceil_div(n, LEAF_CHUNK) + 16; }
+size_t leaf_ctr_words(uint64_t n) { return CTR_EDGE_LIST + n + 16; }
+
+// Waves of the fixed-shape kernel for n records (the ragged kernel needs the same number).
 
 // Two workgroups per CU (8 waves): room on every CU for the ordering kernels on the aux stream. Three
 // speed the leaf hash alone but stretch the co-running sort past it (build 2.26-2.60 vs 2.18-2.23 ms).
 constexpr int LEAF_WGS = 2;
 
-bool launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                       uint8_t *out, uint32_t *ctr, hipStream_t st, uint8_t *kcopy, uint64_t kcap, uint64_t *ocopy) {
-    MKV_HIP(hipMemsetAsync(ctr, 0, CTR_HEAD * sizeof(uint32_t), st));
-    if (!n) return false;
+uint32_t leaf_fixed_waves(uint64_t n) {
     const uint64_t blocks = std::min<uint64_t>(ceil_div(ceil_div(n, 64), LEAF_WAVES), (uint64_t)leaf_cus() * LEAF_WGS);
-    // the key copy stores at the source's byte offsets: kb must share kcopy's 16-B alignment (k_keycopy_rest)
-    const KeyOut KO{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? kcopy : nullptr, ocopy, kcap};
-    hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3((uint32_t)blocks), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
-                       vb, voff, n, out, ctr, KO);
+    return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(blocks, 1) * LEAF_WAVES, LEAF_MAX_WAVES);
+}
+
+void launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                       uint8_t *out, uint32_t *ctr, hipStream_t st) {
+    const uint32_t nw = leaf_fixed_waves(n);
+    MKV_HIP(hipMemsetAsync(ctr, 0, (CTR_LIST + nw) * sizeof(uint32_t), st));
+    if (!n) return;
+    hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3(nw / LEAF_WAVES), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
+                       vb, voff, n, out, ctr);
     MKV_LAUNCH_CHECK();
-    return KO.kdst != nullptr;
 }
 
 void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                       uint8_t *out, uint32_t *ctr, hipStream_t st) {
-    launch_leaf_fixed(kb, koff, vb, voff, n, out, ctr, st, nullptr, 0, nullptr);
-    launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st);
+    launch_leaf_fixed(kb, koff, vb, voff, n, out, ctr, st);
+    launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st);  // (and the edge records it leaves)
 }
 
 }  // namespace mkv

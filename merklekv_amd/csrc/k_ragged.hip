@@ -26,7 +26,6 @@
 // v_perm_b32 (byte-swap + byte offset from two aligned dwords) and no per-word compare. Positions outside
 // the slot land in trash dwords: a lane's slot is followed by 20 dwords shared with the next lane's
 // leading trash (the key run reaches 15 below, the value / zero runs 15 above); nobody reads them.
-// Lane stride 36 dwords: the ds_read_b128 lane groups hit distinct banks (36 / 4 = 9 is odd).
 #include "common.hpp"
 #include "kernels.hpp"
 #include "leaf.hpp"
@@ -37,11 +36,15 @@ namespace mkv {
 namespace {
 
 constexpr int RG_WAVES = 4;                             // waves per workgroup
-constexpr uint32_t RG_STRIDE = 36;                      // dwords per lane
+// Lane stride 34 dwords: slots 8-B aligned, read back as 8-B words — lanes 0-31 (and 32-63) of a
+// ds_read_b64 then start on 32 distinct even banks of 64 (34 / 2 = 17 is odd), conflict-free — and a
+// 4-wave workgroup takes 34.3 KiB: three of them (12 waves per CU) leave room for a 56.5-KiB sort tile.
+constexpr uint32_t RG_STRIDE = 34;                      // dwords per lane
 constexpr uint32_t RG_FRONT = 16;                       // trash below lane 0's slot
-constexpr uint32_t RG_WAVE_DW = RG_FRONT + 64 * RG_STRIDE;  // lane 63 reaches dword 16 + 63 x 36 + 30
+constexpr uint32_t RG_WAVE_DW = RG_FRONT + 64 * RG_STRIDE;  // lane 63 reaches dword 16 + 63 x 34 + 30
 static_assert(RG_FRONT + 63 * RG_STRIDE + 31 <= RG_WAVE_DW, "lane 63's trash fits the wave region");
-static_assert(RG_STRIDE >= 31 && (RG_STRIDE / 4) % 2 == 1, "trash shared with neighbours; conflict-free reads");
+static_assert(RG_STRIDE >= 31 && RG_STRIDE % 2 == 0 && (RG_STRIDE / 2) % 2 == 1,
+              "trash shared with neighbours; 8-B aligned, conflict-free slots");
 constexpr uint32_t RG_GRAIN = 4;                        // virtual chunks per hand-out atomic
 constexpr uint32_t RG_INV = 0xFFFFFFFFu;
 #ifndef MKV_RAGGED_WGS
@@ -65,25 +68,6 @@ __device__ __forceinline__ void rg_ld17(const uint8_t *base, int64_t a, uint32_t
     }
     d[16] = reinterpret_cast<const uint32_t *>(base + a)[16];
 }
-// The same, every dword outside [lo, hi) read as zero (records within ~128 B of a blob end): each load
-// goes to a clamped in-range address (lo is a readable dword of a non-empty blob; an empty blob is never
-// read), its value is dropped when the dword is outside.
-__device__ __forceinline__ void rg_ld17_checked(const uint8_t *base, int64_t a, int64_t lo, int64_t hi,
-                                                uint32_t d[17]) {
-    if (lo >= hi) {
-#pragma unroll
-        for (int j = 0; j < 17; ++j) d[j] = 0u;
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < 17; ++j) {
-        const int64_t p = a + 4 * j;
-        const bool in = p >= lo && p + 4 <= hi;
-        const uint32_t x = *reinterpret_cast<const uint32_t *>(base + (in ? p : lo));
-        d[j] = in ? x : 0u;
-    }
-}
-
 // Big-endian word of the 4 bytes at byte offset sel (0..3, encoded as a v_perm selector) of (lo, hi).
 __device__ __forceinline__ uint32_t rg_be(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
@@ -133,6 +117,19 @@ __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint64_t k1, uint
     R.live = true;
 }
 
+// A record whose source dwords would reach outside the blobs (within ~128 B of a blob's ends; every record
+// of a blob of empty or tiny keys) goes to k_leaf_edges instead: no bounds checks in this kernel's loads
+// (the checked form cost ~70 VGPRs).
+__device__ __forceinline__ void rg_take_or_leave(RgRec &R, uint64_t k0, uint64_t k1, uint64_t v0, uint64_t v1,
+                                                 uint32_t r, uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi,
+                                                 int64_t vlo, int64_t vhi, uint32_t *ctr) {
+    rg_take(R, k0, k1, v0, v1, r, kmis, vmis, klo, khi, vlo, vhi);
+    if (!R.safe) {
+        ctr[CTR_EDGE_LIST + atomicAdd(&ctr[CTR_EDGES], 1u)] = r;
+        R.live = false;
+    }
+}
+
 // The block's positions of the boundary words (block-relative, may lie outside 0..15).
 struct RgPos {
     int32_t tb1, tb3;
@@ -152,28 +149,34 @@ __device__ __forceinline__ RgPos rg_pos(const RgRec &R) {
 }
 
 // Source dwords of the lane's current (record, block): key run and value run.
-__device__ __forceinline__ void rg_fetch(const RgRec &R, bool all_safe, const uint8_t *kbase, const uint8_t *vbase,
-                                         int64_t klo, int64_t khi, int64_t vlo, int64_t vhi, uint32_t dk[17],
+__device__ __forceinline__ void rg_fetch(const RgRec &R, const uint8_t *kbase, const uint8_t *vbase, uint32_t dk[17],
                                          uint32_t dv[17]) {
     const RgPos P = rg_pos(R);
     const int64_t ak = R.ka + 4 * (int64_t)((int32_t)(16 * R.blk) + P.kend - 16);
     const int64_t av = R.va + 4 * (int64_t)((int32_t)(16 * R.blk) + P.vbeg - (int32_t)R.b1 - 1);
-    if (all_safe) {
-        if (P.key_in) rg_ld17(kbase, ak, dk);
-        if (P.val_in) rg_ld17(vbase, av, dv);
-    } else {
-        if (P.key_in) rg_ld17_checked(kbase, ak, klo, khi, dk);
-        if (P.val_in) rg_ld17_checked(vbase, av, vlo, vhi, dv);
-    }
+    if (P.key_in) rg_ld17(kbase, ak, dk);
+    if (P.val_in) rg_ld17(vbase, av, dv);
 }
 
-// Virtual chunk id -> chunk: the chunks k_leaf_direct listed, then [B, nch).
+// Virtual chunk ids -> chunks: the fixed-shape kernel's slots first (NW x LEAF_GRAIN ids: slot v / G,
+// its (v % G)-th chunk; ids past a slot's count are skipped), then chunks [B, nch).
 struct RgQueue {
     uint32_t qc, qn, qpos;  // current / next chunk, records of qc handed out
     uint32_t pv, pe;        // ids left in the current grab
     uint32_t pnext;         // first id of the next grab (its atomic was issued when this grab opened)
-    uint32_t nv, nlist, B;
+    uint32_t nv, nslot, B;  // ids in all, ids of the slot part, first chunk never handed to k_leaf_direct
 };
+
+// The fixed kernel's hand-off state (leaf.hpp): B, and whether any slot holds chunks.
+__device__ __forceinline__ void rg_handoff(const uint32_t *ctr, uint32_t nch, uint32_t nw, uint32_t *B, uint32_t *nslot) {
+    const uint64_t b = (uint64_t)nw + ctr[CTR_FIXED];
+    *B = b < nch ? (uint32_t)b : nch;
+    *nslot = ctr[CTR_STOP] ? nw * LEAF_GRAIN : 0u;
+}
+__device__ __forceinline__ uint32_t rg_slot_chunk(const uint32_t *ctr, uint32_t v) {  // RG_INV: empty id
+    const uint32_t s = ctr[CTR_LIST + v / LEAF_GRAIN], off = v % LEAF_GRAIN;
+    return off < (s & 31u) ? (s >> 5) + off : RG_INV;
+}
 
 __device__ __forceinline__ uint32_t rg_grab(uint32_t *ctr, uint32_t lane) {
     uint32_t b = 0;
@@ -181,35 +184,38 @@ __device__ __forceinline__ uint32_t rg_grab(uint32_t *ctr, uint32_t lane) {
     return __builtin_amdgcn_readfirstlane(__shfl(b, 0));
 }
 
-__device__ __forceinline__ uint32_t rg_next_chunk(RgQueue &Q, const uint32_t *ctr, uint32_t *ctrw, uint32_t lane) {
-    if (Q.pv >= Q.pe) {
-        if (Q.pnext >= Q.nv) return RG_INV;  // nothing left anywhere: no further atomics
-        Q.pv = Q.pnext;
-        Q.pe = Q.pnext + RG_GRAIN;
-        Q.pnext = rg_grab(ctrw, lane);
+__device__ __forceinline__ uint32_t rg_next_chunk(RgQueue &Q, uint32_t *ctr, uint32_t lane) {
+    while (true) {
+        if (Q.pv >= Q.pe) {
+            if (Q.pnext >= Q.nv) return RG_INV;  // nothing left anywhere: no further atomics
+            Q.pv = Q.pnext;
+            Q.pe = Q.pnext + RG_GRAIN;
+            Q.pnext = rg_grab(ctr, lane);
+        }
+        const uint32_t v = Q.pv++;
+        if (v >= Q.nv) return RG_INV;
+        if (v >= Q.nslot) return Q.B + (v - Q.nslot);
+        const uint32_t c = __builtin_amdgcn_readfirstlane(rg_slot_chunk(ctr, v));
+        if (c != RG_INV) return c;
     }
-    const uint32_t v = Q.pv++;
-    if (v >= Q.nv) return RG_INV;
-    return v < Q.nlist ? __builtin_amdgcn_readfirstlane(ctr[CTR_LIST + v]) : Q.B + (v - Q.nlist);
 }
 
 template <bool SHORT>
-__global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_leaf_ragged(const uint8_t *__restrict__ kb,
+__global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_leaf_ragged(const uint8_t *__restrict__ kb,
                                                               const uint64_t *__restrict__ koff,
                                                               const uint8_t *__restrict__ vb,
                                                               const uint64_t *__restrict__ voff, uint64_t n,
-                                                              uint8_t *__restrict__ out, uint32_t *__restrict__ ctr) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_all[RG_WAVES * RG_WAVE_DW];
+                                                              uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
+                                                              uint32_t nw) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_all[RG_WAVES * RG_WAVE_DW];  // 34.3 KiB
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t *lb = lds_all + wave * RG_WAVE_DW + RG_FRONT + lane * RG_STRIDE;  // this lane's block slot
 
     const uint32_t nch = (uint32_t)((n + 63) / 64);
-    const uint32_t bp1 = ctr[CTR_BP1];
     RgQueue Q;
-    Q.nlist = ctr[CTR_NLIST];
-    Q.B = bp1 ? bp1 - 1 : nch;
-    Q.nv = Q.nlist + (nch - Q.B);
+    rg_handoff(ctr, nch, nw, &Q.B, &Q.nslot);
+    Q.nv = Q.nslot + (nch - Q.B);
     if (Q.nv == 0) return;  // k_leaf_direct hashed every chunk
 
     // dword-aligned blob bases; the blobs' byte ranges rounded out to whole dwords (as offsets from the
@@ -221,9 +227,9 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3
 
     Q.pnext = rg_grab(ctr, lane);
     Q.pv = Q.pe = 0;
-    Q.qc = rg_next_chunk(Q, ctr, ctr, lane);
+    Q.qc = rg_next_chunk(Q, ctr, lane);
     if (Q.qc == RG_INV) return;
-    Q.qn = rg_next_chunk(Q, ctr, ctr, lane);
+    Q.qn = rg_next_chunk(Q, ctr, lane);
     Q.qpos = 0;
 
     // next record of this lane (offsets in flight one step ahead)
@@ -255,26 +261,25 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3
             if (Q.qpos >= 64) {
                 Q.qpos -= 64;
                 Q.qc = Q.qn;
-                Q.qn = Q.qc == RG_INV ? RG_INV : rg_next_chunk(Q, ctr, ctr, lane);
+                Q.qn = Q.qc == RG_INV ? RG_INV : rg_next_chunk(Q, ctr, lane);
             }
         }
     };
 
     RgRec R;
     R.live = false;
-    R.safe = true;
     R.k = R.L = R.b1 = R.b3 = R.nb = R.blk = R.r = 0;
     R.ka = R.va = 0;
     R.ksel = R.vsel = R.hc = R.vhl = R.vtl = R.he = R.term = 0;
     refill(true);
-    if (nok) rg_take(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi);
+    if (nok) rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, ctr);
     nok = false;
     refill(true);
 
     uint32_t dk[17], dv[17];
 #pragma unroll
     for (int j = 0; j < 17; ++j) dk[j] = dv[j] = 0;
-    rg_fetch(R, __all(R.safe || !R.live), kbase, vbase, klo, khi, vlo, vhi, dk, dv);
+    rg_fetch(R, kbase, vbase, dk, dv);
     uint32_t st[8];
     sha_init(st);
 
@@ -315,14 +320,12 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3
                 lb[14] = R.L >> 29;
                 lb[15] = R.L << 3;
             }
-            const uint4 *l4 = reinterpret_cast<const uint4 *>(lb);
+            const uint2 *l2 = reinterpret_cast<const uint2 *>(lb);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint4 x = l4[j];
-                w[4 * j] = x.x;
-                w[4 * j + 1] = x.y;
-                w[4 * j + 2] = x.z;
-                w[4 * j + 3] = x.w;
+            for (int j = 0; j < 8; ++j) {
+                const uint2 x = l2[j];
+                w[2 * j] = x.x;
+                w[2 * j + 1] = x.y;
             }
         }
         // ---- advance: next block, or the next record ----
@@ -332,12 +335,12 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3
         if (R.live && !fin) {
             ++R.blk;
         } else {
-            if (nok) rg_take(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi);
+            if (nok) rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, ctr);
             else R.live = false;
             nok = false;
         }
         refill(!nok);
-        rg_fetch(R, __all(R.safe || !R.live), kbase, vbase, klo, khi, vlo, vhi, dk, dv);  // in flight during the rounds
+        rg_fetch(R, kbase, vbase, dk, dv);  // in flight during the rounds
         // ---- compress ----
         sha_compress<SHORT>(st, w);
         if (fin) store_digest(out + 32 * (uint64_t)rfin, st);
@@ -345,37 +348,48 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(3
     }
 }
 
-// Key-ownership copy of what the fixed-shape kernel left to the ragged stage: the records of chunks
-// [B, nch) (one contiguous byte range) and of the listed chunks, at their source byte offsets in 16-B
-// granules (neighbouring ranges may share a granule: same bytes), plus their offsets. Runs on the aux
-// stream beside the ragged hash (HBM-bound copy next to VALU-bound hashing); does nothing when
-// k_leaf_direct hashed everything.
-__global__ __launch_bounds__(256) void k_keycopy_rest(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
-                                                     uint64_t n, const uint32_t *__restrict__ ctr, KeyOut KO) {
-    const uint32_t bp1 = ctr[CTR_BP1];
-    if (!bp1) return;
-    const uint64_t nch = (n + 63) / 64;
-    const uint64_t B = bp1 - 1, nlist = ctr[CTR_NLIST];
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
-    auto copy_span = [&](uint64_t r0, uint64_t r1, uint64_t t0, uint64_t step) {  // records [r0, r1)
-        if (KO.kdst) {
-            const uint64_t g0 = koff[r0] & ~15ull, g1 = (koff[r1] + 15) & ~15ull;
-            if (g1 <= KO.kcap)
-                for (uint64_t g = g0 + 16 * t0; g < g1; g += 16 * step)
-                    *reinterpret_cast<uint4 *>(KO.kdst + g) = *reinterpret_cast<const uint4 *>(kb + g);
+// The records k_leaf_ragged left (near the blobs' ends): one wave per record, lane l reads message byte l of
+// each block inside the record's fields (no load outside them), shuffles assemble the 16 words, and every
+// lane runs the compression. A handful of records normally; every record only for blobs of empty or tiny
+// keys.
+__device__ __forceinline__ uint32_t edge_byte(const uint8_t *kp, const uint8_t *vp, uint32_t k, uint32_t v, uint32_t L,
+                                              uint32_t nb, uint32_t p) {
+    if (p < 4) return (k >> (24 - 8 * p)) & 0xFFu;
+    if (p < 4 + k) return kp[p - 4];
+    if (p < 8 + k) return (v >> (24 - 8 * (p - 4 - k))) & 0xFFu;
+    if (p < L) return vp[p - 8 - k];
+    if (p == L) return 0x80u;
+    if (p >= 64 * nb - 8) {  // the big-endian u64 bit length 8L in the last 8 bytes
+        const uint32_t i = p - (64 * nb - 8);
+        return (uint32_t)((((uint64_t)L << 3) >> (56 - 8 * i)) & 0xFFu);
+    }
+    return 0u;
+}
+__global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                   const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
+                                                   uint8_t *__restrict__ out, const uint32_t *__restrict__ ctr) {
+    const uint32_t m = ctr[CTR_EDGES];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * (blockDim.x / 64);
+    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < m; i += nw) {
+        const uint32_t r = ctr[CTR_EDGE_LIST + i];
+        const uint64_t k0 = koff[r], v0 = voff[r];
+        const uint32_t k = (uint32_t)(koff[r + 1] - k0), v = (uint32_t)(voff[r + 1] - v0);
+        const uint32_t L = 8 + k + v, nb = (L + 72) >> 6;
+        uint32_t st[8];
+        sha_init(st);
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t byte = edge_byte(kb + k0, vb + v0, k, v, L, nb, 64 * b + lane);
+            const uint32_t mine = (byte << (24 - 8 * (lane & 3)));  // this byte's place in its BE word
+            uint32_t word = mine;
+            word |= __shfl_xor(word, 1);
+            word |= __shfl_xor(word, 2);  // every lane of a 4-lane group now holds the group's word
+            uint32_t w[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = __shfl(word, 4 * j);
+            sha_compress<false>(st, w);
         }
-        if (KO.odst)
-            for (uint64_t r = r0 + t0; r <= r1; r += step) KO.odst[r] = koff[r];  // r1's offset too (= next start)
-    };
-    if (blockIdx.y == 0) {
-        if (B < nch) copy_span(B * 64, n, t, stride);
-    } else {
-        const uint32_t lane = threadIdx.x & 63;
-        const uint64_t wv = t / 64, nw = stride / 64;
-        for (uint64_t i = wv; i < nlist; i += nw) {
-            const uint64_t c = ctr[CTR_LIST + i];
-            copy_span(c * 64, std::min<uint64_t>(c * 64 + 64, n), lane, 64);
-        }
+        if (lane == 0) store_digest(out + 32 * (uint64_t)r, st);
     }
 }
 
@@ -396,16 +410,11 @@ void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *
     if (!n) return;
     const uint64_t grid = std::min<uint64_t>((uint64_t)device_cus() * MKV_RAGGED_WGS, ceil_div(ceil_div(n, 64), RG_WAVES));
     hipLaunchKernelGGL(k_leaf_ragged<false>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
-                       kb, koff, vb, voff, n, out, ctr);
+                       kb, koff, vb, voff, n, out, ctr, leaf_fixed_waves(n));
+    hipLaunchKernelGGL(k_leaf_edges, dim3((uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256)), dim3(256), 0, st, kb, koff,
+                       vb, voff, out, ctr);
     MKV_LAUNCH_CHECK();
 }
 
-void launch_keycopy_rest(const uint8_t *kb, const uint64_t *koff, uint64_t n, const uint32_t *ctr, uint8_t *kdst,
-                         uint64_t kcap, uint64_t *odst, hipStream_t st) {
-    if (!n || (!kdst && !odst)) return;
-    const KeyOut KO{kdst, odst, kcap};
-    hipLaunchKernelGGL(k_keycopy_rest, dim3(1024, 2), dim3(256), 0, st, kb, koff, n, ctr, KO);
-    MKV_LAUNCH_CHECK();
-}
 
 }  // namespace mkv

@@ -20,23 +20,17 @@ void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uin
 // Words of the leaf stage's device counter block (ctr, leaf.hpp): chunk hand-out counters and the list of
 // chunks the fixed-shape kernel leaves to the ragged one.
 size_t leaf_ctr_words(uint64_t n);
-// The fixed-shape kernel (k_leaf_direct): zeroes the counter head, hashes every chunk of the configs'
-// 32/100-B shape until it meets another shape (then it stops and hands the rest over). kcopy/kcap/ocopy:
-// optional fused key-ownership copy (keys at the same byte offsets into kcopy, at most kcap bytes;
-// offsets into ocopy). Returns true when the key copy was fused (kb 16-B aligned); the records left to
-// the ragged stage are then copied by launch_keycopy_rest.
-bool launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st, uint8_t *kcopy, uint64_t kcap,
-                       uint64_t *ocopy);
-// Every chunk launch_leaf_fixed left (k_ragged.hip: any key / value lengths and alignments). Same stream,
-// after launch_leaf_fixed.
+// Waves of the fixed-shape kernel's grid for n records (its hand-off slots; the ragged stage reads them).
+uint32_t leaf_fixed_waves(uint64_t n);
+// The fixed-shape kernel (k_leaf_direct): zeroes the counter head and the hand-off slots, hashes every
+// chunk of the configs' 32/100-B shape and hands every other chunk to the ragged stage.
+void launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
+// Every chunk launch_leaf_fixed left (k_ragged.hip: any key / value lengths and alignments), then the few
+// records near the blobs' ends (k_leaf_edges). Same stream, after launch_leaf_fixed.
 void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                         uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
-// Key-ownership copy of the records the fixed-shape kernel left (no-op when it hashed everything); any
-// stream ordered after launch_leaf_fixed.
-void launch_keycopy_rest(const uint8_t *kb, const uint64_t *koff, uint64_t n, const uint32_t *ctr, uint8_t *kdst,
-                         uint64_t kcap, uint64_t *odst, hipStream_t st);
-// Both kernels, no key copy (staged inputs, update batches).
+// Both (the whole leaf stage).
 void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
 
@@ -78,8 +72,12 @@ constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;
 void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
 // lcp: also measure the shared prefix with key 0 (PH_NLCP_WORD) and key 0's first bytes (PH_K0_WORD),
 // for any window offset.
+// kdst / kcap / odst: optional key-ownership copy (builds from borrowed device blobs): key bytes at their
+// source offsets into kdst when every 16-B granule of them fits kcap (kb must be 16-B aligned), offsets
+// into odst. The caller checks koff[n] + 16 <= kcap to know the keys were copied.
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st, uint64_t off = 0, bool lcp = true);
+                        hipStream_t st, uint64_t off = 0, bool lcp = true, uint8_t *kdst = nullptr, uint64_t kcap = 0,
+                        uint64_t *odst = nullptr);
 // v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;
 // with no pass at all v is filled with them). The result is in (k, v) or, when true is returned, (k2, v2).
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,

@@ -8,25 +8,21 @@ namespace mkv {
 // A chunk is 64 consecutive records (one wave's worth).
 constexpr uint32_t LEAF_CHUNK = 64;
 
-// Counter block (leaf_ctr_words(n) u32, head zeroed before every leaf stage):
-//   [CTR_FIXED]  k_leaf_direct's chunk hand-out counter. The first wave that meets a chunk of another
-//                shape pushes it to CTR_ABORT with one atomicMax, so every later grab ends its wave.
-//   [CTR_BP1]    1 + the first chunk k_leaf_direct never handed out (0: it handed out all of them).
-//   [CTR_NLIST]  chunks k_leaf_direct handed out but left unhashed (the rest of an aborting wave's grab);
-//                their ids follow at [CTR_LIST, CTR_LIST + nlist).
-//   [CTR_RAGGED] k_leaf_ragged's hand-out counter over its virtual chunk space: the listed chunks
-//                first, then chunks [B, nchunks).
-constexpr uint32_t CTR_FIXED = 0, CTR_BP1 = 1, CTR_NLIST = 2, CTR_RAGGED = 3, CTR_HEAD = 4, CTR_LIST = 8;
-constexpr uint32_t CTR_ABORT = 0x40000000u;
-
-// Optional key-ownership copy fused into the fixed-shape kernel (builds from borrowed device inputs: the
-// caller may reuse its buffers, so the tree keeps the key bytes and offsets): keys are stored to kdst at
-// their source byte offsets (at most kcap bytes), offsets to odst. The chunks left to the ragged stage
-// are copied by k_keycopy_rest.
-struct KeyOut {
-    uint8_t *kdst;   // null: no copy
-    uint64_t *odst;  // null: offsets not copied
-    uint64_t kcap;
-};
+// Counter block (leaf_ctr_words(n) u32; head + one slot per fixed-kernel wave zeroed before every stage):
+//   [CTR_FIXED]  k_leaf_direct's hand-out counter: wave w of NW starts with chunk w, later grabs take
+//                LEAF_GRAIN chunks from NW + counter. B = min(NW + final counter, nch) is the first chunk
+//                it never handed out.
+//   [CTR_STOP]   set by any wave that met a chunk of another shape (that wave stops there and leaves the
+//                chunk and the rest of its range in its slot); other waves go on.
+//   [CTR_RAGGED] k_leaf_ragged's hand-out counter over its virtual chunk space: the slots' chunks first
+//                (NW x LEAF_GRAIN ids, empty ones skipped), then chunks [B, nch).
+//   [CTR_EDGES]  records the ragged kernel left to k_leaf_edges (their source dwords would reach outside
+//                the blobs: records within ~128 B of a blob's ends); their ids at [CTR_EDGE_LIST ..).
+//   [CTR_LIST + w] wave w's slot: (first chunk << 5) | count (0: nothing left to the ragged stage).
+// No same-address atomics when every chunk is ragged: the waves' first chunks are static.
+constexpr uint32_t CTR_FIXED = 0, CTR_STOP = 1, CTR_RAGGED = 2, CTR_EDGES = 3, CTR_HEAD = 4, CTR_LIST = 8;
+constexpr uint32_t LEAF_GRAIN = 4;     // k_leaf_direct: chunks per hand-out atomic
+constexpr uint32_t LEAF_MAX_WAVES = 16384;  // slots: fixed-kernel waves (persistent grid, <= 16 per CU)
+constexpr uint32_t CTR_EDGE_LIST = CTR_LIST + LEAF_MAX_WAVES;  // n entries (every record may be an edge one)
 
 }  // namespace mkv

@@ -23,6 +23,7 @@
 using namespace mkv;
 
 static thread_local std::string g_err;
+void mkv::set_last_error(const char *msg) { g_err = msg; }
 
 // Host-side phase trace of the last API call on this thread (mkv_debug_trace): labelled timestamps
 // (µs since the call started) at the call's blocking points, so a slow call names where its host time
@@ -171,6 +172,24 @@ struct mkv_keylist {
     mkv_keylist() { offsets = &zero; }
 };
 
+// A key list over host bytes (the sharded diff's gathered global list, comm.cpp): one pinned block holding
+// offsets[0..n] (offsets[0] == 0) and the key bytes.
+mkv_keylist *mkv::keylist_from_host(const uint8_t *bytes, const uint64_t *offsets, uint64_t n) {
+    auto *l = new mkv_keylist();
+    if (!n) return l;
+    const uint64_t kpos = (8 * (n + 1) + 15) & ~uint64_t(15), nb = offsets[n];
+    auto blk = std::make_shared<PinnedBlock>(kpos + nb + 16);
+    std::memcpy(blk->p, offsets, 8 * (n + 1));
+    if (nb) std::memcpy(blk->p + kpos, bytes, nb);
+    l->blk = blk;
+    l->offsets = reinterpret_cast<const uint64_t *>(blk->p);
+    l->bytes = blk->p + kpos;
+    l->n = n;
+    return l;
+}
+
+uint64_t mkv::tree_global_n(const mkv_tree *t);  // defined after mkv_tree
+
 // Key-set identity: two trees with the same id hold the same sorted key sequence (a clone inherits its
 // source's id; every build or merge draws a fresh one; value-only updates keep it), so a diff between
 // them can skip checking that divergent leaf positions hold equal keys.
@@ -181,7 +200,7 @@ struct mkv_tree {
     int dev = 0;
     hipStream_t st = nullptr;   // main stream: leaf hashing, digest gather, reduction, diff
     hipStream_t st2 = nullptr;  // aux stream: key ownership copy, prefix sort, ties, dedup (overlaps st)
-    hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr, ev_leaf = nullptr;
+    hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr;
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
@@ -259,6 +278,8 @@ struct mkv_tree {
     const uint8_t *in_tomb = nullptr;
     bool counted = false;  // counted in g_live_trees
 };
+
+uint64_t mkv::tree_global_n(const mkv_tree *t) { return t->sharded ? t->gN : t->n; }
 
 // Same key-set id => same sorted keys. The id is a correctness input (the batched dirty path locates a
 // replica's batch in another tree, the walks skip the leaf-key check), so the cheap host-side facts that
@@ -868,8 +889,10 @@ struct SortedSet {
     DevBuf *pk, *pm;
     uint64_t n;
 };
+// kdst / kcap / odst: the tree's own copy of borrowed keys, written by the first histogram pass
+// (launch_prefix_hist).
 SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
-                      bool drop_tomb) {
+                      bool drop_tomb, uint8_t *kdst = nullptr, uint64_t kcap = 0, uint64_t *odst = nullptr) {
     hipStream_t st = t->st2;
     uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
     uint64_t *k2 = ens<uint64_t>(t->s_k2, n_in + 1);
@@ -885,7 +908,7 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     // handle found (sort_win_hint; repeated builds of one key space share it), so the second histogram
     // pass below only runs when the hint is off.
     const uint64_t hint = n_in > 1 ? t->sort_win_hint : 0;
-    launch_prefix_hist(kb, koff, n_in, k1, radix, st, hint, true);
+    launch_prefix_hist(kb, koff, n_in, k1, radix, st, hint, true, kdst, kcap, odst);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
     uint64_t win = hint;    // byte offset of the sort window
@@ -970,8 +993,9 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     return SortedSet{pkbuf, pmbuf, n};
 }
 
-// fused_kcap: the leaf hash already copied the borrowed keys into t->kb (capacity fused_kcap bytes;
-// complete when the key bytes + 16 fit) and the offsets into t->koff (fused_koff); 0 / false: copy here.
+// fused_kcap: the sort's first histogram pass copies the borrowed keys into t->kb (capacity fused_kcap
+// bytes; complete when the key bytes + 16 fit) and the offsets into t->koff (fused_koff); 0 / false: the
+// copy is made here.
 void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
                        bool staged_inputs, uint64_t staged_kbytes, bool defer_gather, uint64_t fused_kcap = 0,
                        bool fused_koff = false) {
@@ -979,7 +1003,8 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
     hipStream_t st = t->st2;
     const uint8_t *dig = t->s_dig.as<uint8_t>();
-    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true);
+    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true, fused_kcap ? t->kb.as<uint8_t>() : nullptr, fused_kcap,
+                                    fused_koff ? t->koff.as<uint64_t>() : nullptr);
     DevBuf *pkbuf = S.pk, *pmbuf = S.pm;
     const uint64_t n = S.n;
     uint32_t *perm;
@@ -994,12 +1019,6 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // a readback there would hold the host until the gather finishes and delay the reduce launches)
     const uint64_t kbytes = staged_inputs ? staged_kbytes : (n_in ? d2h_u64(t, koff + n_in, st) : 0);
     const bool keys_done = !staged_inputs && fused_kcap && kbytes + 16 <= fused_kcap;
-    if (keys_done || (!staged_inputs && fused_koff)) {
-        // the records the fixed-shape kernel left to the ragged one: copied here, beside the ragged hash
-        MKV_HIP(hipStreamWaitEvent(st, t->ev_leaf, 0));
-        launch_keycopy_rest(kb, koff, n_in, t->leaf_ctr.as<uint32_t>(), keys_done ? t->kb.as<uint8_t>() : nullptr,
-                            fused_kcap, fused_koff ? t->koff.as<uint64_t>() : nullptr, st);
-    }
     // The reduction on st needs only the sorted order: join here, before the key copy.
     MKV_HIP(hipEventRecord(t->ev_join, st));
     MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
@@ -1208,7 +1227,6 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_wait, hipEventDisableTiming);
-        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_leaf, hipEventDisableTiming);
         if (e2 != hipSuccess) {
             mkv_tree_destroy(t);
             throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
@@ -1227,7 +1245,6 @@ void mkv_tree_destroy(mkv_tree *t) {
     if (t->ev_in) (void)hipEventDestroy(t->ev_in);
     if (t->ev_join) (void)hipEventDestroy(t->ev_join);
     if (t->ev_wait) (void)hipEventDestroy(t->ev_wait);
-    if (t->ev_leaf) (void)hipEventDestroy(t->ev_leaf);
     if (t->st2) (void)hipStreamDestroy(t->st2);
     for (auto &p : t->evpool) {
         (void)hipEventDestroy(p.a);
@@ -1328,27 +1345,15 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
 }
 
 // The leaf stage of a build: the fixed-shape kernel, then the ragged kernel for whatever it left. Borrowed
-// device inputs (!staged): the fixed-shape kernel also copies the keys (and offsets) into the tree's own
-// buffers when the capacity of an earlier build suffices (*kcap / *ko_fused say what was fused; the
-// records it left are copied by launch_keycopy_rest in sort_dedup_gather; otherwise sort_dedup_gather
-// copies everything).
+// device inputs (!staged): the tree must own a copy of the keys; the sort's first pass writes it when the
+// buffers of an earlier build are large enough (*kcap / *ko_fused, see sort_unique), else
+// sort_dedup_gather copies the keys afterwards.
 static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
                                   const uint64_t *voff, uint64_t n, uint8_t *dig, bool staged, uint64_t *kcap,
                                   bool *ko_fused) {
-    *kcap = 0;
-    *ko_fused = false;
-    uint32_t *ctr = ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n));
-    if (!staged) {
-        *kcap = t->kb.p ? t->kb.cap : 0;
-        *ko_fused = t->koff.p && t->koff.cap >= (n + 1) * 8;
-        if (!launch_leaf_fixed(kb, koff, vb, voff, n, dig, ctr, t->st, t->kb.as<uint8_t>(), *kcap,
-                               *ko_fused ? t->koff.as<uint64_t>() : nullptr))
-            *kcap = 0;
-        MKV_HIP(hipEventRecord(t->ev_leaf, t->st));  // the hand-off state k_keycopy_rest reads
-    } else {
-        launch_leaf_fixed(kb, koff, vb, voff, n, dig, ctr, t->st, nullptr, 0, nullptr);
-    }
-    launch_leaf_ragged(kb, koff, vb, voff, n, dig, ctr, t->st);
+    *kcap = !staged && t->kb.p && (reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? t->kb.cap : 0;
+    *ko_fused = !staged && t->koff.p && t->koff.cap >= (n + 1) * 8;
+    launch_leaf_hash(kb, koff, vb, voff, n, dig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)), t->st);
 }
 
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
@@ -2291,9 +2296,13 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
                          fout, cnt + (L - 1), 0, t->st);
     std::swap(fin, fout);
     const std::vector<size_t> T = jump_targets(L);
+    t->walk_jumps.clear();  // mkv_tree_walk_stats describes this walk (one variant)
+    t->walk_L = (uint32_t)L;
+    t->walk_k = 1;
     for (size_t q = 1; q < T.size(); ++q) {
         const size_t l = T[q - 1], lt = T[q];
         const int k = (int)(l - lt);
+        t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
         launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
                             cnt + lt, std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
         std::swap(fin, fout);

@@ -577,7 +577,8 @@ class MerkleTree:
         return [out[i] for i in range(min(nl.value, 64))]
 
     def walk_stats(self) -> dict:
-        """The last batched top-down walk with this tree as the base (mkv_tree_walk_stats)."""
+        """The last top-down walk with this tree as the base (mkv_tree_walk_stats): a batched walk of
+        diff_keys_many or an unsharded pair walk."""
         out = (C.c_uint64 * 4)()
         check(lib().mkv_tree_walk_stats(self._h, out))
         return {"entries": out[0], "bytes": out[1], "divergent_positions": out[2], "launches": out[3]}
@@ -620,6 +621,57 @@ class MerkleTree:
         has = C.c_int()
         check(lib().mkv_shard_combine_device(self._h, dptr, world, stride, global_n, out, C.byref(has)))
         return bytes(out) if has.value else None
+
+    # ------------------------------------------------------------------ sharded entry points (comm.cpp)
+    # `comm` is a merklekv_amd.comm.Comm; the library runs the collectives itself (RCCL or the host form).
+    def sharded_build(self, comm, keys, values, on_device: bool = False, range_check: bool = True) -> list[int]:
+        """mkv_sharded_build: this rank's key range -> afterwards get_root_hash() is the GLOBAL root on
+        every rank (bit-exact with one tree over all ranks' records). Returns every rank's leaf count."""
+        counts = (C.c_uint64 * comm.world)()
+        if on_device:
+            kb, ko, vb, vo, cnt = (x.data_ptr() if hasattr(x, "data_ptr") else x for x in keys)
+            kblob, vblob = Blob(kb, ko, cnt), Blob(vb, vo, cnt)
+        else:
+            pk, pv = pack_blob(keys), pack_blob(values)
+            kblob, vblob = pk.blob(), pv.blob()
+        self._pending.clear()
+        self._cache.clear()
+        comm.check(lib().mkv_sharded_build(self._h, comm.handle, kblob, vblob, int(bool(on_device)),
+                                           int(bool(range_check)), counts))
+        return list(counts)
+
+    def sharded_root(self, comm) -> bytes | None:
+        """mkv_sharded_root: the global root again after in-range updates of this shard."""
+        self._flush()
+        self._cache.clear()
+        out = (C.c_uint8 * 32)()
+        has = C.c_int()
+        comm.check(lib().mkv_sharded_root(self._h, comm.handle, out, C.byref(has)))
+        return bytes(out) if has.value else None
+
+    @staticmethod
+    def sharded_root_many(trees, comm) -> list:
+        """mkv_sharded_root_many: global roots of k replicas of one key range, ONE all-gather."""
+        trees = list(trees)
+        k = len(trees)
+        for t in trees:
+            t._flush()
+            t._cache.clear()
+        hs = (C.c_void_p * max(k, 1))(*[t._h.value for t in trees])
+        roots = (C.c_uint8 * (32 * max(k, 1)))()
+        has = (C.c_int * max(k, 1))()
+        comm.check(lib().mkv_sharded_root_many(hs, k, comm.handle, roots, has))
+        raw = bytes(roots)
+        return [raw[32 * i:32 * i + 32] if has[i] else None for i in range(k)]
+
+    def sharded_diff(self, other: "MerkleTree", comm) -> KeyList:
+        """mkv_sharded_diff: diff_keys of two sharded trees with one key-range partition, as ONE sorted
+        list on every rank (what sync_once consumes, sync.rs:67-83)."""
+        self._flush()
+        other._flush()
+        kl = C.c_void_p()
+        comm.check(lib().mkv_sharded_diff(self._h, other._h, comm.handle, C.byref(kl)))
+        return KeyList(kl)
 
     # ------------------------------------------------------------------ redistribution (f-3)
     # Tensor arguments are device tensors on this tree's GPU: key / value bytes (uint8), offsets (int64,

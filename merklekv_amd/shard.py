@@ -1,26 +1,25 @@
-"""Sharded (multi-GPU) tree build: one process per GPU, contiguous key ranges ordered by rank.
+"""Sharded (multi-GPU) trees: one process per GPU, contiguous key ranges ordered by rank.
 
-SURVEY.md §8e. Per rank: hash + sort + dedup the local range (mkv_shard_prepare), all-gather the leaf
-counts (8 B/rank) -> global leaf offset o_g and total N, reduce every node whose leaf span lies inside
-[o_g, o_g + n_g) (mkv_shard_reduce), export the seam fringe (<= 2 nodes per level, MKV_FRINGE_BYTES),
-all-gather fringes, and hash the seam nodes on the device (mkv_shard_combine). Every rank ends with the
-same global root, bit-exact with the single-tree root. Collectives go through torch.distributed: on
-ROCm the "nccl" backend is RCCL over xGMI; "gloo" is used by the CPU tests.
-
-Device path (collective device = a GPU): fringes are written straight into a device buffer
-(mkv_shard_fringe_device), all-gathered by RCCL into another device buffer and combined from there
-(mkv_shard_combine_device) — no host staging of the payload. Several trees (replicas) share ONE
-all-gather per step (shard_recombine_many). Host path (gloo / CPU): byte payloads, as the CPU tests use.
+SURVEY.md §8e. The protocol runs INSIDE the C library (csrc/comm.cpp; include/mkv_merkle.h
+mkv_sharded_*): hash + sort + dedup of the rank's range, ONE all-gather of the 8-B leaf counts, the range
+check, in-shard reduction, ONE all-gather of the <= 6 KiB seam fringes, device seam combine. Every rank
+ends with the same global root, bit-exact with the single-tree root. This module is the thin caller: it
+gets the communicator of a torch.distributed group (merklekv_amd.comm.Comm.from_dist: RCCL over xGMI
+when the collective device is a GPU and the backend "nccl", else the host form over gloo) and calls
+MerkleTree.sharded_build / sharded_root_many / sharded_diff. Collective timings are read back from the
+communicator into `coll_stats`.
 
 Range check: the seam protocol is exact only if rank r holds a contiguous key range below rank r+1's
-(the reference keeps one leaf per key, last write wins). `sharded_root(..., validate=True)` all-gathers
-each shard's first and last sorted key and raises unless last(r) < first(next non-empty rank).
+(the reference keeps one leaf per key, last write wins). `validate=True` makes every rank check that
+last(r) < first(next non-empty rank) and raise otherwise.
+
+Trees without the C entry points (tests/shard_model.ModelShardTree: a pure-Python model of the shard_*
+steps) run the same protocol here step by step over torch.distributed, so the CPU tests exercise the
+orchestration and the seam math without a GPU.
 
 Redistribution: `redistribute` moves records that sit on the ranks in no key order into
 key-range shards with one all-to-all (route kernels in csrc/k_route.hip); `sharded_root_unpartitioned`
 chains it with the sharded build.
-
-`tree` is anything with the shard_* (and route_*) methods of merklekv_amd.MerkleTree.
 """
 from __future__ import annotations
 
@@ -121,9 +120,39 @@ def check_ranges(tree, counts: list[int], dist, device, group=None) -> None:
         prev_last, prev_rank = last, r
 
 
+def _native(*trees) -> bool:
+    return all(hasattr(t, "sharded_build") for t in trees)
+
+
+def _comm(dist, device, group):
+    from .comm import Comm
+    return Comm.from_dist(dist, device, group)
+
+
+def _absorb(comm) -> None:
+    """Move the communicator's collective timings into coll_stats."""
+    for name, (secs, calls, nbytes) in comm.stats(reset=True).items():
+        if calls:
+            s = coll_stats.setdefault(name, [0.0, 0, 0])
+            s[0] += secs
+            s[1] += calls
+            s[2] += int(nbytes)
+
+
 def sharded_root(tree, keys, values, dist, device="cpu", group=None, on_device: bool = False,
                  validate: bool = True):
     """Build this rank's shard of the global tree and return (global root or None, counts)."""
+    if _native(tree):
+        comm = _comm(dist, device, group)
+        try:
+            counts = tree.sharded_build(comm, keys, values, on_device=on_device, range_check=validate)
+        except Exception as e:
+            _absorb(comm)
+            if "key ranges overlap" in str(e):
+                raise ValueError(str(e)) from e
+            raise
+        _absorb(comm)
+        return tree.get_root_hash(), counts
     rank = dist.get_rank(group)
     n_local = tree.shard_prepare(keys, values, on_device=on_device)
     counts = shard_counts(dist, n_local, device, group)
@@ -142,6 +171,11 @@ def shard_recombine_many(trees, dist, total: int, device="cpu", group=None) -> l
     k = len(trees)
     if k == 0:
         return []
+    if _native(*trees):
+        comm = _comm(dist, device, group)
+        roots = type(trees[0]).sharded_root_many(trees, comm)
+        _absorb(comm)
+        return roots
     world = dist.get_world_size(group)
     if _is_gpu(device) and all(hasattr(t, "shard_fringe_device") for t in trees):
         import torch
@@ -190,6 +224,11 @@ def sharded_diff_gather(a, b, dist, device="cpu", group=None):
     import time
 
     import torch
+    if _native(a, b):
+        comm = _comm(dist, device, group)
+        kl = a.sharded_diff(b, comm)
+        _absorb(comm)
+        return kl.raw.copy(), kl.offs.copy()
     world = dist.get_world_size(group)
     raw, offs = a.diff_keys_packed(b)
     n, nb = len(offs) - 1, int(offs[-1])

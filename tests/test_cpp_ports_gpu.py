@@ -31,3 +31,15 @@ def test_cpp_boundary_const_call_sites():
     r = subprocess.run([b], capture_output=True, text=True, timeout=300)
     print(r.stdout[-4000:])
     assert r.returncode == 0 and "boundary: ok" in r.stdout, r.stdout[-4000:] + r.stderr[-2000:]
+
+
+def test_cpp_sharded_comm():
+    """mkv_comm_* / mkv_sharded_* from C++: RCCL at world 1 and the host form at world 3 (threads) vs an
+    OpenSSL restatement of rebuild() / diff_keys() (tests/cpp/test_sharded.cpp)."""
+    b = os.path.join(ROOT, "tests", "cpp", "test_sharded")
+    if not os.path.exists(b):
+        import __graft_entry__
+        __graft_entry__.build_cpp_tests()
+    r = subprocess.run([b], capture_output=True, text=True, timeout=300)
+    print(r.stdout[-4000:])
+    assert r.returncode == 0 and "sharded: ok" in r.stdout, r.stdout[-4000:] + r.stderr[-2000:]
