@@ -40,9 +40,9 @@ sys.path.insert(0, ROOT)
 SEED = 0x4D65726B6C654B56
 KLEN, VLEN = 32, 100
 LEAF_BYTES = 8 + KLEN + VLEN + 32   # record model: 140-B record (k, v, 8 B of offsets) read + 32-B digest written
-# what the timed leaf kernel moves per leaf in a build from borrowed device buffers: the record model plus
-# the fused key-ownership copy (32-B key + 8-B offset written into the tree's own key store)
-LEAF_BYTES_BUILD = LEAF_BYTES + KLEN + 8
+# (SURVEY §8(d)). Round 4: the key-ownership copy of a build from borrowed device buffers moved out of the
+# leaf kernel into the sort's first histogram pass (which reads every key anyway), so the timed leaf kernel
+# moves exactly the record model.
 HBM_PEAK_GBS = 8000.0                # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 SHA_OPS_PER_LEAF = 3 * 1450          # model: 3 compressions x ~1450 VALU lane-ops
@@ -169,17 +169,15 @@ def random_values(torch, m, dev, gen):
 
 # ============================================================================================ build
 def leaf_roofline(n, leaf_avg_ms, launches):
-    """roofline of the dominant kernel (the leaf hash, k_leaf_direct). achieved = 212 B/leaf x n / live launch time
-    (172 B record model + the fused 40-B key-ownership copy the timed kernel also does; the 172-B figure is
-    reported beside it) (HIP
-    events on the tree's stream, sort co-running); traffic and the VALU fractions come from the PMC file
-    of the same tree (profiles/pmc_leaf_hash.json, written by scripts/prof_summary.py)."""
-    achieved = LEAF_BYTES_BUILD * n / (leaf_avg_ms * 1e-3) / 1e9
+    """roofline of the dominant kernel (the leaf hash, k_leaf_direct). achieved = §8(d)'s 172 B/leaf x n /
+    live launch time (HIP events on the tree's stream, sort co-running); `frac_record_model` names the same
+    figure. traffic and the VALU fractions come from the PMC file of the same tree
+    (profiles/pmc_leaf_hash.json, written by scripts/prof_summary.py)."""
+    achieved = LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_leaf_direct",
-           "bytes_per_leaf": LEAF_BYTES_BUILD, "avg_launch_ms": leaf_avg_ms, "launches": launches,
-           "achieved_record_model": LEAF_BYTES * n / (leaf_avg_ms * 1e-3) / 1e9,
-           "bytes_per_leaf_record_model": LEAF_BYTES,
+           "bytes_per_leaf": LEAF_BYTES, "avg_launch_ms": leaf_avg_ms, "launches": launches,
+           "frac_record_model": achieved / HBM_PEAK_GBS,
            "gb_per_s_hashed": (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9,
            "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): the HBM frac ceiling is ~0.39; "
                    "avg_launch_ms is measured live while the ordering kernels co-run on the aux stream"}

@@ -3,8 +3,9 @@
 // The reference builds a BTreeSet over the union of both leaf maps and looks every key up in both
 // HashMaps. Both trees here already hold their leaves sorted by key (R3), so the same set is a
 // merge-join of two sorted (key, digest) arrays:
-//   pass 0  partition the merged sequence into 512-output wave tiles (exact merge-path searches at every
-//           64th tile, interpolation + galloping search in between);
+//   pass 0  partition the merged sequence into 512-output wave tiles, one launch: a wave per 64 tiles
+//           finds the group's two boundary splits by a cooperative 33-ary merge-path search, then each
+//           lane the split of one tile between them (interpolation + galloping search);
 //   pass 1  one wave per tile, no LDS: near-identical tiles (every A key paired in lockstep with a B key
 //           of the same prefix) compare their digest pairs with coalesced loads and wave ballots; any
 //           other tile runs the general per-lane 8-output merge: an A key is divergent unless the B
@@ -12,7 +13,8 @@
 //           equal. Lane results are packed to one u32 (split, from-A bits, divergent bits) plus a
 //           per-tile count;
 //   scan    exclusive scan of tile counts;
-//   pass 2  wave-scan compaction writes (side, index) refs of divergent keys in merged = sorted order.
+//   pass 2  wave-scan compaction writes (side, index) refs of divergent keys in merged = sorted order;
+//           the same launch verifies the aligned path's deferred key checks.
 // Ties on the 8-byte prefix fall back to a full-key compare in HBM (key_cmp), so any key set is exact.
 #include <algorithm>
 
@@ -92,79 +94,101 @@ __device__ __forceinline__ int cmp_merge(const DiffSide &A, uint64_t i, uint64_t
     return cmp_ab(A, i, pa, B, j, pb);
 }
 
-// Merge-path split of diagonal d over the full arrays: number of A elements among the first d outputs
-// (A before B on equal keys).
-__device__ uint64_t split_global(const DiffSide &A, const DiffSide &B, uint64_t d) {
-    uint64_t lo = d > B.n ? d - B.n : 0, hi = d < A.n ? d : A.n;
-    while (lo < hi) {
-        uint64_t mid = (lo + hi) >> 1;
-        uint64_t jb = d - 1 - mid;
-        if (cmp_merge(A, mid, A.pfx[mid], B, jb, B.pfx[jb]) <= 0) lo = mid + 1;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// Two-level partition. Coarse: exact global searches at every PART_STRIDE-th tile (and the last).
+// Partition, one wave per group of PART_STRIDE tiles (one launch). The group's two boundary splits
+// (tiles t0 and t1 = min(t0 + PART_STRIDE, ntiles)) by a cooperative search: lanes 0-31 search t0's
+// diagonal, lanes 32-63 t1's, each half probing 32 points per step (33-ary: 100M keys in ~6 dependent
+// round trips instead of ~27 for a binary search). Then lane l computes tile t0 + l's split inside that
+// bracket: the split is monotone in the diagonal, so it lies between the two boundary splits; start at
+// their linear interpolation (exact for near-identical replicas up to the few inserts/deletes in
+// between), gallop outwards, then binary search the bracket — probes within a few cache lines that
+// neighbouring tiles share.
 constexpr uint64_t PART_STRIDE = 64;
 
-__global__ void k_diff_partition(DiffSide A, DiffSide B, uint64_t ntiles, uint64_t *__restrict__ split) {
-    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t nc = (ntiles + PART_STRIDE - 1) / PART_STRIDE;
-    if (u > nc) return;
-    const uint64_t t = u < nc ? u * PART_STRIDE : ntiles;
-    const uint64_t M = A.n + B.n;
-    uint64_t d = t * WTILE;
-    if (d > M) d = M;
-    split[t] = split_global(A, B, d);
+// pred(a): A[a] precedes B[d-1-a] in the merge (A first on equal keys), i.e. the split of diagonal d is
+// > a. Valid for max(0, d - B.n) <= a < min(d, A.n).
+__device__ __forceinline__ bool part_pred(const DiffSide &A, const DiffSide &B, uint64_t d, uint64_t a) {
+    const uint64_t jb = d - 1 - a;
+    return cmp_merge(A, a, A.pfx[a], B, jb, B.pfx[jb]) <= 0;
 }
 
-// Fine: every other tile's split lies between its two coarse neighbours' splits (the split is monotone
-// in the diagonal, and so is the B count). Start at the linear interpolation of the two (exact for
-// near-identical replicas up to the few inserts/deletes in between) and gallop outwards, then binary
-// search the bracket; the probes stay within a few cache lines that neighbouring tiles share.
-__global__ void k_diff_partition_fine(DiffSide A, DiffSide B, uint64_t ntiles, uint64_t *__restrict__ split) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles || t % PART_STRIDE == 0) return;
+__global__ __launch_bounds__(256) void k_diff_partition(DiffSide A, DiffSide B, uint64_t ntiles,
+                                                        uint64_t *__restrict__ split, uint32_t *__restrict__ defer_count,
+                                                        uint64_t *__restrict__ fail) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g == 0 && lane == 0) {  // this diff's deferred-check counter and fail word
+        *defer_count = 0;
+        fail[0] = 0;
+    }
+    const uint64_t ngroups = (ntiles + PART_STRIDE - 1) / PART_STRIDE;
+    if (g >= ngroups) return;  // wave-uniform
     const uint64_t M = A.n + B.n;
-    const uint64_t t0 = t - t % PART_STRIDE, t1 = t0 + PART_STRIDE < ntiles ? t0 + PART_STRIDE : ntiles;
+    const uint64_t t0 = g * PART_STRIDE, t1 = t0 + PART_STRIDE < ntiles ? t0 + PART_STRIDE : ntiles;
+    const uint32_t half = lane >> 5, k = lane & 31;
+    // ---- boundary splits: half h searches diagonal dh; answer in [lo, hi] ----
+    const uint64_t dh = half ? (t1 * WTILE < M ? t1 * WTILE : M) : t0 * WTILE;
+    uint64_t lo = dh > B.n ? dh - B.n : 0, hi = dh < A.n ? dh : A.n;
+    while (__any(lo < hi)) {
+        const uint64_t n = hi - lo;
+        const bool act = lo < hi;
+        uint64_t p = 0;
+        bool pv = false;
+        if (act) {
+            p = n <= 32 ? lo + k : lo + ((uint64_t)(k + 1) * n) / 33;
+            pv = (n > 32 || k < n) && part_pred(A, B, dh, p);
+        }
+        const uint32_t m = (uint32_t)(__ballot(pv) >> (32 * half));
+        const uint32_t c = (uint32_t)__popc(m);  // preds are monotone: c leading trues
+        if (act) {
+            if (n <= 32) {
+                lo = hi = lo + c;
+            } else {
+                const uint64_t pc1 = c ? lo + ((uint64_t)c * n) / 33 : 0;                       // p_{c-1}
+                const uint64_t pc = c < 32 ? lo + ((uint64_t)(c + 1) * n) / 33 : hi;            // p_c
+                if (c) lo = pc1 + 1;
+                hi = pc;
+            }
+        }
+    }
+    const uint64_t s0 = __shfl(lo, 0), s1 = __shfl(lo, 32);
+    if (lane == 0) split[t0] = s0;
+    if (lane == 32 && t1 == ntiles) split[ntiles] = s1;
+    // ---- the group's other tiles ----
+    const uint64_t t = t0 + lane;
+    if (lane == 0 || t >= t1) return;
     const uint64_t d = t * WTILE, d0 = t0 * WTILE, d1 = t1 * WTILE < M ? t1 * WTILE : M;
-    const uint64_t a0 = split[t0], a1 = split[t1];
-    uint64_t lo = a1 > d1 - d ? a1 - (d1 - d) : 0, hi = a0 + (d - d0);
+    const uint64_t a0 = s0, a1 = s1;
+    lo = a1 > d1 - d ? a1 - (d1 - d) : 0;
+    hi = a0 + (d - d0);
     if (lo < a0) lo = a0;
     if (hi > a1) hi = a1;
     if (d > B.n && lo < d - B.n) lo = d - B.n;
     if (hi > A.n) hi = A.n;
     if (hi > d) hi = d;
-    // pred(a): A[a] precedes B[d-1-a] in the merge, i.e. the split is > a (valid for lo <= a < hi)
-    auto pred = [&](uint64_t a) {
-        const uint64_t jb = d - 1 - a;
-        return cmp_merge(A, a, A.pfx[a], B, jb, B.pfx[jb]) <= 0;
-    };
-    uint64_t g = a0 + (uint64_t)((double)(a1 - a0) * (double)(d - d0) / (double)(d1 - d0) + 0.5);
-    if (g < lo) g = lo;
-    if (g > hi) g = hi;
+    uint64_t gs = a0 + (uint64_t)((double)(a1 - a0) * (double)(d - d0) / (double)(d1 - d0) + 0.5);
+    if (gs < lo) gs = lo;
+    if (gs > hi) gs = hi;
     uint64_t L = lo, H = hi;  // answer in [L, H]
-    if (g < hi && pred(g)) {
-        L = g + 1;
+    if (gs < hi && part_pred(A, B, d, gs)) {
+        L = gs + 1;
         for (uint64_t step = 1;; step <<= 1) {
-            const uint64_t p = g + step;
-            if (p >= hi) break;
-            if (!pred(p)) { H = p; break; }
-            L = p + 1;
+            const uint64_t q = gs + step;
+            if (q >= hi) break;
+            if (!part_pred(A, B, d, q)) { H = q; break; }
+            L = q + 1;
         }
     } else {
-        H = g;
+        H = gs;
         for (uint64_t step = 1;; step <<= 1) {
-            if (g < lo + step) break;
-            const uint64_t p = g - step;
-            if (pred(p)) { L = p + 1; break; }
-            H = p;
+            if (gs < lo + step) break;
+            const uint64_t q = gs - step;
+            if (part_pred(A, B, d, q)) { L = q + 1; break; }
+            H = q;
         }
     }
     while (L < H) {
         const uint64_t mid = (L + H) >> 1;
-        if (pred(mid)) L = mid + 1;
+        if (part_pred(A, B, d, mid)) L = mid + 1;
         else H = mid;
     }
     split[t] = L;
@@ -359,7 +383,7 @@ __device__ __forceinline__ uint4 shfl_u4(uint4 v, int src) {
 // divergent count (wave-uniform). lp: the wave's LDS prefix slice (WTILE + 2 entries).
 // Deferred key checks of the aligned path (round 3): a pair with equal 8-byte prefixes and different
 // digests is taken as the same key with a changed value, and its (A index, B index) goes to this list;
-// k_diff_verify then compares all their keys at once, off pass 1's critical path (each inline check is
+// pass 2's verify blocks then compare all their keys at once, off pass 1's critical path (each inline check is
 // three dependent random reads per side that hold the wave). A failed check or a full list makes the
 // caller run the diff again without deferral (exact for any key sets).
 struct DeferList {
@@ -536,7 +560,7 @@ __device__ __forceinline__ uint32_t diff_tile(const DiffSide &A, const DiffSide 
 template <bool DEFER>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_diff_pass1(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, uint32_t *__restrict__ packed,
-                                                    uint32_t *__restrict__ tilecnt, DeferList V) {
+                                                    uint64_t *__restrict__ tilecnt, DeferList V) {
     __shared__ uint64_t lds[4 * (WTILE + 2)];  // per-wave prefix slices for the general merge
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= nt) return;  // wave-uniform
@@ -549,9 +573,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 }
 
 // Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
+// The deferred key checks ride in the same launch (blocks from nb2 on): fail[0] = 1 if any pair holds
+// different keys or the list overflowed (the caller then reruns without deferral).
 __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, const uint32_t *__restrict__ packed,
-                                                    const uint64_t *__restrict__ tileoff, uint64_t *__restrict__ refs) {
+                                                    const uint64_t *__restrict__ tileoff, uint64_t *__restrict__ refs,
+                                                    uint32_t nb2, DeferList V, uint64_t *__restrict__ fail) {
+    if (blockIdx.x >= nb2) {
+        const uint32_t cnt = *V.count;
+        const uint64_t vb = blockIdx.x - nb2, nvb = gridDim.x - nb2;
+        if (cnt > V.cap) {
+            if (vb == 0 && threadIdx.x == 0) fail[0] = 1;
+            return;
+        }
+        for (uint64_t k = vb * blockDim.x + threadIdx.x; k < cnt; k += nvb * blockDim.x) {
+            const uint64_t e = V.ent[k], i = e >> 32, j = e & 0xFFFFFFFFull;
+            if (cmp_ab(A, i, A.pfx[i], B, j, B.pfx[j]) != 0) fail[0] = 1;
+        }
+        return;
+    }
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= nt) return;
     const uint32_t lane = threadIdx.x & 63;
@@ -568,27 +608,6 @@ __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, cons
         const uint64_t ref = fa ? i : (j | (1ull << 63));
         if (fa) ++i; else ++j;
         if ((div >> s) & 1u) refs[off++] = ref;
-    }
-}
-
-// The deferred key checks: fail[0] = 1 if any pair holds different keys or the list overflowed.
-__global__ __launch_bounds__(256) void k_diff_verify(DiffSide A, DiffSide B, DeferList V, uint64_t *__restrict__ fail) {
-    const uint32_t cnt = *V.count;
-    if (cnt > V.cap) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) fail[0] = 1;
-        return;
-    }
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t e = V.ent[k], i = e >> 32, j = e & 0xFFFFFFFFull;
-        if (cmp_ab(A, i, A.pfx[i], B, j, B.pfx[j]) != 0) fail[0] = 1;
-    }
-}
-
-// Zeroes the deferred-check counter and the fail word of this diff (one launch before pass 1).
-__global__ void k_diff_defer_reset(uint32_t *__restrict__ count, uint64_t *__restrict__ fail) {
-    if (threadIdx.x == 0) {
-        *count = 0;
-        fail[0] = 0;
     }
 }
 
@@ -878,11 +897,6 @@ __global__ __launch_bounds__(256) void k_tail_copy_dev(const uint64_t *__restric
     if (t < bytes - nvk * 16) dkeys[nvk * 16 + t] = kout[nvk * 16 + t];
 }
 
-__global__ void k_widen_u32(const uint32_t *__restrict__ c, uint64_t *__restrict__ o, uint64_t n) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) o[i] = c[i];
-}
-
 inline dim3 grid1d(uint64_t n, uint32_t bs = 256) { return dim3((uint32_t)ceil_div(n ? n : 1, bs)); }
 
 }  // namespace
@@ -894,7 +908,7 @@ size_t diff_scratch_bytes(uint64_t M) {
     size_t b = 0;
     b += (nt + 2) * sizeof(uint64_t);             // split
     b += nt * 64 * sizeof(uint32_t);              // packed
-    b += (nt + 2) * sizeof(uint32_t);             // tile counts
+    b += (nt + 2) * sizeof(uint64_t);             // tile counts
     b += (nt + 2) * sizeof(uint64_t);             // tile offsets
     b += scan_scratch_bytes(nt) + 1024;
     b += defer_cap(M) * sizeof(uint64_t) + 512;                     // deferred key checks + their count
@@ -917,26 +931,25 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     };
     uint64_t *split = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     uint32_t *packed = reinterpret_cast<uint32_t *>(carve(nt * 64 * sizeof(uint32_t)));
-    uint32_t *tilecnt = reinterpret_cast<uint32_t *>(carve((nt + 2) * sizeof(uint32_t)));
+    uint64_t *tilecnt = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     uint64_t *tileoff = reinterpret_cast<uint64_t *>(carve((nt + 2) * sizeof(uint64_t)));
     void *sc = carve(scan_scratch_bytes(nt));
     DeferList V{reinterpret_cast<uint64_t *>(carve(defer_cap(M) * sizeof(uint64_t))),
                 reinterpret_cast<uint32_t *>(carve(256)), (uint32_t)defer_cap(M)};
-    hipLaunchKernelGGL(k_diff_defer_reset, dim3(1), dim3(64), 0, st, V.count, count + 1);
-    const dim3 wg((uint32_t)ceil_div(nt, 4));
-    hipLaunchKernelGGL(k_diff_partition, grid1d(ceil_div(nt, PART_STRIDE) + 1), dim3(256), 0, st, A, B, nt, split);
-    hipLaunchKernelGGL(k_diff_partition_fine, grid1d(nt), dim3(256), 0, st, A, B, nt, split);
+    const uint32_t wg = (uint32_t)ceil_div(nt, 4);
+    // partition + this diff's deferred-check reset (one launch)
+    hipLaunchKernelGGL(k_diff_partition, dim3((uint32_t)ceil_div(ceil_div(nt, PART_STRIDE), 4)), dim3(256), 0, st, A, B,
+                       nt, split, V.count, count + 1);
     if (defer)
-        hipLaunchKernelGGL(k_diff_pass1<true>, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt, V);
+        hipLaunchKernelGGL(k_diff_pass1<true>, dim3(wg), dim3(256), 0, st, A, B, split, nt, packed, tilecnt, V);
     else
-        hipLaunchKernelGGL(k_diff_pass1<false>, wg, dim3(256), 0, st, A, B, split, nt, packed, tilecnt, V);
+        hipLaunchKernelGGL(k_diff_pass1<false>, dim3(wg), dim3(256), 0, st, A, B, split, nt, packed, tilecnt, V);
     MKV_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_widen_u32, grid1d(nt), dim3(256), 0, st, tilecnt, tileoff, nt);
-    exclusive_scan_u64(tileoff, tileoff, nt, count, sc, st);
-    hipLaunchKernelGGL(k_diff_pass2, wg, dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs);
-    if (defer)
-        hipLaunchKernelGGL(k_diff_verify, dim3((uint32_t)std::min<uint64_t>(ceil_div(defer_cap(M), 256), 1024)),
-                           dim3(256), 0, st, A, B, V, count + 1);
+    exclusive_scan_u64(tilecnt, tileoff, nt, count, sc, st);
+    // pass 2 + (defer) the key checks in the same launch
+    const uint32_t nvb = defer ? (uint32_t)std::min<uint64_t>(ceil_div(defer_cap(M), 256), 1024) : 0;
+    hipLaunchKernelGGL(k_diff_pass2, dim3(wg + nvb), dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs, wg, V,
+                       count + 1);
     MKV_LAUNCH_CHECK();
 }
 

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
     }
 }
 
-// ---- top of the tree (round 3): every level from a <= 64-tile level to the root in ONE launch ----
+// ---- top of the tree: every level from a <= RD_TOP_TILES-tile level to the root in ONE launch ----
 // Phase 1: each workgroup fuses up to 10 levels of its 512-parent tile in LDS (the tile's
 // subtree collapses to one node after 10 levels). Phase 2: the last workgroup to finish (agent-scope
 // arrival counter; it resets the counter for the next launch) reads the <= ntiles + 2 nodes the tiles
@@ -183,14 +183,9 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
         __threadfence();
         __syncthreads();
     }
-    // level nf (owned nodes [a, a + c), c <= RD_TILE) into LDS as BE words, read coherently
-    {
-        const uint64_t cnt = p.c[nf];
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(nf == 0 ? p.in : p.out[nf - 1]);
-        for (uint32_t w = threadIdx.x; w < 8 * cnt; w += RD_TILE)
-            buf[nf & 1][w] = bswap32(__hip_atomic_load(src + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __syncthreads();
+    // levels nf+1 .. nl: parents [a[k], a[k] + c[k]) (<= RD_TILE: level nf holds <= ntiles <= RD_TOP_TILES
+    // nodes); the first of them reads its children (level nf, written by every tile) coherently from HBM,
+    // the others from LDS
     for (int k = nf + 1; k <= p.nl; ++k) {
         const uint32_t i = threadIdx.x;
         const uint64_t j = p.a[k] + i;  // owned parents [a[k], a[k] + c[k]), children owned at level k-1
@@ -198,11 +193,20 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
             uint32_t l[8], r[8], o[8];
             const uint64_t c0 = 2 * j;
             const bool pair = c0 + 1 < p.S[k - 1];
-            const uint32_t *src = buf[(k - 1) & 1] + 8 * (c0 - p.a[k - 1]);
+            if (k == nf + 1) {
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(p.out[nf - 1]) + 8 * (c0 - p.a[nf]);
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                l[q] = src[q];
-                r[q] = pair ? src[8 + q] : 0u;
+                for (int q = 0; q < 8; ++q) {
+                    l[q] = bswap32(__hip_atomic_load(src + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    r[q] = pair ? bswap32(__hip_atomic_load(src + 8 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : 0u;
+                }
+            } else {
+                const uint32_t *src = buf[(k - 1) & 1] + 8 * (c0 - p.a[k - 1]);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    l[q] = src[q];
+                    r[q] = pair ? src[8 + q] : 0u;
+                }
             }
             if (pair) {
                 sha_node<SHORT>(l, r, o);

@@ -60,12 +60,17 @@ constexpr uint64_t PH_LCP_CAP = 1u << 16;
 // kdst / kcap / odst (builds from borrowed device blobs): the tree's own copy of the keys — key bytes at
 // their source offsets in 16-B granules (all or none: only when the granules fit kcap; kb 16-B aligned)
 // and the offsets. This pass already reads every key's cache lines, so the copy costs only its writes.
+// host_out (device view of mapped pinned memory, optional): the last workgroup to finish (arrival counter
+// PH_ARRIVE_WORD) copies the histograms and control words there, so the host reads them without a copy
+// launch of its own. zero2 (optional): two counter words zeroed for the tie marker that follows.
 __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__restrict__ kb,
                                                            const uint64_t *__restrict__ koff, uint64_t n,
                                                            uint64_t off, bool lcp, uint64_t *__restrict__ pfx,
                                                            uint32_t *__restrict__ counts, uint8_t *__restrict__ kdst,
-                                                           uint64_t kcap, uint64_t *__restrict__ odst) {
+                                                           uint64_t kcap, uint64_t *__restrict__ odst,
+                                                           uint32_t *__restrict__ host_out, uint32_t *__restrict__ zero2) {
     sort_prio();
+    if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
     if (kdst) {
         const uint64_t g0 = koff[0] & ~15ull, g1 = (koff[n] + 15) & ~15ull;
         if (g1 <= kcap)
@@ -138,10 +143,23 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
         if (lmax) atomicMax(&counts[PH_MAXLEN_WORD], lmax);
         if (lcp) atomicMax(&counts[PH_NLCP_WORD], ~lmin);  // the words start at 0: max of ~x = min of x
         if (lcp && blockIdx.x == 0) {
-            counts[PH_K0_WORD] = (uint32_t)(k0w >> 32);
-            counts[PH_K0_WORD + 1] = (uint32_t)k0w;
+            __hip_atomic_store(&counts[PH_K0_WORD], (uint32_t)(k0w >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&counts[PH_K0_WORD + 1], (uint32_t)k0w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    if (!host_out) return;
+    // ---- the last workgroup hands every word to the host ----
+    __shared__ uint32_t last;
+    __threadfence();  // this thread's histogram atomics performed device-wide before the arrival
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(&counts[PH_ARRIVE_WORD], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev + 1 == gridDim.x;
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int i = threadIdx.x; i < 8 * 256 + 64; i += RS_THREADS)
+        host_out[i] = __hip_atomic_load(&counts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sorted set prefixes from sort windows at byte offset win > 0 (bytes [0, win) are shared by every key;
@@ -153,7 +171,10 @@ __global__ void k_pfx_from_window(uint64_t *__restrict__ pk, uint64_t n, uint64_
 }
 
 // ---- onesweep LSD radix pass ----
-// Look-back word per (tile, digit): [31:30] status (0 not ready, 1 aggregate, 2 inclusive), [29:0] count.
+// Look-back word per (tile, digit), 64 bits: [63:32] epoch of the pass that wrote it, [31:30] status (1
+// aggregate, 2 inclusive), [29:0] count. A word of another epoch reads as "not ready", so a buffer that
+// only ever holds look-back words needs no zeroing between passes or sorts (the build's sort keeps one
+// per tree, zeroed once when allocated; every pass draws a fresh epoch).
 constexpr uint32_t LB_AGG = 1u << 30, LB_INC = 2u << 30, LB_VAL = (1u << 30) - 1u;
 constexpr uint32_t LB_SPIN_LIMIT = 1u << 26;  // bounded spin: sets an error flag instead of hanging
 
@@ -193,7 +214,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
                                                        const uint32_t *__restrict__ vin,
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout,
                                                        uint64_t n, int shift, const uint32_t *__restrict__ gcount,
-                                                       uint32_t *__restrict__ lookback, uint32_t *__restrict__ ctl) {
+                                                       uint64_t *__restrict__ lookback, uint32_t *__restrict__ ctl,
+                                                       uint32_t epoch) {
     sort_prio();
     __shared__ uint64_t sk[(RS_THREADS * IPT)];
     __shared__ uint32_t sv_full[HALF ? 1 : (RS_THREADS * IPT)];
@@ -255,8 +277,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
         wcnt[ww][d] = c;  // exclusive prefix over waves
         c += x;
     }
-    if (bid == 0) __hip_atomic_exchange(&lookback[d], LB_INC | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], LB_AGG | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t ep = (uint64_t)epoch << 32;
+    if (bid == 0) __hip_atomic_exchange(&lookback[d], ep | LB_INC | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], ep | LB_AGG | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t ds = block_excl_scan<uint32_t>(c, scan_lds, nullptr);
     const uint64_t gb = block_excl_scan<uint64_t>((uint64_t)gcount[d], scan_lds64, nullptr);
     dstart[d] = ds;
@@ -270,10 +293,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
         while (j >= 0) {
             uint32_t v[LB_WIN];
 #pragma unroll
-            for (int q = 0; q < LB_WIN; ++q)
-                v[q] = j - q >= 0 ? __hip_atomic_load(&lookback[(uint64_t)(j - q) * 256 + d], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)
-                                  : LB_INC;  // before tile 0: an inclusive zero
+            for (int q = 0; q < LB_WIN; ++q) {
+                const uint64_t x = j - q >= 0 ? __hip_atomic_load(&lookback[(uint64_t)(j - q) * 256 + d], __ATOMIC_RELAXED,
+                                                                  __HIP_MEMORY_SCOPE_AGENT)
+                                              : ep | LB_INC;  // before tile 0: an inclusive zero
+                v[q] = (x & ~0xFFFFFFFFull) == ep ? (uint32_t)x : 0u;  // another epoch: not ready
+            }
             int used = 0;
             bool done = false;
 #pragma unroll
@@ -295,7 +320,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
                 __builtin_amdgcn_s_sleep(1);
             }
         }
-        __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], LB_INC | (uint32_t)(excl + c), __ATOMIC_RELAXED,
+        __hip_atomic_exchange(&lookback[(uint64_t)bid * 256 + d], ep | LB_INC | (uint32_t)(excl + c), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
     }
     gofs[d] = gb + excl - ds;  // output position = gofs[digit] + local sorted position
@@ -429,8 +454,11 @@ constexpr int MT_THREADS = 1024;
 constexpr uint32_t MT_BUF = 4096;
 __global__ __launch_bounds__(MT_THREADS) void k_mark_ties(const uint64_t *__restrict__ pfx, uint64_t n, int shift,
                                                          uint8_t *__restrict__ tie, uint32_t *__restrict__ count,
-                                                         uint32_t *__restrict__ heads) {
+                                                         uint32_t *__restrict__ heads, uint32_t *__restrict__ zero,
+                                                         uint32_t nzero) {
     sort_prio();
+    if (blockIdx.x == 0)  // the sort's histogram / control words, ready (zero) for the next sort
+        for (uint32_t i = threadIdx.x; i < nzero; i += MT_THREADS) zero[i] = 0;
     __shared__ uint32_t buf[MT_BUF];
     __shared__ uint32_t wcnt[MT_THREADS / 64];
     __shared__ uint32_t sbase;
@@ -771,8 +799,8 @@ size_t scan_scratch_bytes(uint64_t n) { return (ceil_div(n ? n : 1, SC_TILE) + 1
 size_t radix_scratch_bytes(uint64_t n) {
     // look-back words for the smallest tile any pass may use (12 items per thread)
     const uint64_t nb = ceil_div(n ? n : 1, (uint64_t)RS_THREADS * 12);
-    // digit counts (8 x 256) + control words (8 passes x 4) + look-back words (8 passes x tiles x 256)
-    return (8 * 256 + 64 + 8ull * nb * 256) * sizeof(uint32_t) + 1024 + scan_scratch_bytes(n);
+    // digit counts (8 x 256) + control words (8 passes x 4) + u64 look-back words (8 passes x tiles x 256)
+    return (8 * 256 + 64) * sizeof(uint32_t) + 8ull * nb * 256 * sizeof(uint64_t) + 1024 + scan_scratch_bytes(n);
 }
 
 bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, int bit0, int bit1,
@@ -783,9 +811,9 @@ bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint
     const int npass = (bit1 - bit0 + 7) / 8;
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *ctl = counts + 8 * 256;
-    uint32_t *lookback = ctl + 64;
-    const size_t zero_words = 8 * 256 + 64 + (size_t)npass * nb * 256;
-    MKV_HIP(hipMemsetAsync(counts, 0, zero_words * sizeof(uint32_t), st));
+    uint64_t *lookback = reinterpret_cast<uint64_t *>(ctl + 64);  // byte offset 8448: 8-B aligned
+    // this scratch is shared with other kernels (scans): zeroed look-back words, epoch 1
+    MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t) + (size_t)npass * nb * 256 * sizeof(uint64_t), st));
     const uint32_t hist_blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 16), 2048);
     hipLaunchKernelGGL(k_os_hist, dim3(hist_blocks), dim3(RS_THREADS), 0, st, k, n, bit0, npass, counts);
     MKV_LAUNCH_CHECK();
@@ -795,10 +823,10 @@ bool radix_sort_pairs(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint
     for (int p = 0; p < npass; ++p) {
         if (lds_rank_ok(st))
             hipLaunchKernelGGL((k_os_pass<true, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
-                               counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
+                               counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p, 1u);
         else
             hipLaunchKernelGGL((k_os_pass<false, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, bit0 + 8 * p,
-                               counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p);
+                               counts + 256 * p, lookback + (size_t)p * nb * 256, ctl + 4 * p, 1u);
         MKV_LAUNCH_CHECK();
         std::swap(ki, ko);
         std::swap(vi, vo);
@@ -817,9 +845,10 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
 }
 
 void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, uint32_t *heads,
-                      hipStream_t st, int shift) {
+                      hipStream_t st, int shift, uint32_t *zero, uint32_t nzero) {
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n + 1, (uint64_t)MT_THREADS * 4), 512);
-    hipLaunchKernelGGL(k_mark_ties, dim3(blocks), dim3(MT_THREADS), 0, st, pfx, n, shift, tie, count, heads);
+    hipLaunchKernelGGL(k_mark_ties, dim3(blocks), dim3(MT_THREADS), 0, st, pfx, n, shift, tie, count, heads, zero,
+                       zero ? nzero : 0u);
     MKV_LAUNCH_CHECK();
 }
 void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint32_t *perm, uint64_t *pfx,
@@ -838,13 +867,17 @@ void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const
 }
 
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st, uint64_t off, bool lcp, uint8_t *kdst, uint64_t kcap, uint64_t *odst) {
+                        hipStream_t st, uint64_t off, bool lcp, uint8_t *kdst, uint64_t kcap, uint64_t *odst,
+                        bool zeroed, uint32_t *host_out, uint32_t *zero2) {
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
-    MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
-    if (!n) return;
+    if (!zeroed) MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
+    if (!n) {
+        if (zero2) MKV_HIP(hipMemsetAsync(zero2, 0, 8, st));
+        return;
+    }
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
     hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, lcp, pfx,
-                       counts, kdst, kcap, odst);
+                       counts, kdst, kcap, odst, host_out, zero2);
     MKV_LAUNCH_CHECK();
 }
 
@@ -863,8 +896,10 @@ void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t
     MKV_LAUNCH_CHECK();
 }
 
+uint64_t radix_prefix_lookback_words(uint64_t n) { return ceil_div(n ? n : 1, (uint64_t)RS_THREADS * MKV_SORT_IPT) * 256; }
+
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
-                         void *scratch, hipStream_t st, bool v_identity) {
+                         void *scratch, uint64_t *lookback, uint32_t *epoch, hipStream_t st, bool v_identity) {
     if (n <= 1 || !digit_mask) {
         if (v_identity && n) {
             hipLaunchKernelGGL(k_iota_u32, grid1d(n), dim3(256), 0, st, v, n);
@@ -876,26 +911,24 @@ bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, u
     const uint32_t nb = (uint32_t)ceil_div(n, (uint64_t)RS_THREADS * MKV_SORT_IPT);
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     uint32_t *ctl = counts + 8 * 256;
-    uint32_t *lookback = ctl + 64;
-    const int np = __builtin_popcount(digit_mask);
-    MKV_HIP(hipMemsetAsync(lookback, 0, (size_t)np * nb * 256 * sizeof(uint32_t), st));
     uint64_t *ki = k, *ko = k2;
     uint32_t *vi = v_identity ? nullptr : v, *vo = v2;
     uint32_t *valt = v;  // the ping-pong partner of vo once the first pass has produced real values
     bool swapped = false;
-    int q = 0;
     for (int p = 0; p < 8; ++p) {
         if (!((digit_mask >> p) & 1u)) continue;
         const bool lr = lds_rank_ok(st);
-        uint32_t *lb = lookback + (size_t)q * nb * 256;
+        // every pass a fresh epoch (0 is never drawn: the buffer starts zeroed); one region serves every
+        // pass, since the previous pass's words read as not ready
+        if (++*epoch == 0) ++*epoch;
+        uint64_t *lb = lookback;
         if (lr)
             hipLaunchKernelGGL((k_os_pass<true, true, MKV_SORT_IPT>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
-                               8 * p, counts + 256 * p, lb, ctl + 4 * p);
-        else
-            hipLaunchKernelGGL((k_os_pass<false, false>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n, 8 * p,
-                               counts + 256 * p, lb, ctl + 4 * p);
+                               8 * p, counts + 256 * p, lb, ctl + 4 * p, *epoch);
+        else  // same tile size (nb tiles of 256 x MKV_SORT_IPT), ballot ranks
+            hipLaunchKernelGGL((k_os_pass<false, true, MKV_SORT_IPT>), dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, ko, vo, n,
+                               8 * p, counts + 256 * p, lb, ctl + 4 * p, *epoch);
         MKV_LAUNCH_CHECK();
-        ++q;
         std::swap(ki, ko);
         uint32_t *written = vo;
         vo = vi ? vi : valt;

@@ -54,8 +54,10 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
 // tie[i] = (pfx[i] == pfx[i-1]) for i>0, tie[0] = 0; count[0] += number of ties. tie has n+1 entries
 // (tie[n] = 0 sentinel). Tie-run heads (tie[i] == 0, tie[i+1] == 1) go to heads[] (capacity n / 2 + 1,
 // any order), count[1] += their number.
+// zero / nzero (optional): words the first workgroup zeroes (a sort's histogram and control words, for the
+// next sort; the passes that read them are done).
 void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, uint32_t *heads,
-                      hipStream_t st, int shift = 0);
+                      hipStream_t st, int shift = 0, uint32_t *zero = nullptr, uint32_t nzero = 0);
 // Adaptive prefix sort (tree builds): one histogram read gives all eight byte-digit histograms
 // (counts[p*256+d], p = 0 the least significant byte) in `scratch`; the host then picks the digits
 // worth a pass (radix_prefix_passes: bit p of digit_mask = sort on byte p). Digits below the chosen
@@ -69,19 +71,29 @@ void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t
 constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
 constexpr uint32_t PH_NLCP_WORD = 8 * 256 + 62;
 constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;
+constexpr uint32_t PH_ARRIVE_WORD = 8 * 256 + 59;  // k_prefix_hist's arrival counter (host_out hand-off)
+constexpr uint32_t SORT_CTL_WORDS = 8 * 256 + 64;
 void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
 // lcp: also measure the shared prefix with key 0 (PH_NLCP_WORD) and key 0's first bytes (PH_K0_WORD),
 // for any window offset.
 // kdst / kcap / odst: optional key-ownership copy (builds from borrowed device blobs): key bytes at their
 // source offsets into kdst when every 16-B granule of them fits kcap (kb must be 16-B aligned), offsets
 // into odst. The caller checks koff[n] + 16 <= kcap to know the keys were copied.
+// zeroed: the SORT_CTL_WORDS words at scratch are already zero (else they are zeroed here). host_out
+// (device view of mapped pinned memory): receives every word when the pass is done (no copy launch).
+// zero2: two words zeroed on the way (the tie marker's counters).
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
                         hipStream_t st, uint64_t off = 0, bool lcp = true, uint8_t *kdst = nullptr, uint64_t kcap = 0,
-                        uint64_t *odst = nullptr);
+                        uint64_t *odst = nullptr, bool zeroed = false, uint32_t *host_out = nullptr,
+                        uint32_t *zero2 = nullptr);
 // v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;
 // with no pass at all v is filled with them). The result is in (k, v) or, when true is returned, (k2, v2).
+// scratch: the SORT_CTL_WORDS histogram / control words of launch_prefix_hist. lookback: ceil(n / 6144) x
+// 256 u64 words that hold nothing but look-back words (zeroed once when allocated); *epoch: the caller's
+// epoch counter, advanced once per pass.
 bool radix_prefix_passes(uint64_t *k, uint32_t *v, uint64_t *k2, uint32_t *v2, uint64_t n, uint32_t digit_mask,
-                         void *scratch, hipStream_t st, bool v_identity = false);
+                         void *scratch, uint64_t *lookback, uint32_t *epoch, hipStream_t st, bool v_identity = false);
+uint64_t radix_prefix_lookback_words(uint64_t n);
 // Orders every tie run of <= 16 positions on the full key in place (one thread per run); tie[] becomes
 // full-key equality there. count[0] += duplicate positions, count[1] += longer runs (left as they are).
 // Visits only the *nheads run heads of launch_mark_ties (max_heads: a host-side upper bound on *nheads).
@@ -143,10 +155,12 @@ struct FusePlan {
 };
 void launch_reduce_fused(const FusePlan &p, hipStream_t st);
 // Every remaining level in one launch (k_reduce_top): ntiles <= RD_TOP_TILES tiles of 512 parents fuse
-// nf (<= 10) levels each, then the last tile to arrive climbs levels nf+1 .. nl (<= 512 nodes at level
-// nf). arrive: a device counter that is 0 before the launch (the kernel leaves it 0 again).
+// nf (<= 10) levels each, then the last tile to arrive climbs levels nf+1 .. nl (level nf holds <= ntiles
+// nodes, so level nf+1 <= 512). arrive: a device counter that is 0 before the launch (the kernel leaves it
+// 0 again). 1024 tiles: a 10M-key tree goes from level 4 (611 tiles, ~3 per CU co-resident) to the root
+// in one launch instead of one 4-level launch + the top from level 8.
 constexpr int TOP_MAX_LEVELS = 40;
-constexpr uint64_t RD_TOP_TILES = 64;
+constexpr uint64_t RD_TOP_TILES = 1024;
 struct TopPlan {
     const uint8_t *in;
     uint8_t *out[TOP_MAX_LEVELS];

@@ -228,6 +228,11 @@ struct mkv_tree {
     DevBuf s_k1, s_k2, s_v1, s_v2;
     DevBuf s_tie, s_flags, s_scan, s_pos, s_pos0, s_lens;
     DevBuf s_radix, s_misc;
+    // the build sort's own histogram / control words (zero between sorts: the tie marker clears them) and
+    // epoch-tagged look-back words (zeroed once when allocated, never written by anything else)
+    DevBuf s_sortctl, s_lb;
+    uint32_t lb_epoch = 0;
+    bool sortctl_dirty = true;  // a sort started and did not reach its clearing launch
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
     // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
     std::vector<std::pair<uint32_t, uint32_t>> walk_jumps;
@@ -262,6 +267,7 @@ struct mkv_tree {
     uint64_t *h_small = nullptr;  // pinned host scalars (1 KB: bytes [512, 1024) = batched-walk counters)
     uint8_t *h_small_dev = nullptr;  // h_small as the device sees it (readbacks are kernel stores)
     uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
+    uint32_t *h_counts_dev = nullptr;  // h_counts as the device sees it (k_prefix_hist stores there)
     uint8_t *h_seam = nullptr;     // pinned staging of seam-combine inputs
     size_t h_seam_cap = 0;
 
@@ -901,20 +907,33 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     uint8_t *tie = ens<uint8_t>(t->s_tie, n_in + 2);
     uint32_t *misc = ens<uint32_t>(t->s_misc, 64);
     void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(n_in), scan_scratch_bytes(n_in + 1)));
+    // histogram / control words and look-back words of this sort: dedicated, so no zero-fill launches on
+    // the ordering stream (each one queued behind the co-running leaf hash for tens of microseconds)
+    const uint64_t lbw = radix_prefix_lookback_words(n_in);
+    if (!t->s_lb.p || t->s_lb.cap < lbw * 8) {
+        t->s_lb.ensure(lbw * 8);
+        MKV_HIP(hipMemsetAsync(t->s_lb.p, 0, t->s_lb.cap, st));
+        t->lb_epoch = 0;
+    }
+    if (!t->s_sortctl.p) t->s_sortctl.ensure(SORT_CTL_WORDS * 4);
+    uint32_t *sctl = t->s_sortctl.as<uint32_t>();
+    const bool ctl_zero = !t->sortctl_dirty;
+    t->sortctl_dirty = true;
 
     size_t ps = prof_begin(t, "sort", st);
     // one read of the keys: 8-byte windows + all eight digit histograms (the indices come from pass 1),
     // plus the prefix every key shares. The window starts at the shared length the previous sort of this
     // handle found (sort_win_hint; repeated builds of one key space share it), so the second histogram
-    // pass below only runs when the hint is off.
+    // pass below only runs when the hint is off. The pass hands its words to the host itself and zeroes
+    // the tie marker's two counters.
     const uint64_t hint = n_in > 1 ? t->sort_win_hint : 0;
-    launch_prefix_hist(kb, koff, n_in, k1, radix, st, hint, true, kdst, kcap, odst);
+    launch_prefix_hist(kb, koff, n_in, k1, sctl, st, hint, true, kdst, kcap, odst, ctl_zero,
+                       n_in > 1 ? t->h_counts_dev : nullptr, misc);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
     uint64_t win = hint;    // byte offset of the sort window
     uint64_t shared8 = 0;   // the first min(win, 8) bytes every key shares, big-endian at the top
     if (n_in > 1) {
-        MKV_HIP(hipMemcpyAsync(t->h_counts, radix, (8 * 256 + 64) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         wait_stream(t, st);
         // Bytes every key shares carry no order: move the window past them ("tenant/0001/object/..."
         // keys would otherwise tie on the whole prefix and leave all n keys to the chunk-by-chunk
@@ -926,23 +945,22 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         const uint64_t want = lcp > 0 && lcp < maxlen ? lcp : 0;
         if (want != hint) {
             win = want;
-            launch_prefix_hist(kb, koff, n_in, k1, radix, st, win, false);
-            MKV_HIP(hipMemcpyAsync(t->h_counts, radix, 8 * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+            launch_prefix_hist(kb, koff, n_in, k1, sctl, st, win, false, nullptr, 0, nullptr, false, t->h_counts_dev);
             wait_stream(t, st);
         }
         shared8 = win == 0 ? 0 : win >= 8 ? k0w : k0w & (~0ull << (64 - 8 * win));
         t->sort_win_hint = win;
         digits = choose_prefix_digits(t->h_counts, n_in, &lo_bit);
     }
-    const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, radix, st, true);
+    const bool sw = radix_prefix_passes(k1, v1, k2, v2, n_in, digits, sctl, t->s_lb.as<uint64_t>(), &t->lb_epoch, st, true);
     DevBuf *pkbuf = sw ? &t->s_k2 : &t->s_k1, *pkalt = sw ? &t->s_k1 : &t->s_k2;
     DevBuf *pmbuf = sw ? &t->s_v2 : &t->s_v1, *pmalt = sw ? &t->s_v1 : &t->s_v2;
     uint64_t *pk = pkbuf->as<uint64_t>();
     uint32_t *perm = pmbuf->as<uint32_t>();
     // run heads into the dedup flag scratch (free until the dedup below), their count in misc[1]
     uint32_t *heads = ens<uint32_t>(t->s_flags, n_in + 1);
-    MKV_HIP(hipMemsetAsync(misc, 0, 8, st));
-    launch_mark_ties(pk, n_in, tie, misc, heads, st, lo_bit);
+    launch_mark_ties(pk, n_in, tie, misc, heads, st, lo_bit, sctl, SORT_CTL_WORDS);  // clears sctl for the next sort
+    t->sortctl_dirty = false;
     prof_end(t, ps);
     const uint32_t nties = n_in ? d2h_u32(t, misc, st) : 0;
     static const bool dbg_sort = getenv("MKV_DEBUG_SORT") != nullptr;
@@ -1219,6 +1237,11 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess)
             e2 = hipHostMalloc(reinterpret_cast<void **>(&t->h_counts), (8 * 256 + 64) * sizeof(uint32_t),
                                hipHostMallocDefault);
+        if (e2 == hipSuccess) {
+            void *d = nullptr;
+            e2 = hipHostGetDevicePointer(&d, t->h_counts, 0);
+            t->h_counts_dev = static_cast<uint32_t *>(d);
+        }
         if (e2 == hipSuccess) {
             int lo = 0, hi = 0;  // aux (ordering) stream at the highest priority: its WGs dispatch first
             (void)hipDeviceGetStreamPriorityRange(&lo, &hi);

@@ -272,6 +272,55 @@ def test_diff_shared_long_prefixes_vs_oracle(oracle_lib):
     assert a.diff_keys_bytes(b) == oa.diff(ob)
 
 
+@pytest.mark.parametrize("extra", [True, False])
+def test_diff_distinct_keys_equal_prefix_equal_value_vs_oracle(oracle_lib, extra):
+    """R7 (merkle.rs:181-190) compares KEYS; the merge-join pairs leaves by 8-byte prefix + digest and
+    falls back to the full keys when the digests differ. Distinct keys with one 8-byte prefix (also the
+    zero-padding twins "pfx_0001" / "pfx_0001\\0") carrying IDENTICAL values sit on opposite sides: their
+    digests differ (the key is hashed), so the fallback must report both keys. extra=True adds a key on
+    one side (unequal leaf counts: merge-join), False keeps the counts equal (top-down walk)."""
+    common = [(b"cmn/%06d" % i, b"same") for i in range(3000)]
+    a_only = [(b"pfx_0000-alpha", b"v"), (b"pfx_0001", b"v"), (b"pfx_0002\x00\x00", b"w"), (b"zz-edge-a", b"q")]
+    b_only = [(b"pfx_0000-beta", b"v"), (b"pfx_0001\x00", b"v"), (b"pfx_0002\x00", b"w"), (b"zz-edge-b", b"q")]
+    a_pairs = common + a_only
+    b_pairs = common + b_only + ([(b"zzz-extra", b"x")] if extra else [])
+    a, b = MerkleTree(), MerkleTree()
+    a.build([k for k, _ in a_pairs], [v for _, v in a_pairs])
+    b.build([k for k, _ in b_pairs], [v for _, v in b_pairs])
+    want = oracle_lib.OracleTree.from_pairs(a_pairs).diff(oracle_lib.OracleTree.from_pairs(b_pairs))
+    assert want == sorted(k for k, _ in a_only + b_only + ([(b"zzz-extra", b"")] if extra else []))
+    assert a.diff_keys_bytes(b) == want
+    assert b.diff_keys_bytes(a) == want
+
+
+@pytest.mark.parametrize("na,nb", [
+    (16384, 16384 - 1),       # 32767 merged outputs: 64 tiles, one partition group, last tile short
+    (16383, 16385),           # exactly 64 tiles: the group's end split is the array end
+    (16385, 16384),           # 65 tiles: a second group holding one tile
+    (64 * 512 * 3, 700),      # three groups, B much shorter (splits clamp at B's end)
+    (5, 40000),               # A much shorter
+    (0, 3000),                # empty A
+    (3000, 0),                # empty B
+])
+def test_merge_join_partition_group_edges_vs_oracle(oracle_lib, na, nb):
+    """The merge-join's one-launch partition (a wave per 64 tiles: cooperative boundary searches, then
+    per-tile searches between them) at tile-count edges; unequal leaf counts force the merge-join."""
+    keys = sorted({b"%09d" % (i * 7919 % 1000003) for i in range(max(na, nb) + 2000)})
+    a_pairs = [(k, b"a") for k in keys[:na]]
+    # B: A's keys shifted by one position (key sets differ), every 13th value changed
+    b_keys = keys[1:nb + 1] if nb <= len(keys) - 1 else keys[:nb]
+    b_pairs = [(k, b"a" if i % 13 else b"b") for i, k in enumerate(b_keys)]
+    a, b = MerkleTree(), MerkleTree()
+    if a_pairs:
+        a.build([k for k, _ in a_pairs], [v for _, v in a_pairs])
+    if b_pairs:
+        b.build([k for k, _ in b_pairs], [v for _, v in b_pairs])
+    oa = oracle_lib.OracleTree.from_pairs(a_pairs)
+    ob = oracle_lib.OracleTree.from_pairs(b_pairs)
+    assert a.diff_keys_bytes(b) == oa.diff(ob)
+    assert b.diff_keys_bytes(a) == ob.diff(oa)
+
+
 def _near_identical(rng, n, shared_prefix, events):
     """Base replica + variant with 0.2 % value changes and the given structural events."""
     pre = b"tenant/0001/obj/" if shared_prefix else b""
