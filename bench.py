@@ -487,8 +487,8 @@ def ragged_block(ctx, n, fixed_leaf_ms, steps=5, warmup=2, klen=64, vlen=256):
            "gb_per_s_hashed": lsum / (leaf_ms * 1e-3) / 1e9,
            "fixed_shape_compressions_per_s": fixed_cps,
            "ratio_vs_fixed": cps / fixed_cps if fixed_cps else None, "root": root.hex(),
-           "note": "leaf_hash_ms = the whole leaf stage of the build (listing pass, bucketing by block count, "
-                   "k_leaf_ragged) while the ordering kernels co-run, HIP events on the tree's stream"}
+           "note": "leaf_hash_ms = the whole leaf stage of the build (k_leaf_direct hand-off, lane-refill k_leaf_ragged, "
+                   "k_leaf_edges) while the ordering kernels co-run, HIP events on the tree's stream"}
     del t, kb, vb, ko, vo
     torch.cuda.empty_cache()
     return out

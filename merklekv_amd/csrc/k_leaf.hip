@@ -289,6 +289,14 @@ __device__ __forceinline__ void load_words_a4(const uint8_t *p, uint32_t *w) {
     for (uint32_t i = NW / 4 * 4; i < NW; ++i) w[i] = reinterpret_cast<const uint32_t *>(p)[i];
 }
 
+template <uint32_t NW>
+__device__ __forceinline__ void store_words_a4(uint8_t *p, const uint32_t *w) {
+    u32x4_a4 *q = reinterpret_cast<u32x4_a4 *>(p);
+#pragma unroll
+    for (uint32_t i = 0; i < NW / 4; ++i) q[i] = u32x4_a4{w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]};
+#pragma unroll
+    for (uint32_t i = NW / 4 * 4; i < NW; ++i) reinterpret_cast<uint32_t *>(p)[i] = w[i];
+}
 
 // Fixed-shape records (the configs' 32-B keys / 100-B values at 4-B alignment): each lane loads its own
 // record's 33 message words straight from HBM into VGPRs with 16-B loads at 4-B alignment (gfx950 serves
@@ -298,10 +306,13 @@ __device__ __forceinline__ void load_words_a4(const uint8_t *p, uint32_t *w) {
 // with chunk w, then takes LEAF_GRAIN chunks per atomic from a device counter, so waves on CUs that also
 // run ordering workgroups simply take fewer. A chunk of any other shape ends the wave's work: it leaves
 // that chunk and the rest of its range in its slot for k_leaf_ragged and raises the flag (leaf.hpp).
+// KO: the key words already in registers go to the tree's own key buffer (and the offsets), so a build
+// from borrowed buffers needs no separate key copy (leaf.hpp).
 template <bool SHORT, uint32_t K0, uint32_t V0>
 __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                     const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
-                                                    uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ ctr) {
+                                                    uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
+                                                    KeyOut KO) {
     using Sh = LeafShape<K0, V0>;
     constexpr uint32_t MW = Sh::kw + Sh::vw;
     const uint32_t lane = threadIdx.x & 63;
@@ -330,6 +341,11 @@ __global__ __launch_bounds__(256) void k_leaf_direct(const uint8_t *__restrict__
             uint32_t m[MW];
             load_words_a4<Sh::kw>(kp, m);
             load_words_a4<Sh::vw>(vp, m + Sh::kw);
+            if (KO.kdst && kend <= KO.kcap) store_words_a4<Sh::kw>(KO.kdst + kbeg, m);
+            if (KO.odst) {
+                KO.odst[r] = kbeg;
+                if (r + 1 == n) KO.odst[n] = kend;
+            }
 #pragma unroll
             for (uint32_t i = 0; i < MW; ++i) m[i] = bswap32(m[i]);
             uint32_t st[8];
@@ -380,19 +396,21 @@ uint32_t leaf_fixed_waves(uint64_t n) {
 }
 
 void launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                       uint8_t *out, uint32_t *ctr, hipStream_t st) {
+                       uint8_t *out, uint32_t *ctr, hipStream_t st, const KeyOut &KO) {
     const uint32_t nw = leaf_fixed_waves(n);
     MKV_HIP(hipMemsetAsync(ctr, 0, (CTR_LIST + nw) * sizeof(uint32_t), st));
     if (!n) return;
     hipLaunchKernelGGL((k_leaf_direct<false, 32, 100>), dim3(nw / LEAF_WAVES), dim3(64 * LEAF_WAVES), 0, st, kb, koff,
-                       vb, voff, n, out, ctr);
+                       vb, voff, n, out, ctr, KO);
     MKV_LAUNCH_CHECK();
 }
 
 void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                      uint8_t *out, uint32_t *ctr, hipStream_t st) {
-    launch_leaf_fixed(kb, koff, vb, voff, n, out, ctr, st);
-    launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st);  // (and the edge records it leaves)
+                      uint8_t *out, uint32_t *ctr, hipStream_t st, const KeyOut &KO) {
+    // the key copy stores at the source's byte offsets: kb must share kdst's 16-B alignment
+    const KeyOut K{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? KO.kdst : nullptr, KO.odst, KO.kcap};
+    launch_leaf_fixed(kb, koff, vb, voff, n, out, ctr, st, K);
+    launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st, K);  // (and the edge records it leaves)
 }
 
 }  // namespace mkv

@@ -123,6 +123,7 @@ __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint64_t k1, uint
 __device__ __forceinline__ void rg_take_or_leave(RgRec &R, uint64_t k0, uint64_t k1, uint64_t v0, uint64_t v1,
                                                  uint32_t r, uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi,
                                                  int64_t vlo, int64_t vhi, uint32_t *ctr) {
+
     rg_take(R, k0, k1, v0, v1, r, kmis, vmis, klo, khi, vlo, vhi);
     if (!R.safe) {
         ctr[CTR_EDGE_LIST + atomicAdd(&ctr[CTR_EDGES], 1u)] = r;
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
                                                               const uint8_t *__restrict__ vb,
                                                               const uint64_t *__restrict__ voff, uint64_t n,
                                                               uint8_t *__restrict__ out, uint32_t *__restrict__ ctr,
-                                                              uint32_t nw) {
+                                                              uint32_t nw, KeyOut KO) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_all[RG_WAVES * RG_WAVE_DW];  // 34.3 KiB
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -224,6 +225,9 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     const uint8_t *kbase = kb - kmis, *vbase = vb - vmis;
     const int64_t klo = (int64_t)((kmis + koff[0]) & ~3ull), khi = (int64_t)((kmis + koff[n] + 3) & ~3ull);
     const int64_t vlo = (int64_t)((vmis + voff[0]) & ~3ull), vhi = (int64_t)((vmis + voff[n] + 3) & ~3ull);
+    // key ownership: a block's key-run dwords go to the same offsets of the tree's key buffer (kb is 16-B
+    // aligned there, so kmis == 0; every source dword lies inside [klo, khi) for the records kept here)
+    uint8_t *const kcp = KO.kdst && kmis == 0 && (uint64_t)khi + 16 <= KO.kcap ? KO.kdst : nullptr;
 
     Q.pnext = rg_grab(ctr, lane);
     Q.pv = Q.pe = 0;
@@ -254,6 +258,10 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
                 nk1 = ((uint64_t)a.w << 32) | a.z;
                 nv0 = ((uint64_t)b.y << 32) | b.x;
                 nv1 = ((uint64_t)b.w << 32) | b.z;
+                if (KO.odst) {  // key ownership: every record of a ragged chunk passes here (leaf.hpp)
+                    KO.odst[rec] = nk0;
+                    if (rec + 1 == n) KO.odst[n] = nk1;
+                }
             }
         }
         if (Q.qc != RG_INV) {
@@ -320,6 +328,12 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
                 lb[14] = R.L >> 29;
                 lb[15] = R.L << 3;
             }
+            if (kcp && P.key_in) {  // the 17 source dwords of the key run, unchanged, to the key buffer
+                rg4 *q = reinterpret_cast<rg4 *>(kcp + (R.ka + 4 * (int64_t)((int32_t)(16 * R.blk) + P.kend - 16)));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) q[j] = rg4{dk[4 * j], dk[4 * j + 1], dk[4 * j + 2], dk[4 * j + 3]};
+                reinterpret_cast<uint32_t *>(q)[16] = dk[16];
+            }
             const uint2 *l2 = reinterpret_cast<const uint2 *>(lb);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -367,7 +381,8 @@ __device__ __forceinline__ uint32_t edge_byte(const uint8_t *kp, const uint8_t *
 }
 __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                    const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
-                                                   uint8_t *__restrict__ out, const uint32_t *__restrict__ ctr) {
+                                                   uint8_t *__restrict__ out, const uint32_t *__restrict__ ctr,
+                                                   KeyOut KO) {
     const uint32_t m = ctr[CTR_EDGES];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
@@ -376,6 +391,8 @@ __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ 
         const uint64_t k0 = koff[r], v0 = voff[r];
         const uint32_t k = (uint32_t)(koff[r + 1] - k0), v = (uint32_t)(voff[r + 1] - v0);
         const uint32_t L = 8 + k + v, nb = (L + 72) >> 6;
+        if (KO.kdst && k0 + k <= KO.kcap)  // key ownership (the offset was stored when the record was taken)
+            for (uint32_t j = lane; j < k; j += 64) KO.kdst[k0 + j] = kb[k0 + j];
         uint32_t st[8];
         sha_init(st);
         for (uint32_t b = 0; b < nb; ++b) {
@@ -406,13 +423,13 @@ int device_cus() {
 }  // namespace
 
 void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                        uint8_t *out, uint32_t *ctr, hipStream_t st) {
+                        uint8_t *out, uint32_t *ctr, hipStream_t st, const KeyOut &KO) {
     if (!n) return;
     const uint64_t grid = std::min<uint64_t>((uint64_t)device_cus() * MKV_RAGGED_WGS, ceil_div(ceil_div(n, 64), RG_WAVES));
     hipLaunchKernelGGL(k_leaf_ragged<false>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
-                       kb, koff, vb, voff, n, out, ctr, leaf_fixed_waves(n));
+                       kb, koff, vb, voff, n, out, ctr, leaf_fixed_waves(n), KO);
     hipLaunchKernelGGL(k_leaf_edges, dim3((uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256)), dim3(256), 0, st, kb, koff,
-                       vb, voff, out, ctr);
+                       vb, voff, out, ctr, KO);
     MKV_LAUNCH_CHECK();
 }
 

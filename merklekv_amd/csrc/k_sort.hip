@@ -57,27 +57,15 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
 // with key 0 (PH_NLCP_WORD; bounded by the longer of the two keys, capped at PH_LCP_CAP) and key 0's
 // first 8 bytes (PH_K0_WORD, PH_K0_WORD + 1: high, low half).
 constexpr uint64_t PH_LCP_CAP = 1u << 16;
-// kdst / kcap / odst (builds from borrowed device blobs): the tree's own copy of the keys — key bytes at
-// their source offsets in 16-B granules (all or none: only when the granules fit kcap; kb 16-B aligned)
-// and the offsets. This pass already reads every key's cache lines, so the copy costs only its writes.
-// host_out (device view of mapped pinned memory, optional): the last workgroup to finish (arrival counter
-// PH_ARRIVE_WORD) copies the histograms and control words there, so the host reads them without a copy
-// launch of its own. zero2 (optional): two counter words zeroed for the tie marker that follows.
+// zero2 (optional): two counter words zeroed for the tie marker that follows. (No "last workgroup hands
+// the words to the host" tail: its per-workgroup agent-scope fence + same-address arrival atomic made
+// this pass 3x slower (161 -> 515 us) and, at sort priority, the co-running leaf hash 20 % slower.)
 __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__restrict__ kb,
                                                            const uint64_t *__restrict__ koff, uint64_t n,
                                                            uint64_t off, bool lcp, uint64_t *__restrict__ pfx,
-                                                           uint32_t *__restrict__ counts, uint8_t *__restrict__ kdst,
-                                                           uint64_t kcap, uint64_t *__restrict__ odst,
-                                                           uint32_t *__restrict__ host_out, uint32_t *__restrict__ zero2) {
+                                                           uint32_t *__restrict__ counts, uint32_t *__restrict__ zero2) {
     sort_prio();
     if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
-    if (kdst) {
-        const uint64_t g0 = koff[0] & ~15ull, g1 = (koff[n] + 15) & ~15ull;
-        if (g1 <= kcap)
-            for (uint64_t g = g0 + 16 * ((uint64_t)blockIdx.x * RS_THREADS + threadIdx.x); g < g1;
-                 g += 16 * (uint64_t)gridDim.x * RS_THREADS)
-                *reinterpret_cast<uint4 *>(kdst + g) = *reinterpret_cast<const uint4 *>(kb + g);
-    }
     __shared__ uint32_t h[8][256];
     __shared__ uint32_t lmax, lmin;
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
@@ -97,10 +85,6 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
     for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
         const uint64_t a = koff[i], b = koff[i + 1], len = b - a;
         const uint64_t k = key_chunk(kb + a, len, off);
-        if (odst) {
-            odst[i] = a;
-            if (i + 1 == n) odst[n] = b;
-        }
         mx = len > mx ? len : mx;
         pfx[i] = k;
 #pragma unroll
@@ -143,23 +127,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
         if (lmax) atomicMax(&counts[PH_MAXLEN_WORD], lmax);
         if (lcp) atomicMax(&counts[PH_NLCP_WORD], ~lmin);  // the words start at 0: max of ~x = min of x
         if (lcp && blockIdx.x == 0) {
-            __hip_atomic_store(&counts[PH_K0_WORD], (uint32_t)(k0w >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&counts[PH_K0_WORD + 1], (uint32_t)k0w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            counts[PH_K0_WORD] = (uint32_t)(k0w >> 32);
+            counts[PH_K0_WORD + 1] = (uint32_t)k0w;
         }
     }
-    if (!host_out) return;
-    // ---- the last workgroup hands every word to the host ----
-    __shared__ uint32_t last;
-    __threadfence();  // this thread's histogram atomics performed device-wide before the arrival
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t prev = __hip_atomic_fetch_add(&counts[PH_ARRIVE_WORD], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        last = prev + 1 == gridDim.x;
-    }
-    __syncthreads();
-    if (!last) return;
-    for (int i = threadIdx.x; i < 8 * 256 + 64; i += RS_THREADS)
-        host_out[i] = __hip_atomic_load(&counts[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Sorted set prefixes from sort windows at byte offset win > 0 (bytes [0, win) are shared by every key;
@@ -867,8 +838,7 @@ void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const
 }
 
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st, uint64_t off, bool lcp, uint8_t *kdst, uint64_t kcap, uint64_t *odst,
-                        bool zeroed, uint32_t *host_out, uint32_t *zero2) {
+                        hipStream_t st, uint64_t off, bool lcp, bool zeroed, uint32_t *zero2) {
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     if (!zeroed) MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) {
@@ -877,7 +847,7 @@ void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uin
     }
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
     hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, lcp, pfx,
-                       counts, kdst, kcap, odst, host_out, zero2);
+                       counts, zero2);
     MKV_LAUNCH_CHECK();
 }
 

@@ -2,6 +2,7 @@
 // All launchers are asynchronous on `st`; none allocates or synchronises.
 #pragma once
 #include "common.hpp"
+#include "leaf.hpp"
 
 namespace mkv {
 
@@ -25,14 +26,14 @@ uint32_t leaf_fixed_waves(uint64_t n);
 // The fixed-shape kernel (k_leaf_direct): zeroes the counter head and the hand-off slots, hashes every
 // chunk of the configs' 32/100-B shape and hands every other chunk to the ragged stage.
 void launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
+                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO);
 // Every chunk launch_leaf_fixed left (k_ragged.hip: any key / value lengths and alignments), then the few
 // records near the blobs' ends (k_leaf_edges). Same stream, after launch_leaf_fixed.
 void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                        uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
-// Both (the whole leaf stage).
+                        uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO);
+// Both (the whole leaf stage). KO: optional key-ownership copy (leaf.hpp; used only when kb is 16-B aligned).
 void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
-                      uint8_t *out_digests, uint32_t *ctr, hipStream_t st);
+                      uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO = KeyOut{});
 
 // ---- Kernel C: ordering (k_sort.hip) ----
 // pfx[i] = big-endian first 8 key bytes, zero padded (key i of kb/koff); idx[i] = i
@@ -71,20 +72,14 @@ void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t
 constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
 constexpr uint32_t PH_NLCP_WORD = 8 * 256 + 62;
 constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;
-constexpr uint32_t PH_ARRIVE_WORD = 8 * 256 + 59;  // k_prefix_hist's arrival counter (host_out hand-off)
 constexpr uint32_t SORT_CTL_WORDS = 8 * 256 + 64;
 void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
 // lcp: also measure the shared prefix with key 0 (PH_NLCP_WORD) and key 0's first bytes (PH_K0_WORD),
 // for any window offset.
-// kdst / kcap / odst: optional key-ownership copy (builds from borrowed device blobs): key bytes at their
-// source offsets into kdst when every 16-B granule of them fits kcap (kb must be 16-B aligned), offsets
-// into odst. The caller checks koff[n] + 16 <= kcap to know the keys were copied.
-// zeroed: the SORT_CTL_WORDS words at scratch are already zero (else they are zeroed here). host_out
-// (device view of mapped pinned memory): receives every word when the pass is done (no copy launch).
-// zero2: two words zeroed on the way (the tie marker's counters).
+// zeroed: the SORT_CTL_WORDS words at scratch are already zero (else they are zeroed here). zero2: two
+// words zeroed on the way (the tie marker's counters).
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
-                        hipStream_t st, uint64_t off = 0, bool lcp = true, uint8_t *kdst = nullptr, uint64_t kcap = 0,
-                        uint64_t *odst = nullptr, bool zeroed = false, uint32_t *host_out = nullptr,
+                        hipStream_t st, uint64_t off = 0, bool lcp = true, bool zeroed = false,
                         uint32_t *zero2 = nullptr);
 // v_identity: the values are the input indices 0..n-1 and are not read (the first pass generates them;
 // with no pass at all v is filled with them). The result is in (k, v) or, when true is returned, (k2, v2).
@@ -156,11 +151,11 @@ struct FusePlan {
 void launch_reduce_fused(const FusePlan &p, hipStream_t st);
 // Every remaining level in one launch (k_reduce_top): ntiles <= RD_TOP_TILES tiles of 512 parents fuse
 // nf (<= 10) levels each, then the last tile to arrive climbs levels nf+1 .. nl (level nf holds <= ntiles
-// nodes, so level nf+1 <= 512). arrive: a device counter that is 0 before the launch (the kernel leaves it
-// 0 again). 1024 tiles: a 10M-key tree goes from level 4 (611 tiles, ~3 per CU co-resident) to the root
-// in one launch instead of one 4-level launch + the top from level 8.
+// nodes). arrive: a device counter that is 0 before the launch (the kernel leaves it 0 again). 64 tiles:
+// starting the top at 1,024 tiles (a 10M tree from level 4 instead of one more fused launch + the top
+// from level 8) measured slower in round 4 (229 vs 63 + 105 us).
 constexpr int TOP_MAX_LEVELS = 40;
-constexpr uint64_t RD_TOP_TILES = 1024;
+constexpr uint64_t RD_TOP_TILES = 64;
 struct TopPlan {
     const uint8_t *in;
     uint8_t *out[TOP_MAX_LEVELS];

@@ -25,4 +25,14 @@ constexpr uint32_t LEAF_GRAIN = 4;     // k_leaf_direct: chunks per hand-out ato
 constexpr uint32_t LEAF_MAX_WAVES = 16384;  // slots: fixed-kernel waves (persistent grid, <= 16 per CU)
 constexpr uint32_t CTR_EDGE_LIST = CTR_LIST + LEAF_MAX_WAVES;  // n entries (every record may be an edge one)
 
+// Key ownership of a build from borrowed device blobs: the leaf kernels store the key bytes they load at
+// their source byte offsets into kdst (the tree's key buffer; kb 16-B aligned, so offsets coincide), and
+// every record's key offset into odst. kcap: kdst's capacity in bytes (a store past it is skipped; the
+// host then copies instead). Null pointers: no copy.
+struct KeyOut {
+    uint8_t *kdst;
+    uint64_t *odst;
+    uint64_t kcap;
+};
+
 }  // namespace mkv

@@ -895,10 +895,8 @@ struct SortedSet {
     DevBuf *pk, *pm;
     uint64_t n;
 };
-// kdst / kcap / odst: the tree's own copy of borrowed keys, written by the first histogram pass
-// (launch_prefix_hist).
 SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
-                      bool drop_tomb, uint8_t *kdst = nullptr, uint64_t kcap = 0, uint64_t *odst = nullptr) {
+                      bool drop_tomb) {
     hipStream_t st = t->st2;
     uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
     uint64_t *k2 = ens<uint64_t>(t->s_k2, n_in + 1);
@@ -924,11 +922,11 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     // one read of the keys: 8-byte windows + all eight digit histograms (the indices come from pass 1),
     // plus the prefix every key shares. The window starts at the shared length the previous sort of this
     // handle found (sort_win_hint; repeated builds of one key space share it), so the second histogram
-    // pass below only runs when the hint is off. The pass hands its words to the host itself and zeroes
-    // the tie marker's two counters.
+    // pass below only runs when the hint is off. The pass zeroes the tie marker's two counters; one small
+    // kernel copies its words into mapped pinned memory.
     const uint64_t hint = n_in > 1 ? t->sort_win_hint : 0;
-    launch_prefix_hist(kb, koff, n_in, k1, sctl, st, hint, true, kdst, kcap, odst, ctl_zero,
-                       n_in > 1 ? t->h_counts_dev : nullptr, misc);
+    launch_prefix_hist(kb, koff, n_in, k1, sctl, st, hint, true, ctl_zero, misc);
+    if (n_in > 1) copy_to_host(sctl, reinterpret_cast<uint8_t *>(t->h_counts_dev), SORT_CTL_WORDS * 4, st);
     int lo_bit = 0;
     uint32_t digits = 0xFF;
     uint64_t win = hint;    // byte offset of the sort window
@@ -945,7 +943,8 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         const uint64_t want = lcp > 0 && lcp < maxlen ? lcp : 0;
         if (want != hint) {
             win = want;
-            launch_prefix_hist(kb, koff, n_in, k1, sctl, st, win, false, nullptr, 0, nullptr, false, t->h_counts_dev);
+            launch_prefix_hist(kb, koff, n_in, k1, sctl, st, win, false, false);
+            copy_to_host(sctl, reinterpret_cast<uint8_t *>(t->h_counts_dev), SORT_CTL_WORDS * 4, st);
             wait_stream(t, st);
         }
         shared8 = win == 0 ? 0 : win >= 8 ? k0w : k0w & (~0ull << (64 - 8 * win));
@@ -1011,9 +1010,8 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     return SortedSet{pkbuf, pmbuf, n};
 }
 
-// fused_kcap: the sort's first histogram pass copies the borrowed keys into t->kb (capacity fused_kcap
-// bytes; complete when the key bytes + 16 fit) and the offsets into t->koff (fused_koff); 0 / false: the
-// copy is made here.
+// fused_kcap: the leaf kernels copied the borrowed keys into t->kb (capacity fused_kcap bytes; complete
+// when the key bytes + 16 fit) and the offsets into t->koff (fused_koff); 0 / false: the copy is made here.
 void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
                        bool staged_inputs, uint64_t staged_kbytes, bool defer_gather, uint64_t fused_kcap = 0,
                        bool fused_koff = false) {
@@ -1021,8 +1019,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
     hipStream_t st = t->st2;
     const uint8_t *dig = t->s_dig.as<uint8_t>();
-    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true, fused_kcap ? t->kb.as<uint8_t>() : nullptr, fused_kcap,
-                                    fused_koff ? t->koff.as<uint64_t>() : nullptr);
+    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true);
     DevBuf *pkbuf = S.pk, *pmbuf = S.pm;
     const uint64_t n = S.n;
     uint32_t *perm;
@@ -1368,15 +1365,16 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
 }
 
 // The leaf stage of a build: the fixed-shape kernel, then the ragged kernel for whatever it left. Borrowed
-// device inputs (!staged): the tree must own a copy of the keys; the sort's first pass writes it when the
-// buffers of an earlier build are large enough (*kcap / *ko_fused, see sort_unique), else
-// sort_dedup_gather copies the keys afterwards.
+// device inputs (!staged): the tree must own a copy of the keys; the leaf kernels store the key words they
+// load (and the offsets) into the tree's buffers when those from an earlier build are large enough (*kcap /
+// *ko_fused), else sort_dedup_gather copies the keys afterwards.
 static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
                                   const uint64_t *voff, uint64_t n, uint8_t *dig, bool staged, uint64_t *kcap,
                                   bool *ko_fused) {
     *kcap = !staged && t->kb.p && (reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? t->kb.cap : 0;
     *ko_fused = !staged && t->koff.p && t->koff.cap >= (n + 1) * 8;
-    launch_leaf_hash(kb, koff, vb, voff, n, dig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)), t->st);
+    const KeyOut KO{*kcap ? t->kb.as<uint8_t>() : nullptr, *ko_fused ? t->koff.as<uint64_t>() : nullptr, *kcap};
+    launch_leaf_hash(kb, koff, vb, voff, n, dig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)), t->st, KO);
 }
 
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
