@@ -140,7 +140,9 @@ mkv_status mkv_tree_hash_pattern(const mkv_tree *t, const uint8_t *pattern, uint
                                  int *has_root);
 
 /* Key i of a list is bytes[offsets[i] .. offsets[i+1]) (offsets has n+1 entries; offsets[0] may be
- * nonzero). The memory stays valid until mkv_keylist_free. */
+ * nonzero). The memory stays valid until mkv_keylist_free. The lists of mkv_tree_diff_many may still be
+ * on their way into host memory when the call returns (the copy overlaps the caller's next work): n is
+ * available at once; asking for bytes or offsets waits for the copy. */
 mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **bytes, const uint64_t **offsets);
 void mkv_keylist_free(mkv_keylist *l);
 

@@ -16,6 +16,7 @@ communicator per (group, device, form).
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 
 from ._lib import ALLGATHER_FN, COLL_KINDS, COMM_ID_BYTES, MerkleError, check, lib
 
@@ -89,17 +90,24 @@ class Comm:
         c = _cache.get(key)
         if c is not None:
             return c
+        from .shard import _all_gather_bytes
+        c = None
         if form == "rccl":
             idx = dev.index if dev.index is not None else torch.cuda.current_device()
-            t = torch.zeros(COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+            t = torch.zeros(COMM_ID_BYTES + 1, dtype=torch.uint8, device=dev)
             if rank == 0:
-                t.copy_(torch.frombuffer(bytearray(cls.unique_id()), dtype=torch.uint8))
+                try:
+                    t[:COMM_ID_BYTES].copy_(torch.frombuffer(bytearray(cls.unique_id()), dtype=torch.uint8))
+                    t[COMM_ID_BYTES] = 1
+                except MerkleError as e:  # no RCCL in this process: every rank takes the host form
+                    warnings.warn(f"merklekv_amd: RCCL communicator unavailable ({e}); host all-gather instead")
             src = dist.get_global_rank(group, 0) if group is not None else 0
             dist.broadcast(t, src=src, group=group)
-            c = cls.rccl(t.cpu().numpy().tobytes(), rank, world, idx)
-        else:
-            from .shard import _all_gather_bytes
-            c = cls.host(rank, world, lambda p: _all_gather_bytes(dist, p, "cpu", group))
+            if int(t[COMM_ID_BYTES].item()):
+                c = cls.rccl(t[:COMM_ID_BYTES].cpu().numpy().tobytes(), rank, world, idx)
+        if c is None:  # host form over the group (gloo, or the group's own device collectives)
+            coll_dev = "cpu" if form == "host" else dev
+            c = cls.host(rank, world, lambda p: _all_gather_bytes(dist, p, coll_dev, group))
         _cache[key] = c
         return c
 

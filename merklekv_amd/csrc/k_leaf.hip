@@ -411,6 +411,7 @@ void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
     const KeyOut K{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? KO.kdst : nullptr, KO.odst, KO.kcap};
     launch_leaf_fixed(kb, koff, vb, voff, n, out, ctr, st, K);
     launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st, K);  // (and the edge records it leaves)
+    if (K.kdst) launch_keycopy_ragged(kb, koff, n, ctr, K.kdst, K.kcap, st);
 }
 
 }  // namespace mkv

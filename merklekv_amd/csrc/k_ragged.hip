@@ -225,9 +225,6 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     const uint8_t *kbase = kb - kmis, *vbase = vb - vmis;
     const int64_t klo = (int64_t)((kmis + koff[0]) & ~3ull), khi = (int64_t)((kmis + koff[n] + 3) & ~3ull);
     const int64_t vlo = (int64_t)((vmis + voff[0]) & ~3ull), vhi = (int64_t)((vmis + voff[n] + 3) & ~3ull);
-    // key ownership: a block's key-run dwords go to the same offsets of the tree's key buffer (kb is 16-B
-    // aligned there, so kmis == 0; every source dword lies inside [klo, khi) for the records kept here)
-    uint8_t *const kcp = KO.kdst && kmis == 0 && (uint64_t)khi + 16 <= KO.kcap ? KO.kdst : nullptr;
 
     Q.pnext = rg_grab(ctr, lane);
     Q.pv = Q.pe = 0;
@@ -328,12 +325,6 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
                 lb[14] = R.L >> 29;
                 lb[15] = R.L << 3;
             }
-            if (kcp && P.key_in) {  // the 17 source dwords of the key run, unchanged, to the key buffer
-                rg4 *q = reinterpret_cast<rg4 *>(kcp + (R.ka + 4 * (int64_t)((int32_t)(16 * R.blk) + P.kend - 16)));
-#pragma unroll
-                for (int j = 0; j < 4; ++j) q[j] = rg4{dk[4 * j], dk[4 * j + 1], dk[4 * j + 2], dk[4 * j + 3]};
-                reinterpret_cast<uint32_t *>(q)[16] = dk[16];
-            }
             const uint2 *l2 = reinterpret_cast<const uint2 *>(lb);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -381,8 +372,7 @@ __device__ __forceinline__ uint32_t edge_byte(const uint8_t *kp, const uint8_t *
 }
 __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                    const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
-                                                   uint8_t *__restrict__ out, const uint32_t *__restrict__ ctr,
-                                                   KeyOut KO) {
+                                                   uint8_t *__restrict__ out, const uint32_t *__restrict__ ctr) {
     const uint32_t m = ctr[CTR_EDGES];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
@@ -391,8 +381,6 @@ __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ 
         const uint64_t k0 = koff[r], v0 = voff[r];
         const uint32_t k = (uint32_t)(koff[r + 1] - k0), v = (uint32_t)(voff[r + 1] - v0);
         const uint32_t L = 8 + k + v, nb = (L + 72) >> 6;
-        if (KO.kdst && k0 + k <= KO.kcap)  // key ownership (the offset was stored when the record was taken)
-            for (uint32_t j = lane; j < k; j += 64) KO.kdst[k0 + j] = kb[k0 + j];
         uint32_t st[8];
         sha_init(st);
         for (uint32_t b = 0; b < nb; ++b) {
@@ -407,6 +395,37 @@ __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ 
             sha_compress<false>(st, w);
         }
         if (lane == 0) store_digest(out + 32 * (uint64_t)r, st);
+    }
+}
+
+// Key ownership of the chunks the ragged stage hashed (leaf.hpp; their offsets were stored by the
+// ragged kernel's refill): the key bytes of every such chunk, copied in 16-B granules at their source
+// offsets — chunks [B, nch) as one span (blockIdx.y 0), each fixed-kernel slot's chunks by one wave
+// (blockIdx.y 1). It runs on a stream of its own as soon as k_leaf_direct is done, beside the VALU-bound
+// ragged hash (a few VGPRs, no LDS). (Stores of the key-run dwords from inside k_leaf_ragged cost 10 % of
+// the hash: 68 B of partial-line stores per record and key block; queued after the ragged kernels it
+// stretched the sort's co-running passes.)
+__global__ __launch_bounds__(256) void k_keycopy_ragged(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                        uint64_t n, const uint32_t *__restrict__ ctr, uint32_t nw,
+                                                        uint8_t *__restrict__ kdst, uint64_t kcap) {
+    const uint32_t nch = (uint32_t)((n + 63) / 64);
+    uint32_t B, nslot;
+    rg_handoff(ctr, nch, nw, &B, &nslot);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    auto copy_span = [&](uint64_t r0, uint64_t r1, uint64_t t0, uint64_t step) {  // records [r0, r1)
+        const uint64_t g0 = koff[r0] & ~15ull, g1 = (koff[r1] + 15) & ~15ull;
+        if (g1 <= kcap)
+            for (uint64_t g = g0 + 16 * t0; g < g1; g += 16 * step)
+                *reinterpret_cast<uint4 *>(kdst + g) = *reinterpret_cast<const uint4 *>(kb + g);
+    };
+    if (blockIdx.y == 0) {
+        if (B < nch) copy_span((uint64_t)B * 64, n, t, stride);
+    } else if (nslot) {
+        const uint32_t lane = threadIdx.x & 63;
+        for (uint64_t s = t / 64; s < nw; s += stride / 64) {
+            const uint32_t v = ctr[CTR_LIST + s], c = v >> 5, cnt = v & 31u;
+            if (cnt) copy_span((uint64_t)c * 64, std::min<uint64_t>((uint64_t)(c + cnt) * 64, n), lane, 64);
+        }
     }
 }
 
@@ -429,7 +448,14 @@ void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *
     hipLaunchKernelGGL(k_leaf_ragged<false>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
                        kb, koff, vb, voff, n, out, ctr, leaf_fixed_waves(n), KO);
     hipLaunchKernelGGL(k_leaf_edges, dim3((uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256)), dim3(256), 0, st, kb, koff,
-                       vb, voff, out, ctr, KO);
+                       vb, voff, out, ctr);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_keycopy_ragged(const uint8_t *kb, const uint64_t *koff, uint64_t n, const uint32_t *ctr, uint8_t *kdst,
+                           uint64_t kcap, hipStream_t st) {
+    if (!n || !kdst) return;
+    hipLaunchKernelGGL(k_keycopy_ragged, dim3(1024, 2), dim3(256), 0, st, kb, koff, n, ctr, leaf_fixed_waves(n), kdst, kcap);
     MKV_LAUNCH_CHECK();
 }
 

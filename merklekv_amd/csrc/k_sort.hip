@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
 // with key 0 (PH_NLCP_WORD; bounded by the longer of the two keys, capped at PH_LCP_CAP) and key 0's
 // first 8 bytes (PH_K0_WORD, PH_K0_WORD + 1: high, low half).
 constexpr uint64_t PH_LCP_CAP = 1u << 16;
-// zero2 (optional): two counter words zeroed for the tie marker that follows. (No "last workgroup hands
+// zero2 (optional): eight counter words zeroed for the tie marker and refinement that follow. (No "last workgroup hands
 // the words to the host" tail: its per-workgroup agent-scope fence + same-address arrival atomic made
 // this pass 3x slower (161 -> 515 us) and, at sort priority, the co-running leaf hash 20 % slower.)
 __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__restrict__ kb,
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
                                                            uint64_t off, bool lcp, uint64_t *__restrict__ pfx,
                                                            uint32_t *__restrict__ counts, uint32_t *__restrict__ zero2) {
     sort_prio();
-    if (zero2 && blockIdx.x == 0 && threadIdx.x < 2) zero2[threadIdx.x] = 0;
+    if (zero2 && blockIdx.x == 0 && threadIdx.x < 8) zero2[threadIdx.x] = 0;
     __shared__ uint32_t h[8][256];
     __shared__ uint32_t lmax, lmin;
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
@@ -559,15 +559,10 @@ __global__ void k_refine_apply(const uint32_t *__restrict__ pos, uint64_t m, con
 // tie[] becomes full-key equality for those runs; count[0] += equal-key positions (duplicates),
 // count[1] += longer runs, which are left untouched for the general refinement.
 constexpr uint32_t RS_SMALL_RUN = 16;
-__global__ __launch_bounds__(256) void k_refine_small(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
-                                                     uint64_t n, uint32_t *__restrict__ perm,
-                                                     uint64_t *__restrict__ pfx, uint8_t *__restrict__ tie,
-                                                     uint32_t *__restrict__ count,
-                                                     const uint32_t *__restrict__ heads,
-                                                     const uint32_t *__restrict__ nheads) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *nheads) return;
-    const uint64_t i = heads[t];  // a run head: tie[i] == 0, tie[i + 1] == 1
+// One run, starting at head i (tie[i] == 0, tie[i + 1] == 1).
+__device__ void refine_small_run(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff, uint64_t n,
+                                 uint32_t *__restrict__ perm, uint64_t *__restrict__ pfx, uint8_t *__restrict__ tie,
+                                 uint32_t *__restrict__ count, uint64_t i) {
     uint64_t j = i + 1;
     while (j < n && tie[j] && j - i <= RS_SMALL_RUN) ++j;
     if (j - i > RS_SMALL_RUN) {
@@ -605,6 +600,17 @@ __global__ __launch_bounds__(256) void k_refine_small(const uint8_t *__restrict_
         dups += eq;
     }
     if (dups) atomicAdd(&count[0], dups);
+}
+
+__global__ __launch_bounds__(256) void k_refine_small(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
+                                                     uint64_t n, uint32_t *__restrict__ perm,
+                                                     uint64_t *__restrict__ pfx, uint8_t *__restrict__ tie,
+                                                     uint32_t *__restrict__ count,
+                                                     const uint32_t *__restrict__ heads,
+                                                     const uint32_t *__restrict__ nheads) {
+    const uint64_t nh = *nheads;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nh; t += (uint64_t)gridDim.x * blockDim.x)
+        refine_small_run(kb, koff, n, perm, pfx, tie, count, heads[t]);
 }
 
 // After a refinement that started at chunk 0: the prefixes of re-ordered tie-run positions follow.
@@ -826,8 +832,9 @@ void launch_refine_small(const uint8_t *kb, const uint64_t *koff, uint64_t n, ui
                          uint8_t *tie, uint32_t *count, const uint32_t *heads, const uint32_t *nheads,
                          uint64_t max_heads, hipStream_t st) {
     if (!n || !max_heads) return;
-    hipLaunchKernelGGL(k_refine_small, grid1d(max_heads), dim3(256), 0, st, kb, koff, n, perm, pfx, tie, count, heads,
-                       nheads);
+    // grid-stride over the device-side head count: a bounded grid however loose max_heads is
+    const dim3 g((uint32_t)std::min<uint64_t>(ceil_div(max_heads, 256), 512));
+    hipLaunchKernelGGL(k_refine_small, g, dim3(256), 0, st, kb, koff, n, perm, pfx, tie, count, heads, nheads);
     MKV_LAUNCH_CHECK();
 }
 void launch_fix_pfx(const uint32_t *pos, uint64_t m, const uint32_t *perm, const uint8_t *kb, const uint64_t *koff,
@@ -842,7 +849,7 @@ void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uin
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     if (!zeroed) MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) {
-        if (zero2) MKV_HIP(hipMemsetAsync(zero2, 0, 8, st));
+        if (zero2) MKV_HIP(hipMemsetAsync(zero2, 0, 32, st));
         return;
     }
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);

@@ -31,7 +31,13 @@ void launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *v
 // records near the blobs' ends (k_leaf_edges). Same stream, after launch_leaf_fixed.
 void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                         uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO);
-// Both (the whole leaf stage). KO: optional key-ownership copy (leaf.hpp; used only when kb is 16-B aligned).
+// Key bytes of the chunks the ragged stage hashes (k_leaf_ragged stores only their offsets), 16-B
+// granules at the source offsets into kdst (<= kcap). Needs only launch_leaf_fixed's hand-off words: may
+// run on another stream once launch_leaf_fixed is done.
+void launch_keycopy_ragged(const uint8_t *kb, const uint64_t *koff, uint64_t n, const uint32_t *ctr, uint8_t *kdst,
+                           uint64_t kcap, hipStream_t st);
+// Both (the whole leaf stage; the ragged key copy queued after it). KO: optional key-ownership copy
+// (leaf.hpp; used only when kb is 16-B aligned).
 void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                       uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO = KeyOut{});
 
@@ -76,8 +82,8 @@ constexpr uint32_t SORT_CTL_WORDS = 8 * 256 + 64;
 void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
 // lcp: also measure the shared prefix with key 0 (PH_NLCP_WORD) and key 0's first bytes (PH_K0_WORD),
 // for any window offset.
-// zeroed: the SORT_CTL_WORDS words at scratch are already zero (else they are zeroed here). zero2: two
-// words zeroed on the way (the tie marker's counters).
+// zeroed: the SORT_CTL_WORDS words at scratch are already zero (else they are zeroed here). zero2: eight
+// words zeroed on the way (the tie marker's and the short-run refinement's counters).
 void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uint64_t *pfx, void *scratch,
                         hipStream_t st, uint64_t off = 0, bool lcp = true, bool zeroed = false,
                         uint32_t *zero2 = nullptr);

@@ -163,13 +163,37 @@ struct PinnedBlock {
 };
 }  // namespace
 
+// Completion of an asynchronous device -> pinned copy (a key list still in flight).
+struct KeyEvent {
+    hipEvent_t e = nullptr;
+    KeyEvent() { MKV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming)); }
+    ~KeyEvent() {
+        if (e) (void)hipEventDestroy(e);
+    }
+    KeyEvent(const KeyEvent &) = delete;
+    KeyEvent &operator=(const KeyEvent &) = delete;
+};
+
 struct mkv_keylist {
     std::shared_ptr<PinnedBlock> blk;  // null for an empty list
     const uint8_t *bytes = nullptr;
     const uint64_t *offsets = nullptr;  // n+1 entries; offsets[0] may be nonzero (a view into a shared block)
     uint64_t n = 0;
     uint64_t zero = 0;
+    // set while the bytes / offsets are still being copied (the batched diff's lists): mkv_keylist_get
+    // with a bytes or offsets pointer waits for it, and so does the destructor (before blk goes back to
+    // the pinned pool)
+    std::shared_ptr<KeyEvent> ready;
     mkv_keylist() { offsets = &zero; }
+    ~mkv_keylist() {
+        if (ready) (void)hipEventSynchronize(ready->e);
+    }
+    void wait() {
+        if (ready) {
+            (void)hipEventSynchronize(ready->e);
+            ready.reset();
+        }
+    }
 };
 
 // A key list over host bytes (the sharded diff's gathered global list, comm.cpp): one pinned block holding
@@ -201,6 +225,8 @@ struct mkv_tree {
     hipStream_t st = nullptr;   // main stream: leaf hashing, digest gather, reduction, diff
     hipStream_t st2 = nullptr;  // aux stream: key ownership copy, prefix sort, ties, dedup (overlaps st)
     hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr;
+    hipStream_t st3 = nullptr;  // build: the ragged chunks' key copy, beside the ragged hash
+    hipEvent_t ev_fixed = nullptr, ev_kc = nullptr;
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
@@ -233,6 +259,7 @@ struct mkv_tree {
     DevBuf s_sortctl, s_lb;
     uint32_t lb_epoch = 0;
     bool sortctl_dirty = true;  // a sort started and did not reach its clearing launch
+    bool kc_pending = false;    // the ragged key copy on st3 is not yet joined into st2
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
     // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
     std::vector<std::pair<uint32_t, uint32_t>> walk_jumps;
@@ -241,6 +268,9 @@ struct mkv_tree {
     DevBuf s_nodes2;  // prefix-root scratch levels
     DevBuf leaf_ctr;  // dynamic chunk counter of the leaf hash
     DevBuf d_refs, d_diffscr, d_out, d_outoff;
+    DevBuf a_out, a_outoff, a_lens;    // staging of the batched diff's key list (copied out asynchronously)
+    std::shared_ptr<KeyEvent> a_ev;    // that copy: the next use of a_out / a_outoff waits for it
+    hipEvent_t ev_a = nullptr;         // gather done on st -> copy on st3
     DevBuf td_f0, td_f1, td_cnt, td_k1, td_k2, td_v1, td_v2;
     DevBuf td_bm, td_bc;            // divergent-position bitmap (all-zero between calls) + block counts
     uint64_t tail_cap_m = 0, tail_cap_b = 0;  // one-wait top-down tail: key-list capacity (keys, bytes)
@@ -328,9 +358,11 @@ __global__ __launch_bounds__(256) void k_copy_to_host(const uint8_t *__restrict_
         reinterpret_cast<uint4 *>(dst)[v] = reinterpret_cast<const uint4 *>(src)[v];
     if (t < bytes - nv * 16) dst[nv * 16 + t] = src[nv * 16 + t];
 }
-void copy_to_host(const void *src, uint8_t *dst_dev_view, uint64_t bytes, hipStream_t st) {
+// max_blocks: a PCIe-bound copy needs few waves in flight; an asynchronous one (beside other work) keeps
+// its CU footprint small.
+void copy_to_host(const void *src, uint8_t *dst_dev_view, uint64_t bytes, hipStream_t st, uint64_t max_blocks = 2048) {
     if (!bytes) return;
-    const uint64_t blocks = std::min<uint64_t>(ceil_div(bytes / 16 + 1, 256), 2048);
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(bytes / 16 + 1, 256), max_blocks);
     hipLaunchKernelGGL(k_copy_to_host, dim3((uint32_t)blocks), dim3(256), 0, st, static_cast<const uint8_t *>(src),
                        dst_dev_view, bytes);
     MKV_LAUNCH_CHECK();
@@ -629,6 +661,7 @@ void wait_stream(mkv_tree *t, hipStream_t s) {
 void sync(mkv_tree *t) {
     wait_stream(t, t->st2);
     wait_stream(t, t->st);
+    if (t->st3) wait_stream(t, t->st3);  // an asynchronous key-list copy (or the ragged key copy) of this tree
     prof_collect(t);
 }
 
@@ -895,8 +928,9 @@ struct SortedSet {
     DevBuf *pk, *pm;
     uint64_t n;
 };
+// kbytes_out (optional): koff[n_in], read back with the sort's own counts (one host round trip).
 SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
-                      bool drop_tomb) {
+                      bool drop_tomb, uint64_t *kbytes_out = nullptr) {
     hipStream_t st = t->st2;
     uint64_t *k1 = ens<uint64_t>(t->s_k1, n_in + 1);
     uint64_t *k2 = ens<uint64_t>(t->s_k2, n_in + 1);
@@ -960,8 +994,17 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     uint32_t *heads = ens<uint32_t>(t->s_flags, n_in + 1);
     launch_mark_ties(pk, n_in, tie, misc, heads, st, lo_bit, sctl, SORT_CTL_WORDS);  // clears sctl for the next sort
     t->sortctl_dirty = false;
+    // Short tie runs are ordered in place right behind the tie marker (the kernel reads the head count on
+    // the device, so no host round trip in between); ONE readback then brings the tie, duplicate and
+    // long-run counts (misc[0], [4], [5]) and, for borrowed inputs, the key-byte total.
+    if (n_in > 1) launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, heads, misc + 1, n_in / 2 + 1, st);
     prof_end(t, ps);
-    const uint32_t nties = n_in ? d2h_u32(t, misc, st) : 0;
+    small_d2h(t, t->h_small, misc, 32, st);
+    if (kbytes_out && n_in) small_d2h(t, t->h_small + 4, koff + n_in, 8, st);
+    wait_stream(t, st);
+    const uint32_t *hm = reinterpret_cast<const uint32_t *>(t->h_small);
+    const uint32_t nties = n_in ? hm[0] : 0, dups = hm[4], long_runs = hm[5];
+    if (kbytes_out) *kbytes_out = n_in ? t->h_small[4] : 0;
     static const bool dbg_sort = getenv("MKV_DEBUG_SORT") != nullptr;
     if (dbg_sort)
         fprintf(stderr, "[mkv sort] n=%llu win=%llu lo_bit=%d digits=0x%x ties=%u heads=%u\n", (unsigned long long)n_in,
@@ -969,15 +1012,8 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     bool dedup = false;
     if (nties) {
         size_t pr = prof_begin(t, "sort", st);
-        // short tie runs: one in-place pass; longer ones: the general chunk-by-chunk refinement, which
-        // reorders perm (and, when chunk 0 was sorted only in part, pk) inside tie runs only
-        MKV_HIP(hipMemsetAsync(misc + 4, 0, 8, st));
-        // every run head is followed by >= 1 tie, so heads <= nties
-        launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, heads, misc + 1, nties, st);
-        small_d2h(t, t->h_small, misc + 4, 8, st);
-        wait_stream(t, st);
-        const uint32_t dups = reinterpret_cast<uint32_t *>(t->h_small)[0];
-        const uint32_t long_runs = reinterpret_cast<uint32_t *>(t->h_small)[1];
+        // longer tie runs: the general chunk-by-chunk refinement, which reorders perm (and, when chunk 0
+        // was sorted only in part, pk) inside tie runs only
         // chunks (8-byte aligned) fully ordered so far: bytes [0, win) are shared, window bytes above
         // lo_bit are sorted
         const uint32_t start_depth = (uint32_t)((win + 8 - lo_bit / 8) / 8);
@@ -1019,7 +1055,8 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // t->st (the caller made st2 wait for the staged inputs); the streams join before the digest gather.
     hipStream_t st = t->st2;
     const uint8_t *dig = t->s_dig.as<uint8_t>();
-    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true);
+    uint64_t kb_total = 0;
+    const SortedSet S = sort_unique(t, kb, koff, n_in, tomb, true, staged_inputs ? nullptr : &kb_total);
     DevBuf *pkbuf = S.pk, *pmbuf = S.pm;
     const uint64_t n = S.n;
     uint32_t *perm;
@@ -1032,11 +1069,15 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     perm = t->perm.as<uint32_t>();
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
     // a readback there would hold the host until the gather finishes and delay the reduce launches)
-    const uint64_t kbytes = staged_inputs ? staged_kbytes : (n_in ? d2h_u64(t, koff + n_in, st) : 0);
+    const uint64_t kbytes = staged_inputs ? staged_kbytes : kb_total;
     const bool keys_done = !staged_inputs && fused_kcap && kbytes + 16 <= fused_kcap;
     // The reduction on st needs only the sorted order: join here, before the key copy.
     MKV_HIP(hipEventRecord(t->ev_join, st));
     MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
+    if (t->kc_pending) {  // the ragged key copy (st3) completes before st2 does: the call's sync covers it
+        MKV_HIP(hipStreamWaitEvent(st, t->ev_kc, 0));
+        t->kc_pending = false;
+    }
     // Own the keys (storage order): adopt staged uploads, copy borrowed device inputs. The copy stays on
     // st2 after the join, so its ~0.8 GB of memory traffic (10M keys) overlaps the VALU-bound reduction
     // instead of lengthening the ordering stage that the reduction waits for; the call's final sync
@@ -1247,6 +1288,10 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_join, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_wait, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_fixed, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_kc, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_a, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipStreamCreateWithFlags(&t->st3, hipStreamNonBlocking);
         if (e2 != hipSuccess) {
             mkv_tree_destroy(t);
             throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
@@ -1262,9 +1307,15 @@ void mkv_tree_destroy(mkv_tree *t) {
     (void)hipSetDevice(t->dev);
     if (t->st2) (void)hipStreamSynchronize(t->st2);
     if (t->st) (void)hipStreamSynchronize(t->st);
+    if (t->st3) (void)hipStreamSynchronize(t->st3);
     if (t->ev_in) (void)hipEventDestroy(t->ev_in);
     if (t->ev_join) (void)hipEventDestroy(t->ev_join);
     if (t->ev_wait) (void)hipEventDestroy(t->ev_wait);
+    if (t->ev_fixed) (void)hipEventDestroy(t->ev_fixed);
+    if (t->ev_kc) (void)hipEventDestroy(t->ev_kc);
+    if (t->ev_a) (void)hipEventDestroy(t->ev_a);
+    t->a_ev.reset();
+    if (t->st3) (void)hipStreamDestroy(t->st3);
     if (t->st2) (void)hipStreamDestroy(t->st2);
     for (auto &p : t->evpool) {
         (void)hipEventDestroy(p.a);
@@ -1373,8 +1424,18 @@ static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t
                                   bool *ko_fused) {
     *kcap = !staged && t->kb.p && (reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? t->kb.cap : 0;
     *ko_fused = !staged && t->koff.p && t->koff.cap >= (n + 1) * 8;
-    const KeyOut KO{*kcap ? t->kb.as<uint8_t>() : nullptr, *ko_fused ? t->koff.as<uint64_t>() : nullptr, *kcap};
-    launch_leaf_hash(kb, koff, vb, voff, n, dig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n)), t->st, KO);
+    KeyOut KO{*kcap ? t->kb.as<uint8_t>() : nullptr, *ko_fused ? t->koff.as<uint64_t>() : nullptr, *kcap};
+    if ((reinterpret_cast<uintptr_t>(kb) & 15) != 0) KO.kdst = nullptr;  // copies keep the source offsets
+    uint32_t *ctr = ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n));
+    launch_leaf_fixed(kb, koff, vb, voff, n, dig, ctr, t->st, KO);
+    if (KO.kdst && n) {  // the ragged chunks' key bytes: on st3 beside the ragged hash, joined into st2
+        MKV_HIP(hipEventRecord(t->ev_fixed, t->st));
+        MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_fixed, 0));
+        launch_keycopy_ragged(kb, koff, n, ctr, KO.kdst, KO.kcap, t->st3);
+        MKV_HIP(hipEventRecord(t->ev_kc, t->st3));
+        t->kc_pending = true;
+    }
+    launch_leaf_ragged(kb, koff, vb, voff, n, dig, ctr, t->st, KO);
 }
 
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,
@@ -2436,6 +2497,51 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
     return l;
 }
 
+// The batched diff's key list (configs[4]: one list for every replica of the 1-vs-k walk): keys gathered
+// on st as in keylist_from_refs, then the device -> pinned copy (PCIe-bound: ~28 MB for 7 x 125K keys)
+// runs on st3 and the call returns without waiting for it; mkv_keylist_get waits when the bytes are
+// first read. The caller's next work (the next step's updates) overlaps the copy.
+static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A,
+                                            const DiffSide &B) {
+    auto *l = new mkv_keylist();
+    try {
+        if (m) {
+            if (t->a_ev) MKV_HIP(hipStreamWaitEvent(t->st, t->a_ev->e, 0));  // the last copy read a_out*
+            size_t pk = prof_begin(t, "diff");
+            uint64_t *lens = ens<uint64_t>(t->a_lens, m + 1);
+            uint64_t *off = ens<uint64_t>(t->a_outoff, m + 1);
+            void *scr = t->d_diffscr.ensure(scan_scratch_bytes(m + 1));
+            launch_diff_keylens(refs, m, A, B, lens, t->st);
+            exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
+            prof_end(t, pk);
+            small_d2h(t, t->h_small, off + m, 8, t->st);
+            wait_stream(t, t->st);
+            const uint64_t bytes = t->h_small[0];
+            uint8_t *ob = ens<uint8_t>(t->a_out, bytes + 16);
+            launch_diff_keys(refs, m, A, B, off, ob, t->st);
+            l->n = m;
+            const uint64_t kpos = (8 * (m + 1) + 15) & ~uint64_t(15);
+            l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
+            MKV_HIP(hipEventRecord(t->ev_a, t->st));
+            MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_a, 0));
+            const size_t ph = prof_begin(t, "d2h", t->st3);
+            copy_to_host(off, l->blk->dp, (m + 1) * 8, t->st3, 64);
+            copy_to_host(ob, l->blk->dp + kpos, bytes, t->st3, 64);
+            prof_end(t, ph);
+            auto ev = std::make_shared<KeyEvent>();
+            MKV_HIP(hipEventRecord(ev->e, t->st3));
+            l->ready = ev;
+            t->a_ev = ev;
+            l->offsets = reinterpret_cast<const uint64_t *>(l->blk->p);
+            l->bytes = l->blk->p + kpos;
+        }
+    } catch (...) {
+        delete l;
+        throw;
+    }
+    return l;
+}
+
 static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     mkv_tree *t = const_cast<mkv_tree *>(a);
     t->walk_L = 0;  // td_cnt is about to hold a pair walk's counters: no batched-walk stats any more
@@ -2580,7 +2686,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
         small_d2h(t, hb, nbad, 2 * k * 4, t->st);
     }
-    mkv_keylist *all = keylist_from_refs(t, refs, m, A, A);  // syncs: hb is valid after this
+    mkv_keylist *all = keylist_from_refs_async(t, refs, m, A, A);  // waits for st: hb is valid after this
     // segment starts -> per-variant counts (variants appear in ascending order)
     std::vector<uint64_t> cntv(k, 0);
     if (m) {
@@ -2598,6 +2704,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
             auto *l = new mkv_keylist();  // a view into the shared block
             if (c) {
                 l->blk = all->blk;
+                l->ready = all->ready;
                 l->bytes = all->bytes;
                 l->offsets = all->offsets + at;
                 l->n = c;
@@ -2606,6 +2713,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         }
         at += c;
     }
+    all->ready.reset();  // the views wait for the copy; the shared block lives on in them
     delete all;
     return true;
 }
@@ -2814,6 +2922,7 @@ mkv_status mkv_keylist_get(const mkv_keylist *l, uint64_t *n, const uint8_t **by
     MKV_TRY({
         NEED(l && n, "null argument");
         *n = l->n;
+        if (bytes || offsets) const_cast<mkv_keylist *>(l)->wait();  // a list still being copied out
         if (bytes) *bytes = l->bytes;
         if (offsets) *offsets = l->offsets;
     });
@@ -3232,6 +3341,7 @@ mkv_status mkv_prof_reset(mkv_tree *t) {
 mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms, uint64_t *count) {
     MKV_TRY({
         NEED(t && group && total_ms && count, "null argument");
+        sync(const_cast<mkv_tree *>(t));  // collect event pairs of work still in flight (async copies)
         auto it = t->pg.find(group);
         *total_ms = it == t->pg.end() ? 0.0 : it->second.first;
         *count = it == t->pg.end() ? 0 : it->second.second;

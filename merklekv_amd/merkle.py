@@ -77,29 +77,41 @@ def _keylist_packed(handle) -> tuple[np.ndarray, np.ndarray]:
 
 class KeyList:
     """Zero-copy view of a library-owned key list (pinned host memory written by the device): .raw is
-    the key bytes, .offs the offsets rebased to 0 (n+1). The list is freed with this object."""
+    the key bytes, .offs the offsets rebased to 0 (n+1). The list is freed with this object. len() is
+    available at once; .raw / .offs wait for the list's copy into host memory if it is still in flight
+    (mkv_tree_diff_many returns before that copy ends)."""
 
     def __init__(self, handle):
         self._h = handle
         n = C.c_uint64()
+        check(lib().mkv_keylist_get(handle, C.byref(n), None, None))
+        self.n = n.value
+        self._raw = None
+        self._offs = None
+        if self.n == 0:
+            self._raw, self._offs = np.zeros(0, np.uint8), np.zeros(1, np.uint64)
+
+    def _views(self):
+        n = C.c_uint64()
         bp = C.c_void_p()
         op = C.c_void_p()
-        check(lib().mkv_keylist_get(handle, C.byref(n), C.byref(bp), C.byref(op)))
-        self.n = n.value
-        if self.n == 0:
-            self.raw, self._offs = np.zeros(0, np.uint8), np.zeros(1, np.uint64)
-            return
+        check(lib().mkv_keylist_get(self._h, C.byref(n), C.byref(bp), C.byref(op)))
         offs = np.ctypeslib.as_array(C.cast(op, C.POINTER(C.c_uint64)), shape=(self.n + 1,))
         o0, o1 = int(offs[0]), int(offs[-1])
-        self.raw = np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(o1,))[o0:]
-        self._offs_lib, self._o0 = offs, o0
-        self._offs = offs if o0 == 0 else None
+        self._raw = np.ctypeslib.as_array(C.cast(bp, C.POINTER(C.c_uint8)), shape=(o1,))[o0:]
+        self._offs = offs if o0 == 0 else offs - np.uint64(o0)
+
+    @property
+    def raw(self) -> np.ndarray:
+        if self._raw is None:
+            self._views()
+        return self._raw
 
     @property
     def offs(self) -> np.ndarray:
         """Offsets rebased to 0 (a list sharing one block with other lists is rebased on first use)."""
         if self._offs is None:
-            self._offs = self._offs_lib - np.uint64(self._o0)
+            self._views()
         return self._offs
 
     def __len__(self):
