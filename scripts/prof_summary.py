@@ -17,8 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "gpurun_out", "prof")
 # the kernels of one merge-join diff (k_diff.hip launch_diff_merge); key gathers excluded (output side)
-MERGE_KERNELS = ("k_diff_partition", "k_diff_partition_fine", "k_diff_pass1", "k_widen_u32", "k_diff_pass2",
-                 "k_diff_verify")
+MERGE_KERNELS = ("k_diff_partition", "k_diff_pass1", "k_diff_pass2")  # round 4: verify folded into pass 2
 OUT = os.path.join(ROOT, "profiles")
 
 
