@@ -913,18 +913,26 @@ def wl_incremental(ctx, args):
         out = base_line(ctx, args, "Incremental anti-entropy: update keys/s (dirty-path rehash + 8-replica diff)",
                         total_updates * args.steps / el, "keys/s", el / args.steps * 1e3, wl)
         climb_bytes = 96 * rehashed  # per rehashed node: both children read (64 B) + the node written (32 B)
+        try:  # PMC of the same workload (scripts/gpu_prof.sh BENCH_ARGS="--workload incremental")
+            pmc_inc = json.load(open(os.path.join(ROOT, "profiles", "pmc_incremental.json")))
+        except (OSError, ValueError):
+            pmc_inc = {}
+        pmc_ok = pmc_inc.get("tree_keys") == N and pmc_inc.get("replicas") == R and pmc_inc.get("batch") == m
         comp = 2 * rehashed          # one full + one constant-schedule compression per node
         out["roofline"] = {
             "bound": "hbm", "kernel": "dirty climb (k_dirty_level x levels + k_dirty_top), all replicas",
             "achieved": climb_bytes / (climb_ms * 1e-3) / 1e9 if climb_ms else None, "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": climb_bytes / (climb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if climb_ms else None,
-            "traffic": None, "bytes_per_rehashed_node": 96, "rehashed_nodes_per_step": rehashed,
+            "traffic": pmc_inc.get("climb_hbm_bytes_per_step") if pmc_ok else None,
+            "traffic_source": pmc_inc.get("source") if pmc_ok else None,
+            "bytes_per_rehashed_node": 96, "rehashed_nodes_per_step": rehashed,
             "changed_leaves_per_step": changed, "climb_ms_per_step": climb_ms,
             "valu": {"compressions_per_step": comp, "lane_ops_model": comp * 1376,
                      "frac_of_78.6T": comp * 1376 / (climb_ms * 1e-3) / (VALU_PEAK_TOPS * 1e12) if climb_ms else None,
                      "note": "1,376 VALU lane-ops per compression (measured on the leaf kernel, PMC)"},
             "walk": {"ms_per_step": walk_ms, "ms_per_pair": walk_ms / (R - 1), "entries": ws["entries"],
                      "bytes_compared": ws["bytes"], "bytes_per_pair": ws["bytes"] / (R - 1),
+                     "traffic": pmc_inc.get("walk_hbm_bytes_per_step") if pmc_ok else None,
                      "gb_per_s": ws["bytes"] / (walk_ms * 1e-3) / 1e9 if walk_ms else None,
                      "launches": ws["launches"], "divergent_positions": ws["divergent_positions"]},
             "note": "achieved = 96 B x rehashed nodes (read back from the trees) / HIP-event time of the climb "
