@@ -1291,7 +1291,15 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_fixed, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_kc, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_a, hipEventDisableTiming);
-        if (e2 == hipSuccess) e2 = hipStreamCreateWithFlags(&t->st3, hipStreamNonBlocking);
+        if (e2 == hipSuccess) {
+            // copy stream at the lowest priority: HIP keeps one pool of hardware queues per priority
+            // (GPU_MAX_HW_QUEUES each) and multiplexes streams onto them, so this puts the asynchronous
+            // key-list copies (and the ragged key copy) on queues no tree's st / st2 shares — work queued
+            // behind a copy on a shared queue waited for it (configs[4]: the next update, 0.65 ms)
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            e2 = hipStreamCreateWithPriority(&t->st3, hipStreamNonBlocking, lo);
+        }
         if (e2 != hipSuccess) {
             mkv_tree_destroy(t);
             throw Error(ST_EHIP, std::string("tree resources: ") + hipGetErrorString(e2));
@@ -1731,8 +1739,15 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             // hash of all batches, one sort of (tree, position) keys, then per-tree scatters. One launch
             // chain per tree on its own stream serialised on the device's few hardware queues (~1.06 ms
             // for 7 replicas at 125K keys each).
-            for (size_t q = 1; q < g.size(); ++q) {  // any earlier work on the other trees' streams first
+            // any earlier work on the other trees' streams first. Only a busy stream gets the event: HIP
+            // multiplexes every stream onto a few hardware queues (GPU_MAX_HW_QUEUES, 4), so a marker on an
+            // idle tree's stream can sit behind unrelated work sharing its queue — e.g. another tree's
+            // asynchronous key-list copy, which then held the whole update back (configs[4]: 0.65 ms).
+            for (size_t q = 1; q < g.size(); ++q) {
                 mkv_tree *t = ts[g[q]];
+                const hipError_t e = hipStreamQuery(t->st);
+                if (e == hipSuccess) continue;
+                if (e != hipErrorNotReady) MKV_HIP(e);
                 MKV_HIP(hipEventRecord(t->ev_in, t->st));
                 MKV_HIP(hipStreamWaitEvent(st, t->ev_in, 0));
             }
@@ -2525,8 +2540,10 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
             MKV_HIP(hipEventRecord(t->ev_a, t->st));
             MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_a, 0));
             const size_t ph = prof_begin(t, "d2h", t->st3);
-            copy_to_host(off, l->blk->dp, (m + 1) * 8, t->st3, 64);
-            copy_to_host(ob, l->blk->dp + kpos, bytes, t->st3, 64);
+            // DMA engine, not a copy kernel: beside the next update, a kernel's PCIe writes into pinned
+            // memory slowed the update's random-read locate 2x (configs[4] step 2.83 -> 2.37-2.43 ms)
+            MKV_HIP(hipMemcpyAsync(l->blk->p, off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st3));
+            MKV_HIP(hipMemcpyAsync(l->blk->p + kpos, ob, bytes, hipMemcpyDeviceToHost, t->st3));
             prof_end(t, ph);
             auto ev = std::make_shared<KeyEvent>();
             MKV_HIP(hipEventRecord(ev->e, t->st3));
