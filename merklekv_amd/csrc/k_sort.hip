@@ -188,15 +188,23 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
                                                        uint64_t *__restrict__ lookback, uint32_t *__restrict__ ctl,
                                                        uint32_t epoch) {
     sort_prio();
+    // The scan scratch and the tile id live in the first 260 B of the key tile (written only by the local
+    // sort, after the barrier that follows them): 56,320 B at IPT 24 = 55 KiB, so one tile fits beside
+    // three 34.25-KiB ragged-hash workgroups with 1-KiB LDS allocation granules (56,520 B did not).
     __shared__ uint64_t sk[(RS_THREADS * IPT)];
-    __shared__ uint32_t sv_full[HALF ? 1 : (RS_THREADS * IPT)];
-    uint32_t *sv = HALF ? reinterpret_cast<uint32_t *>(sk) : sv_full;
+    uint32_t *sv;
+    if constexpr (HALF) {
+        sv = reinterpret_cast<uint32_t *>(sk);
+    } else {
+        __shared__ uint32_t sv_full[RS_THREADS * IPT];
+        sv = sv_full;
+    }
     __shared__ uint32_t wcnt[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint64_t gofs[256];
-    __shared__ uint32_t scan_lds[16];
-    __shared__ uint64_t scan_lds64[16];
-    __shared__ uint32_t sbid;
+    uint32_t *scan_lds = reinterpret_cast<uint32_t *>(sk);                 // 16 words
+    uint64_t *scan_lds64 = sk + 8;                                          // 16 words
+    uint32_t &sbid = reinterpret_cast<uint32_t *>(sk + 24)[0];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (threadIdx.x == 0) sbid = atomicAdd(&ctl[0], 1u);
     for (int i = threadIdx.x; i < 1024; i += RS_THREADS) (&wcnt[0][0])[i] = 0;
