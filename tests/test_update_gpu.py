@@ -436,3 +436,39 @@ def test_clone_keyset_change_then_batched_update_and_diff_vs_oracle():
     for (raw, offs), o in zip(got, oracles):
         b, oo = raw.tobytes(), offs.tolist()
         assert [b[oo[j]:oo[j + 1]] for j in range(len(oo) - 1)] == o_orig.diff(o)
+
+
+@pytest.mark.parametrize("n,m,k", [(300_000, 140_000, 2), (40_000, 5_000, 3)])
+def test_batched_update_fixed_shape_hash_vs_oracle(n, m, k):
+    """The batched update hash (k_leaf_multi) on 32/100-B records takes the compile-time register path
+    (and, for k x m >= 2^18 records, the plain round form); one batch mixes in a 99-B value so a wave falls
+    back to the generic path mid-batch. Roots and every level equal the oracle's insert-then-rebuild."""
+    import torch
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    rng = np.random.default_rng(n + m)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    kv = kb.reshape(n, 32)
+    trees, keep, expect = [base.clone() for _ in range(k)], [], []
+    for r in range(k):
+        idx = rng.integers(0, n, size=m)
+        bk = np.ascontiguousarray(kv[idx]).reshape(-1)
+        vals = rng.integers(0, 256, size=(m, 100), dtype=np.uint8)
+        vlens = np.full(m, 100, np.uint64)
+        if r == 1:
+            vlens[m // 2] = 99  # one ragged record: its wave takes the generic path
+        bv = np.concatenate([vals[i, : int(vlens[i])] for i in range(m)]) if r == 1 else vals.reshape(-1)
+        bo = np.arange(m + 1, dtype=np.uint64) * 32
+        bvo = np.zeros(m + 1, np.uint64)
+        bvo[1:] = np.cumsum(vlens)
+        d = [torch.from_numpy(bk.copy()).cuda(), torch.from_numpy(bo.astype(np.int64)).cuda(),
+             torch.from_numpy(np.ascontiguousarray(bv)).cuda(), torch.from_numpy(bvo.astype(np.int64)).cuda()]
+        keep.append(d)
+        expect.append(o.upsert(bk, bo, np.ascontiguousarray(bv), bvo))
+    torch.cuda.synchronize()
+    MerkleTree.upsert_device_many(trees, [(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), m)
+                                          for d in keep])
+    for r in range(k):
+        assert trees[r].get_root_hash() == expect[r].root(), r
+        assert _levels(trees[r]) == _oracle_levels(expect[r]), r
