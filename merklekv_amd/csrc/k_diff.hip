@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     uint32_t total = 0;
     const uint32_t pk = diff_tile<DEFER>(A, B, c, lane, lds + (threadIdx.x >> 6) * (WTILE + 2), &total, V);
     if (lane == 0) tilecnt[t] = total;
-    packed[t * 64 + lane] = pk;
+    if (total) packed[t * 64 + lane] = pk;  // only tiles with divergent outputs are read again (pass 2)
 }
 
 // Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
@@ -577,6 +577,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 // different keys or the list overflowed (the caller then reruns without deferral).
 __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
                                                     uint64_t nt, const uint32_t *__restrict__ packed,
+                                                    const uint64_t *__restrict__ tilecnt,
                                                     const uint64_t *__restrict__ tileoff, uint64_t *__restrict__ refs,
                                                     uint32_t nb2, DeferList V, uint64_t *__restrict__ fail) {
     if (blockIdx.x >= nb2) {
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, cons
         return;
     }
     const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= nt) return;
+    if (t >= nt || tilecnt[t] == 0) return;  // wave-uniform: a tile without divergent outputs (most of them)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t pk = packed[t * 64 + lane];
     const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
@@ -948,8 +949,8 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     exclusive_scan_u64(tilecnt, tileoff, nt, count, sc, st);
     // pass 2 + (defer) the key checks in the same launch
     const uint32_t nvb = defer ? (uint32_t)std::min<uint64_t>(ceil_div(defer_cap(M), 256), 1024) : 0;
-    hipLaunchKernelGGL(k_diff_pass2, dim3(wg + nvb), dim3(256), 0, st, A, B, split, nt, packed, tileoff, refs, wg, V,
-                       count + 1);
+    hipLaunchKernelGGL(k_diff_pass2, dim3(wg + nvb), dim3(256), 0, st, A, B, split, nt, packed, tilecnt, tileoff, refs,
+                       wg, V, count + 1);
     MKV_LAUNCH_CHECK();
 }
 
