@@ -572,7 +572,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     if (total) packed[t * 64 + lane] = pk;  // only tiles with divergent outputs are read again (pass 2)
 }
 
-// Pass 2, one wave per tile: lane offsets by a wave scan of the divergent counts, then refs in merged order.
+// Pass 2, one wave per 64 tiles: lane offsets by a wave scan of the divergent counts, then refs in merged order.
 // The deferred key checks ride in the same launch (blocks from nb2 on): fail[0] = 1 if any pair holds
 // different keys or the list overflowed (the caller then reruns without deferral).
 __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, const uint64_t *__restrict__ split,
@@ -593,22 +593,31 @@ __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, cons
         }
         return;
     }
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= nt || tilecnt[t] == 0) return;  // wave-uniform: a tile without divergent outputs (most of them)
+    // one wave per 64 tiles: lane q reads tile (64 w + q)'s count, the wave then emits only the tiles
+    // with divergent outputs (~23 % at 0.1 % divergence), one after another (one workgroup per tile left
+    // ~100K mostly idle workgroups to dispatch)
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t pk = packed[t * 64 + lane];
-    const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
-    const uint32_t cnt = __popc(div);
-    uint64_t off = tileoff[t] + (wave_incl_scan<uint32_t>(cnt) - cnt);
-    if (!div) return;
-    const TileCtx c = wave_tile(A, B, split, t);
-    const uint64_t dl = (uint64_t)lane * DI;
-    uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
-    for (int s = 0; s < DI; ++s) {
-        const bool fa = (fromA >> s) & 1u;
-        const uint64_t ref = fa ? i : (j | (1ull << 63));
-        if (fa) ++i; else ++j;
-        if ((div >> s) & 1u) refs[off++] = ref;
+    const uint64_t t0 = w * 64;
+    if (t0 >= nt) return;  // wave-uniform
+    uint64_t live = __ballot(t0 + lane < nt && tilecnt[t0 + lane] != 0);
+    while (live) {
+        const uint64_t t = t0 + (uint64_t)__builtin_ctzll(live);
+        live &= live - 1;
+        const uint32_t pk = packed[t * 64 + lane];
+        const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
+        const uint32_t cnt = __popc(div);
+        uint64_t off = tileoff[t] + (wave_incl_scan<uint32_t>(cnt) - cnt);
+        if (!div) continue;
+        const TileCtx c = wave_tile(A, B, split, t);
+        const uint64_t dl = (uint64_t)lane * DI;
+        uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
+        for (int s = 0; s < DI; ++s) {
+            const bool fa = (fromA >> s) & 1u;
+            const uint64_t ref = fa ? i : (j | (1ull << 63));
+            if (fa) ++i; else ++j;
+            if ((div >> s) & 1u) refs[off++] = ref;
+        }
     }
 }
 
@@ -949,8 +958,9 @@ void launch_diff(const DiffSide &A, const DiffSide &B, void *scratch, uint64_t *
     exclusive_scan_u64(tilecnt, tileoff, nt, count, sc, st);
     // pass 2 + (defer) the key checks in the same launch
     const uint32_t nvb = defer ? (uint32_t)std::min<uint64_t>(ceil_div(defer_cap(M), 256), 1024) : 0;
-    hipLaunchKernelGGL(k_diff_pass2, dim3(wg + nvb), dim3(256), 0, st, A, B, split, nt, packed, tilecnt, tileoff, refs,
-                       wg, V, count + 1);
+    const uint32_t wg2 = (uint32_t)ceil_div(ceil_div(nt, 64), 4);  // one wave per 64 tiles
+    hipLaunchKernelGGL(k_diff_pass2, dim3(wg2 + nvb), dim3(256), 0, st, A, B, split, nt, packed, tilecnt, tileoff, refs,
+                       wg2, V, count + 1);
     MKV_LAUNCH_CHECK();
 }
 
