@@ -1,5 +1,5 @@
 """Per-level timestamps of k_reduce_top (s_memrealtime, 100 MHz) from the instrumented variant library
-(scripts/mkvariant.sh topdbg): where the top launch's time goes. Run with MKV_LIB_PATH set to it."""
+(bash scripts/mkvariant.sh topdbg scripts/variants/topdbg.py): where the top launch's time goes. Run with MKV_LIB_PATH set to it."""
 import ctypes
 import os
 import sys
