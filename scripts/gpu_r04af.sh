@@ -1,5 +1,5 @@
 #!/bin/bash
-# Two-level climb launches (k_dirty_level2): update / shard / scale tests, then configs[4] A/B vs HEAD (h7).
+# Climb variant: update / shard / scale tests, then configs[4] A/B vs HEAD (h7).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_update_gpu.py tests/test_shard_gpu.py tests/test_scale_gpu.py tests/test_antientropy_gpu.py \
