@@ -472,3 +472,35 @@ def test_batched_update_fixed_shape_hash_vs_oracle(n, m, k):
     for r in range(k):
         assert trees[r].get_root_hash() == expect[r].root(), r
         assert _levels(trees[r]) == _oracle_levels(expect[r]), r
+
+
+@pytest.mark.parametrize("n", [262_144, 262_100, 300_000])
+def test_locate_top_sample_edges_take_dirty_path(n):
+    """Value batches hitting the smallest and largest keys: the locate's LDS top sample (LOC_TOP entries at
+    a stride of the 1/64 samples) must bracket keys past its last entry (n = 262,144: 4,096 samples at
+    stride 2, the last sample beyond the top sample) — a miss there is exact (merge fallback) but leaves
+    the dirty path, so the test also checks that the dirty path ran (update_counts()[0] > 0)."""
+    import torch
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    srt = sorted(keys)
+    rng = np.random.default_rng(n)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    ks = srt[-300:] + srt[:300] + [srt[int(i)] for i in rng.integers(0, n, size=400)]
+    vs = [b"edge-%d-%d" % (n, j) for j in range(len(ks))]
+    bk, bo = pack(ks)
+    bv, bvo = pack(vs)
+    d = [torch.from_numpy(bk.copy()).cuda(), torch.from_numpy(bo.astype(np.int64)).cuda(),
+         torch.from_numpy(bv.copy()).cuda(), torch.from_numpy(bvo.astype(np.int64)).cuda()]
+    torch.cuda.synchronize()
+    exp = o.upsert(bk, bo, bv, bvo)
+    single = base.clone()
+    single.upsert_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), len(ks))
+    many = [base.clone() for _ in range(2)]
+    MerkleTree.upsert_device_many(many, [(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(),
+                                          len(ks))] * 2)
+    for t in [single] + many:
+        assert t.get_root_hash() == exp.root()
+        assert t.update_counts()[0] == len(set(ks))  # every batch key located: the dirty path ran
