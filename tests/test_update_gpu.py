@@ -504,3 +504,34 @@ def test_locate_top_sample_edges_take_dirty_path(n):
     for t in [single] + many:
         assert t.get_root_hash() == exp.root()
         assert t.update_counts()[0] == len(set(ks))  # every batch key located: the dirty path ran
+
+
+def test_value_only_diffs_take_the_topdown_walk():
+    """Equal key sets with changed values: the pair diff and the batched 1-vs-k diff must come from the
+    top-down walk (its divergent leaf count equals the result), not from the exact merge-join fallback."""
+    n = 200_000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    rng = np.random.default_rng(7)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    variants, expect = [], []
+    for r in range(3):
+        idx = sorted(set(int(i) for i in rng.integers(0, n, size=200)))
+        vs2 = list(vals)
+        for i in idx:
+            vs2[i] = b"changed-%d-%d" % (r, i)
+        bv, bvo = pack(vs2)
+        t = MerkleTree()
+        t.build((kb, ko), (bv, bvo))
+        variants.append(t)
+        expect.append(o.diff(coracle.OracleTree.build(kb, ko, bv, bvo)))
+    assert base.diff_keys_bytes(variants[0]) == expect[0]
+    ws = base.walk_stats()
+    assert ws["launches"] > 0 and ws["divergent_positions"] == len(expect[0])
+    got = base.diff_keys_many_packed(variants)
+    for (raw, offs), e in zip(got, expect):
+        assert split_blob(raw, offs) == e
+    ws = base.walk_stats()
+    assert ws["launches"] > 0 and ws["divergent_positions"] == sum(len(e) for e in expect)
