@@ -367,7 +367,9 @@ __global__ __launch_bounds__(DIRTY_TOP_THREADS) void k_dirty_top(LevelPlan P, in
             uint32_t q;
             if (dirty_step<true>(D, list[cur][e], nodes, bm, &q)) list[cur ^ 1][atomicAdd(&ncnt[cur ^ 1], 1u)] = q;
         }
-        __threadfence();  // parents' digests and bits visible to every wave of the next level
+        // parents' digests and bits visible to every wave of the next level: one workgroup, one CU, so a
+        // workgroup-scope fence (its stores complete) instead of an agent-scope one
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
         if (!D.has_parent) break;
         n = ncnt[cur ^ 1];
