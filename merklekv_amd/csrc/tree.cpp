@@ -2648,13 +2648,10 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
             launch_topdown_jump_batch(na + 32 * a->lev_off[lt], V, 32 * a->lev_off[lt], a->lev_cnt[lt], kk, fin, cnt + l,
                                       fout, cnt + lt, std::min<uint64_t>(k * (a->lev_cnt[l] << kk), 1ull << 40), t->st);
             std::swap(fin, fout);
-            if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
-                const uint64_t c = d2h_u32(t, cnt + lt);
-                if (2 * c > k * a->lev_cnt[lt]) {
-                    prof_end(t, pwalk);
-                    return false;
-                }
-            }
+            // the level-4 abort test on the device (k_td_gate: frontier over half the level -> emptied,
+            // bit 31 in cnt[L + 1]), read back with the leaf count: no host round trip inside the walk
+            if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2)
+                launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)lt, k * a->lev_cnt[lt], t->st);
         }
     } else
     for (size_t l = L; l >= 1; --l) {
@@ -2675,7 +2672,9 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         }
     }
     prof_end(t, pwalk);
-    const uint64_t m = d2h_u32(t, cnt);
+    const uint32_t *hc = d2h_u32s(t, cnt, (uint32_t)L + 2);
+    if (hc[L + 1] != 0) return false;  // the gate stopped the walk: not worth finishing
+    const uint64_t m = hc[0];
     uint32_t *nbad = cnt + L + 2, *vcount = nbad + k;
     // per-variant key-check failures and segment starts come back through pinned memory with the
     // key list's own wait (a pageable readback here would hold the host until the sort finishes)
