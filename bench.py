@@ -40,9 +40,11 @@ sys.path.insert(0, ROOT)
 SEED = 0x4D65726B6C654B56
 KLEN, VLEN = 32, 100
 LEAF_BYTES = 8 + KLEN + VLEN + 32   # record model: 140-B record (k, v, 8 B of offsets) read + 32-B digest written
-# (SURVEY §8(d)). Round 4: the key-ownership copy of a build from borrowed device buffers moved out of the
-# leaf kernel into the sort's first histogram pass (which reads every key anyway), so the timed leaf kernel
-# moves exactly the record model.
+# (SURVEY §8(d)). The timed fixed-shape leaf kernel also WRITES the tree's own copy of each key and its offset
+# (key ownership of a build from borrowed device buffers, csrc/k_leaf.hip: the key words it already holds in
+# registers + koff): 40 more bytes per leaf, so it moves LEAF_BYTES_KERNEL = 212 B per leaf. `frac` keeps the
+# §8(d) record model; `frac_kernel_bytes` uses the 212 B the kernel really moves (PMC traffic ~1.24x of 172).
+LEAF_BYTES_KERNEL = LEAF_BYTES + KLEN + 8
 HBM_PEAK_GBS = 8000.0                # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 SHA_OPS_PER_LEAF = 3 * 1450          # model: 3 compressions x ~1450 VALU lane-ops
@@ -178,9 +180,13 @@ def leaf_roofline(n, leaf_avg_ms, launches):
            "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_leaf_direct",
            "bytes_per_leaf": LEAF_BYTES, "avg_launch_ms": leaf_avg_ms, "launches": launches,
            "frac_record_model": achieved / HBM_PEAK_GBS,
+           "bytes_per_leaf_kernel": LEAF_BYTES_KERNEL,
+           "frac_kernel_bytes": LEAF_BYTES_KERNEL * n / (leaf_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
            "gb_per_s_hashed": (8 + KLEN + VLEN) * n / (leaf_avg_ms * 1e-3) / 1e9,
            "note": "SHA-256 is VALU-bound (~22.7 ops/B vs 9.8 balance): the HBM frac ceiling is ~0.39; "
-                   "avg_launch_ms is measured live while the ordering kernels co-run on the aux stream"}
+                   "avg_launch_ms is measured live while the ordering kernels co-run on the aux stream; frac = "
+                   "172 B/leaf (SURVEY 8(d) record model), frac_kernel_bytes = 212 B/leaf (the kernel also stores "
+                   "the tree's 32-B key copy + 8-B offset: the PMC traffic above 172 B/leaf is that copy)"}
     pmc_path = os.path.join(ROOT, "profiles", "pmc_leaf_hash.json")
     try:
         pm = json.load(open(pmc_path))
@@ -623,6 +629,11 @@ def wl_build(ctx, args):
         torch.cuda.empty_cache()
         if args.anchor_records:
             anchor = anchor_block(ctx, args.anchor_records)
+    c4 = c3seq = None
+    if not args.no_diff and ctx.world == 1 and not args.no_big:
+        # configs[4] (125M x 8 replicas, 125K-key batches) and configs[3] (1B keys, 8 shards in sequence)
+        c4 = configs4_measure(ctx, 125_000_000, 125_000, 8, steps=10, warmup=3)
+        c3seq = configs3_sequential_block(ctx)
     c3 = None
     if not args.no_diff and ctx.dist is not None and args.anchor_records:
         c3 = sharded_anchor_block(ctx, args.anchor_records)
@@ -653,6 +664,8 @@ def wl_build(ctx, args):
         out["configs0_gpu"] = c0
         out["shared_prefix_10m"] = shared
         out["ragged_10m"] = ragged
+        out["configs4"] = c4
+        out["configs3_1b_sequential"] = c3seq
         if ctx.dist is not None:
             out["diff_sharded"] = dN
             out["collectives_build"] = coll
@@ -843,15 +856,13 @@ def wl_diff(ctx, args):
 
 
 # ====================================================================================== incremental
-def wl_incremental(ctx, args):
+def configs4_measure(ctx, n, m, R, steps, warmup):
     """configs[4]: 8 replicas (base + 7 variants) of a 1B-key tree (per-GPU shard of n keys); a step =
-    each variant applies its own value-update batch (dirty path + seam recombine) + base diffed vs all 7."""
+    each variant applies its own value-update batch (dirty path + seam recombine) + base diffed vs all 7.
+    Returns the measured dict (rank 0 fields valid on every rank)."""
     torch = ctx.torch
     from merklekv_amd import MerkleTree
     from merklekv_amd.shard import shard_recombine_many
-    n = args.n
-    m = args.batch
-    R = args.replicas
     kb, ko, vb, vo = ctx.records(n)
     base = MerkleTree(ctx.local)
     root, N = ctx.build(base, kb, ko, vb, vo, n, validate=True)
@@ -870,8 +881,8 @@ def wl_incremental(ctx, args):
                         int(torch.unique(sel).numel())))
     torch.cuda.synchronize()
 
-    # The 7 value batches go through one mkv_tree_upsert_device_many call: per-replica locate/hash/sort
-    # on each handle's own stream, then one shared dirty climb (one launch per level for all replicas).
+    # The 7 value batches go through one mkv_tree_upsert_device_many call: one locate / batch hash / sort
+    # for all replicas, then ONE k_dirty_climb launch for every replica's whole climb.
     ptrs = [(ukb.data_ptr(), uko.data_ptr(), uvb.data_ptr(), uvo.data_ptr(), m) for ukb, uko, uvb, uvo, _ in batches]
 
     def step():
@@ -880,29 +891,29 @@ def wl_incremental(ctx, args):
             shard_recombine_many(variants, ctx.dist, N, device=ctx.coll)
         return base.diff_keys_many_view(variants)  # one shared top-down walk (mkv_tree_diff_many)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         diffs = step()
     ctx.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):  # timed without the library's HIP-event pairs
+    for _ in range(steps):  # timed without the library's HIP-event pairs
         diffs = step()
     ctx.barrier()
     el = ctx.max_over_ranks(time.perf_counter() - t0)
     for t in [base] + variants:  # device-time split: the same steps with event pairs
         t.prof_enable(True)
         t.prof_reset()
-    for _ in range(args.steps):
+    for _ in range(steps):
         diffs = step()
-    upd_ms = variants[0].prof_read("update")[0] / args.steps  # one batched call: all R-1 replicas
-    diff_ms = base.prof_read("diff")[0] / (args.steps * (R - 1))  # batched walk: per-pair share
-    climb_ms = variants[0].prof_read("climb")[0] / args.steps      # shared dirty climb, all replicas
-    walk_ms = base.prof_read("walk")[0] / args.steps               # shared 1-vs-(R-1) walk launches
-    d2h_ms = base.prof_read("d2h")[0] / (args.steps * (R - 1))     # key lists into pinned host memory
+    upd_ms = variants[0].prof_read("update")[0] / steps  # one batched call: all R-1 replicas
+    diff_ms = base.prof_read("diff")[0] / (steps * (R - 1))  # batched walk: per-pair share
+    climb_ms = variants[0].prof_read("climb")[0] / steps      # the one climb launch, all replicas
+    walk_ms = base.prof_read("walk")[0] / steps               # shared 1-vs-(R-1) walk launches
+    d2h_ms = base.prof_read("d2h")[0] / (steps * (R - 1))     # key lists into pinned host memory
     for t in [base] + variants:
         t.prof_enable(False)
     # work of the last step (stats of the last update / walk; every step does the same amount)
     counts = [v.update_counts() for v in variants]
-    rehashed = sum(sum(c[1:]) for c in counts)  # internal nodes rehashed by the climb
+    rehashed = sum(sum(c[1:]) for c in counts)  # dirty internal nodes of the climb (promoted copies incl.)
     changed = sum(c[0] for c in counts if c)
     ws = base.walk_stats()
     ok = all(len(d) == b[4] for d, b in zip(diffs, batches))  # every updated key diverges, nothing else
@@ -910,47 +921,107 @@ def wl_incremental(ctx, args):
     roots = []
     if ctx.dist is None:
         roots = [t.get_root_hash().hex() for t in variants[:2]]
+    climb_bytes = 96 * rehashed  # SURVEY §8(d) model: both children read (64 B) + the node written (32 B)
+    try:  # PMC of the same workload (scripts/gpu_prof.sh BENCH_ARGS="--workload incremental")
+        pmc_inc = json.load(open(os.path.join(ROOT, "profiles", "pmc_incremental.json")))
+    except (OSError, ValueError):
+        pmc_inc = {}
+    pmc_ok = pmc_inc.get("tree_keys") == N and pmc_inc.get("replicas") == R and pmc_inc.get("batch") == m
+    comp = 2 * rehashed          # one full + one constant-schedule compression per node
+    roofline = {
+        "bound": "hbm", "kernel": "k_dirty_climb (one launch: every replica's whole climb)",
+        "achieved": climb_bytes / (climb_ms * 1e-3) / 1e9 if climb_ms else None, "peak": HBM_PEAK_GBS,
+        "unit": "GB/s", "frac": climb_bytes / (climb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if climb_ms else None,
+        "traffic": pmc_inc.get("climb_hbm_bytes_per_step") if pmc_ok else None,
+        "traffic_source": pmc_inc.get("source") if pmc_ok else None,
+        "bytes_per_rehashed_node": 96, "bytes_per_rehashed_node_kernel_min": 64,
+        "rehashed_nodes_per_step": rehashed, "changed_leaves_per_step": changed, "climb_ms_per_step": climb_ms,
+        "valu": {"compressions_per_step": comp, "lane_ops_model": comp * 1376,
+                 "frac_of_78.6T": comp * 1376 / (climb_ms * 1e-3) / (VALU_PEAK_TOPS * 1e12) if climb_ms else None,
+                 "note": "1,376 VALU lane-ops per compression (measured on the leaf kernel, PMC)"},
+        "walk": {"ms_per_step": walk_ms, "ms_per_pair": walk_ms / (R - 1), "entries": ws["entries"],
+                 "bytes_compared": ws["bytes"], "bytes_per_pair": ws["bytes"] / (R - 1),
+                 "traffic": pmc_inc.get("walk_hbm_bytes_per_step") if pmc_ok else None,
+                 "gb_per_s": ws["bytes"] / (walk_ms * 1e-3) / 1e9 if walk_ms else None,
+                 "launches": ws["launches"], "divergent_positions": ws["divergent_positions"]},
+        "note": "achieved = 96 B x rehashed nodes (SURVEY 8(d): both children + the node; read back from the trees) "
+                "/ HIP-event time of the climb launch on the group's stream. The kernel itself moves ~64 B per "
+                "rehashed node (the dirty child stays in registers; only the clean sibling is read). The climb "
+                "is 2 SHA-256 compressions per node, so VALU binds (valu.frac_of_78.6T); walk = the shared "
+                "top-down launches (digests compared in both trees) without the key gather / PCIe copy"}
+    inc = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
+           "update_device_ms_all_replicas": upd_ms, "diff_device_ms_per_pair": diff_ms,
+           "climb_device_ms": climb_ms, "walk_device_ms_per_pair": walk_ms / (R - 1),
+           "keys_d2h_ms_per_pair": d2h_ms,
+           "diff_device_ms_per_pair_excl_d2h": diff_ms - d2h_ms,
+           "diff_sizes_match_unique_updates": ok,
+           "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
+    out = {"workload": (f"configs[4]: {N} keys ({n} per rank), {R} replicas (base + {R - 1} variants), "
+                        f"{m} value updates per variant per rank; step = {R - 1} dirty-path batches + "
+                        f"1-vs-{R - 1} diff"),
+           "steps": steps, "warmup": warmup, "ms_per_step": el / steps * 1e3,
+           "update_keys_per_s": total_updates * steps / el, "roofline": roofline, "incremental": inc}
+    del base, variants, batches, kb, ko, diffs
+    torch.cuda.empty_cache()
+    return out
+
+
+def wl_incremental(ctx, args):
+    """configs[4] as its own line (value = update keys/s)."""
+    r = configs4_measure(ctx, args.n, args.batch, args.replicas, args.steps, args.warmup)
     if ctx.rank == 0:
-        wl = (f"configs[4]: {N} keys ({n} per rank), {R} replicas (base + {R - 1} variants), "
-              f"{m} value updates per variant per rank; step = {R - 1} dirty-path batches + 1-vs-{R - 1} diff")
         out = base_line(ctx, args, "Incremental anti-entropy: update keys/s (dirty-path rehash + 8-replica diff)",
-                        total_updates * args.steps / el, "keys/s", el / args.steps * 1e3, wl)
-        climb_bytes = 96 * rehashed  # per rehashed node: both children read (64 B) + the node written (32 B)
-        try:  # PMC of the same workload (scripts/gpu_prof.sh BENCH_ARGS="--workload incremental")
-            pmc_inc = json.load(open(os.path.join(ROOT, "profiles", "pmc_incremental.json")))
-        except (OSError, ValueError):
-            pmc_inc = {}
-        pmc_ok = pmc_inc.get("tree_keys") == N and pmc_inc.get("replicas") == R and pmc_inc.get("batch") == m
-        comp = 2 * rehashed          # one full + one constant-schedule compression per node
-        out["roofline"] = {
-            "bound": "hbm", "kernel": "dirty climb (k_dirty_level x levels + k_dirty_top), all replicas",
-            "achieved": climb_bytes / (climb_ms * 1e-3) / 1e9 if climb_ms else None, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": climb_bytes / (climb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if climb_ms else None,
-            "traffic": pmc_inc.get("climb_hbm_bytes_per_step") if pmc_ok else None,
-            "traffic_source": pmc_inc.get("source") if pmc_ok else None,
-            "bytes_per_rehashed_node": 96, "rehashed_nodes_per_step": rehashed,
-            "changed_leaves_per_step": changed, "climb_ms_per_step": climb_ms,
-            "valu": {"compressions_per_step": comp, "lane_ops_model": comp * 1376,
-                     "frac_of_78.6T": comp * 1376 / (climb_ms * 1e-3) / (VALU_PEAK_TOPS * 1e12) if climb_ms else None,
-                     "note": "1,376 VALU lane-ops per compression (measured on the leaf kernel, PMC)"},
-            "walk": {"ms_per_step": walk_ms, "ms_per_pair": walk_ms / (R - 1), "entries": ws["entries"],
-                     "bytes_compared": ws["bytes"], "bytes_per_pair": ws["bytes"] / (R - 1),
-                     "traffic": pmc_inc.get("walk_hbm_bytes_per_step") if pmc_ok else None,
-                     "gb_per_s": ws["bytes"] / (walk_ms * 1e-3) / 1e9 if walk_ms else None,
-                     "launches": ws["launches"], "divergent_positions": ws["divergent_positions"]},
-            "note": "achieved = 96 B x rehashed nodes (read back from the trees) / HIP-event time of the climb "
-                    "launches on the group's stream; the climb is a random gather of sibling pairs plus 2 "
-                    "compressions per node (VALU-heavy), walk = the shared top-down launches (digests compared "
-                    "in both trees) without the key gather / PCIe copy of the key lists"}
-        out["incremental"] = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
-                              "update_device_ms_all_replicas": upd_ms, "diff_device_ms_per_pair": diff_ms,
-                              "climb_device_ms": climb_ms, "walk_device_ms_per_pair": walk_ms / (R - 1),
-                              "keys_d2h_ms_per_pair": d2h_ms,
-                              "diff_device_ms_per_pair_excl_d2h": diff_ms - d2h_ms,
-                              "diff_sizes_match_unique_updates": ok,
-                              "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
+                        r["update_keys_per_s"], "keys/s", r["ms_per_step"], r["workload"])
+        out["roofline"] = r["roofline"]
+        out["incremental"] = r["incremental"]
         out["cpu_baseline"] = None if (args.no_cpu_baseline or ctx.world > 1) else cpu_baseline_update()
         emit(out)
+
+
+def configs3_sequential_block(ctx, nshards=8, per_shard=125_000_000, steps=2, warmup=1):
+    """configs[3] at its full size on ONE GPU: 1B keys = 8 key ranges x 125M records, all resident in HBM
+    (140 GB of records + offsets), the global root built shard after shard (shard.sequential_root: prepare
+    -> reduce at the shard's global offset -> fringe, then one seam combine). The 8-GPU form of the same
+    config is the N=8 line's sharded_125m_per_rank. matches_golden: the root equals the CPU oracle's
+    (tests/golden/roots_sharded.json, computed once by oracle/root_stream.c over the same records)."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.merkle import gen_records_device
+    from merklekv_amd.shard import sequential_root
+    blobs = []
+    for g in range(nshards):
+        kb = torch.empty(per_shard * KLEN + 64, dtype=torch.uint8, device=ctx.dev)
+        vb = torch.empty(per_shard * VLEN + 64, dtype=torch.uint8, device=ctx.dev)
+        ko = torch.empty(per_shard + 1, dtype=torch.int64, device=ctx.dev)
+        vo = torch.empty(per_shard + 1, dtype=torch.int64, device=ctx.dev)
+        gen_records_device(ctx.local, SEED, g * per_shard, per_shard, KLEN, VLEN, kb.data_ptr(), ko.data_ptr(),
+                           vb.data_ptr(), vo.data_ptr(), shard=g, nshards=nshards)
+        blobs.append((kb, ko, vb, vo, per_shard))
+    torch.cuda.synchronize()
+    N = nshards * per_shard
+    t = MerkleTree(ctx.local)
+    for _ in range(warmup):
+        root, counts = sequential_root(t, blobs, N)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        root, counts = sequential_root(t, blobs, N)
+    el = (time.perf_counter() - t0) / steps
+    golden = None
+    try:
+        d = json.load(open(os.path.join(ROOT, "tests", "golden", "roots_sharded.json")))
+        golden = next((c["root"] for c in d["cases"] if c["shards"] == nshards and c["per_shard"] == per_shard
+                       and c["seed"] == SEED), None)
+    except (OSError, ValueError):
+        pass
+    out = {"keys": N, "shards": nshards, "keys_per_shard": per_shard, "steps": steps,
+           "ms_per_root": el * 1e3, "leaves_per_s": N / el, "root": root.hex() if root else None,
+           "golden_root": golden, "matches_golden": (root.hex() == golden) if (root and golden) else None,
+           "note": "records resident in HBM before timing; per shard hash + sort + dedup + reduction at its "
+                   "global offset + fringe readback (<= 6 KiB), then the seam combine: 1B-key root on one GPU"}
+    del t, blobs
+    torch.cuda.empty_cache()
+    return out
 
 
 # ===================================================================================== CPU baselines
@@ -1155,6 +1226,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--no-diff", action="store_true", help="build workload: skip the secondary blocks")
+    ap.add_argument("--no-big", action="store_true", help="build workload: skip the configs4 / 1B-key blocks")
     ap.add_argument("--diff-records", type=int, default=100_000_000, help="build workload: diff_100m keys")
     ap.add_argument("--anchor-records", type=int, default=125_000_000,
                     help="build workload: the 125M-per-GPU block (N=1 anchor_125m, N>1 sharded_125m_per_rank; "

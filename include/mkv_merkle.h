@@ -182,7 +182,14 @@ mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32
  * points run the all-gathers themselves, so a host in any language (the reference's SyncManager is Rust,
  * sync.rs:56-87) needs no collective layer of its own. Two communicator forms:
  *   RCCL (xGMI): mkv_comm_unique_id on one rank, the 128 bytes shared out of band (TCP, a file, MPI),
- *     then mkv_comm_init_rank on every rank (ncclCommInitRank). Payloads stay in device memory.
+ *     then mkv_comm_init_rank on every rank (ncclCommInitRank). Payloads (boundary keys, fringes, key
+ *     lists) stay in device memory: packed, all-gathered, checked and compacted on the device; the host
+ *     reads only each operation's 32-B status / count words per rank (mkv_comm_traffic: `meta`) and a
+ *     diff's final result.
+ * Failure: every operation's first collective carries each rank's status word, and so does every later
+ * collective of it, so when one rank's local step fails (bad blob, out of memory) EVERY rank returns an
+ * error from the same call (the failing rank its own, the others that rank's code) — no rank is left
+ * waiting in a collective. (A rank that never calls the operation at all still blocks the others.)
  *   host: mkv_comm_create_host with the caller's all-gather (gloo, MPI, a test harness): fn gathers
  *     `bytes` from every rank into recv in rank order (host memory) and returns 0.
  * Replaces: the host-side count / fringe / key-list exchanges a caller had to write around
@@ -202,10 +209,17 @@ mkv_status mkv_comm_all_gather(mkv_comm *c, const void *send, void *recv, uint64
 #define MKV_COLL_COUNTS 0 /* leaf counts (8 B) */
 #define MKV_COLL_RANGE 1  /* range check: first / last key per shard */
 #define MKV_COLL_FRINGE 2 /* seam fringes (k x MKV_FRINGE_BYTES) */
-#define MKV_COLL_DIFF 3   /* divergent-key all-gather-v (meta + padded blocks) */
-#define MKV_COLL_KINDS 4
+#define MKV_COLL_DIFF 3   /* divergent keys: (count, bytes) meta + padded blocks, or the local slice's counts */
+#define MKV_COLL_USER 4   /* mkv_comm_all_gather: the caller's own bytes */
+#define MKV_COLL_KINDS 5
 mkv_status mkv_comm_stats(mkv_comm *c, double secs[MKV_COLL_KINDS], uint64_t calls[MKV_COLL_KINDS],
                           uint64_t bytes[MKV_COLL_KINDS], int reset);
+/* Host <-> device bytes moved around the collectives since creation / the last stats reset, per kind:
+ * staged = payload bytes copied between host and device to feed or read a collective (0 for the RCCL
+ * form's sharded operations; the host form's payloads are host memory by definition and not counted),
+ * meta = the status / count words the host reads back for control flow (32 B per rank per operation, plus
+ * 24-B verdicts of the device block checks). */
+mkv_status mkv_comm_traffic(const mkv_comm *c, uint64_t staged[MKV_COLL_KINDS], uint64_t meta[MKV_COLL_KINDS]);
 void mkv_comm_destroy(mkv_comm *c);
 /* Collective sharded build of this rank's records (device blobs when on_device != 0, else host blobs):
  * hash + sort + dedup, all-gather of the leaf counts, range check when range_check != 0 (every shard's
@@ -224,6 +238,13 @@ mkv_status mkv_sharded_root_many(mkv_tree *const *ts, uint32_t k, mkv_comm *c, u
  * rank — what SyncManager::sync_once consumes (sync.rs:67): local device diff, all-gather of (count,
  * bytes), all-gather of [u32 lengths | key bytes] blocks. Rank order is key order. */
 mkv_status mkv_sharded_diff(const mkv_tree *a, const mkv_tree *b, mkv_comm *c, mkv_keylist **out);
+/* This rank's slice of that global list: the sorted divergent keys of its own key range (one device ->
+ * host copy) and their position in the global list — the sum of the lower ranks' counts, from ONE 32-B
+ * all-gather ("each rank writes its compacted keys at its global offset"). A sharded apply
+ * (sync.rs:74-83 sets / deletes per key) needs only its own slice, so the host traffic of a global diff does
+ * not grow with the number of ranks. global_total (optional): the global list's length. */
+mkv_status mkv_sharded_diff_local(const mkv_tree *a, const mkv_tree *b, mkv_comm *c, mkv_keylist **out,
+                                  uint64_t *global_offset, uint64_t *global_total);
 
 /* ---------------- redistribution of unpartitioned input ----------------
  * The sharded build needs rank r to hold every key of range r. Records that sit on the ranks in no key

@@ -34,10 +34,12 @@ EXPORTS = [
     "mkv_route_sample", "mkv_route_splitters", "mkv_route_plan", "mkv_route_pack", "mkv_route_offsets",
     "mkv_comm_unique_id", "mkv_comm_init_rank", "mkv_comm_create_host", "mkv_comm_rank", "mkv_comm_destroy",
     "mkv_comm_stats", "mkv_comm_all_gather", "mkv_sharded_build", "mkv_sharded_root", "mkv_sharded_root_many", "mkv_sharded_diff",
+    "mkv_sharded_diff_local", "mkv_comm_traffic",
 ]
 
 COMM_ID_BYTES = 128
-COLL_KINDS = ["counts_all_gather", "range_all_gather", "fringe_all_gather", "diff_all_gather_v"]  # MKV_COLL_*
+COLL_KINDS = ["counts_all_gather", "range_all_gather", "fringe_all_gather", "diff_all_gather_v",
+              "user_all_gather"]  # MKV_COLL_*
 # int (*mkv_allgather_fn)(void *ctx, const void *send, void *recv, uint64_t bytes)
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
 
@@ -128,6 +130,8 @@ def lib():
         "mkv_sharded_root": ([vp, vp, vp, P(i32)], i32),
         "mkv_sharded_root_many": ([P(vp), u32, vp, vp, vp], i32),
         "mkv_sharded_diff": ([vp, vp, vp, P(vp)], i32),
+        "mkv_sharded_diff_local": ([vp, vp, vp, P(vp), P(u64), P(u64)], i32),
+        "mkv_comm_traffic": ([vp, vp, vp], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

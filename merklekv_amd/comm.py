@@ -6,7 +6,8 @@ Rust, sync.rs:56-87; it has no sharding of its own, merkle.rs:27-32). Two forms:
 
   * RCCL (`Comm.rccl`): rank 0 makes the 128-byte unique id (mkv_comm_unique_id), it is shared out of
     band (here: a broadcast over the caller's torch.distributed group), every rank calls
-    mkv_comm_init_rank on its GPU. Every payload stays in device memory, all-gathers over xGMI.
+    mkv_comm_init_rank on its GPU. Payloads stay in device memory (all-gathers over xGMI); the host reads
+    only the 32-B status / count words of each operation (`traffic()`).
   * host (`Comm.host`): the caller's all-gather of equal-size host byte payloads, as a C callback
     (here: torch.distributed over gloo — the CPU tests and several ranks sharing one GPU).
 
@@ -133,6 +134,14 @@ class Comm:
         s, k, b = (C.c_double * n)(), (C.c_uint64 * n)(), (C.c_uint64 * n)()
         check(lib().mkv_comm_stats(self._h, s, k, b, int(reset)))
         return {COLL_KINDS[i]: (s[i], k[i], b[i]) for i in range(n)}
+
+    def traffic(self) -> dict:
+        """{kind: (host-staged payload bytes, meta bytes)} since creation / the last stats reset
+        (mkv_comm_traffic: the RCCL form stages no payload bytes for the sharded operations)."""
+        n = len(COLL_KINDS)
+        s, m = (C.c_uint64 * n)(), (C.c_uint64 * n)()
+        check(lib().mkv_comm_traffic(self._h, s, m))
+        return {COLL_KINDS[i]: (s[i], m[i]) for i in range(n)}
 
     @property
     def handle(self):

@@ -1,20 +1,26 @@
 // comm.cpp — multi-GPU key-range shards behind the C ABI: a communicator (RCCL inside the
 // library, or the caller's host all-gather) and the sharded build / root / diff that run the collectives
 // themselves, so a host in any language (the reference's Rust SyncManager, sync.rs:56-87) gets the global
-// root and the one sorted divergent-key list without a collective layer of its own.
+// root and the divergent-key list without a collective layer of its own.
 //
 // RCCL is loaded at run time: the already-resident copy when there is one (a PyTorch process has its own
 // librccl loaded; two RCCL instances in one process would each bring up the devices), else
 // librccl.so.1 from ROCm, with RTLD_LOCAL so its symbols never interpose on anyone else's.
 //
-// Per sharded build (every rank): hash + sort + dedup of the rank's key range (mkv_shard_prepare), ONE
-// all-gather of the 8-B leaf counts, the shard's range check (one all-gather of its first and last key),
-// the in-shard reduction (mkv_shard_reduce), ONE all-gather of the <= 6 KiB seam fringes and the seam
-// combine on the device. With RCCL every payload stays in device memory; sizes are bytes, so the
-// collectives are latency-bound and scaling is weak and near-linear by construction.
+// Every operation starts with a META all-gather: 32 bytes per rank = {status, three words} (leaf count and
+// the shard's first / last key lengths; a diff's key count and byte count). A rank whose local step failed
+// (bad blob, out of memory, ...) still joins it with its error code, so every rank returns the error
+// together instead of waiting forever in a collective the failed rank never reaches; every later
+// collective of the operation carries the same status word in its block header. The host reads these words
+// back because it needs them for control flow (offsets, buffer sizes): counted as `meta` bytes.
+// PAYLOADS never pass through the host in the RCCL form: the range check's boundary keys, the seam fringes
+// and the diff's key lists are packed on the device, all-gathered device to device, checked and compacted
+// by kernels; the only device -> host copy of a diff is its final result. mkv_comm_traffic reports the
+// host-staged payload bytes per kind (0 for the RCCL form's sharded operations).
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -66,6 +72,116 @@ void check_nccl(ncclResult_t e, const char *what) {
     }
 }
 
+constexpr uint64_t HDR = 32;  // block header: status, three words (u64 each)
+inline uint64_t up16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// ---------------- device side of the RCCL form ----------------
+// Header words of this rank's block (kernel arguments: no host -> device copy).
+__global__ void k_put_header(uint64_t *dst, uint64_t status, uint64_t w1, uint64_t w2, uint64_t w3) {
+    if (threadIdx.x == 0) {
+        dst[0] = status;
+        dst[1] = w1;
+        dst[2] = w2;
+        dst[3] = w3;
+    }
+}
+
+// Range-check block: header {status, n, len_first, len_last}, then the first and the last key zero-padded
+// to W bytes each (keys = offsets[0..2] + bytes of the two keys at sorted positions 0 and n-1).
+__global__ void k_pack_ends(uint8_t *dst, uint64_t status, uint64_t n, const uint64_t *off, const uint8_t *kb,
+                            uint64_t W) {
+    uint64_t *h = reinterpret_cast<uint64_t *>(dst);
+    const uint64_t lf = n ? off[1] - off[0] : 0, ll = n ? off[2] - off[1] : 0;
+    if (threadIdx.x == 0) {
+        h[0] = status;
+        h[1] = n;
+        h[2] = lf;
+        h[3] = ll;
+    }
+    for (uint64_t i = threadIdx.x; i < 2 * W; i += blockDim.x) {
+        const bool second = i >= W;
+        const uint64_t j = second ? i - W : i, len = second ? ll : lf;
+        dst[HDR + i] = (n && j < len) ? kb[(second ? off[1] : off[0]) + j] : 0;
+    }
+}
+
+// Verdict over `world` gathered blocks (block r at recv + r * stride): v[0] = first rank whose header status
+// is non-zero (or ~0), v[1] = its status; ranges: v[2] = first non-empty rank whose first key is not above
+// the previous non-empty rank's last key (Rust String order: bytes, then length), or ~0. One thread: the
+// blocks are a few hundred bytes per rank.
+__global__ void k_check_blocks(const uint8_t *recv, uint64_t stride, uint32_t world, int ranges, uint64_t W,
+                               uint64_t *v) {
+    if (threadIdx.x != 0) return;
+    v[0] = ~0ull;
+    v[1] = 0;
+    v[2] = ~0ull;
+    for (uint32_t r = 0; r < world; ++r) {
+        const uint64_t st = reinterpret_cast<const uint64_t *>(recv + r * stride)[0];
+        if (st) {
+            v[0] = r;
+            v[1] = st;
+            return;
+        }
+    }
+    if (!ranges) return;
+    int64_t prev = -1;
+    for (uint32_t r = 0; r < world; ++r) {
+        const uint64_t *h = reinterpret_cast<const uint64_t *>(recv + r * stride);
+        if (!h[1]) continue;
+        if (prev >= 0) {
+            const uint64_t *hp = reinterpret_cast<const uint64_t *>(recv + (uint64_t)prev * stride);
+            const uint8_t *last = recv + (uint64_t)prev * stride + HDR + W, *first = recv + r * stride + HDR;
+            const uint64_t la = hp[3], lb = h[2], m = la < lb ? la : lb;
+            int c = 0;
+            for (uint64_t j = 0; j < m && !c; ++j) c = (int)last[j] - (int)first[j];
+            if (!c) c = la < lb ? -1 : (la > lb ? 1 : 0);
+            if (c >= 0) {
+                v[2] = r;
+                return;
+            }
+        }
+        prev = r;
+    }
+}
+
+// Diff block of this rank: header {status, n, bytes, 0}, offsets[0..n] at +HDR (mn + 1 slots), key bytes at
+// +HDR + up16(8 (mn + 1)).
+__global__ void k_pack_list(uint8_t *dst, uint64_t status, uint64_t n, uint64_t nb, const uint64_t *off, uint64_t mn) {
+    uint64_t *h = reinterpret_cast<uint64_t *>(dst);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    if (t == 0) {
+        h[0] = status;
+        h[1] = n;
+        h[2] = nb;
+        h[3] = 0;
+    }
+    uint64_t *o = reinterpret_cast<uint64_t *>(dst + HDR);
+    for (uint64_t i = t; i <= mn; i += stride) o[i] = (i <= n && off) ? off[i] : 0;
+}
+
+// Global list from the gathered blocks: rank r's keys go to the key range [K_r, K_r + n_r) and byte range
+// [B_r, B_r + nb_r), K / B = the sums over the ranks before r (read from the block headers: ranges are
+// ordered by rank, so the concatenation is the sorted, unique global list, merkle.rs:171-196).
+// grid.y = rank.
+__global__ void k_compact_lists(const uint8_t *recv, uint64_t stride, uint64_t boff, uint64_t *out_off,
+                                uint8_t *out_kb, uint64_t total_n) {
+    const uint32_t r = blockIdx.y;
+    uint64_t K = 0, B = 0;
+    for (uint32_t q = 0; q < r; ++q) {
+        const uint64_t *h = reinterpret_cast<const uint64_t *>(recv + (uint64_t)q * stride);
+        K += h[1];
+        B += h[2];
+    }
+    const uint8_t *blk = recv + (uint64_t)r * stride;
+    const uint64_t n = reinterpret_cast<const uint64_t *>(blk)[1], nb = reinterpret_cast<const uint64_t *>(blk)[2];
+    const uint64_t *off = reinterpret_cast<const uint64_t *>(blk + HDR);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = t; i < n; i += step) out_off[K + i] = B + off[i];
+    const uint8_t *kb = blk + boff;
+    for (uint64_t i = t; i < nb; i += step) out_kb[B + i] = kb[i];
+    if (r == gridDim.y - 1 && t == 0) out_off[total_n] = B + nb;
+}
+
 }  // namespace
 
 struct mkv_comm {
@@ -73,54 +189,102 @@ struct mkv_comm {
     // RCCL form
     ncclComm_t nc = nullptr;
     hipStream_t st = nullptr;
-    DevBuf din, dout;  // collective staging (device)
+    DevBuf din, dout, dres_off, dres_kb, dverdict;  // collective staging, global diff list, verdict words
+    uint64_t *h_meta = nullptr;                     // pinned: meta words (send + world x recv) and verdicts
+    uint64_t h_meta_cap = 0;
     // host form
     mkv_allgather_fn fn = nullptr;
     void *ctx = nullptr;
-    // wall time / calls / bytes per rank of each collective kind (MKV_COLL_*), host clock around the
-    // collective and the wait for its result
+    // per collective kind (MKV_COLL_*): host wall seconds around the collective and the wait for its
+    // result, calls, payload bytes per rank; host <-> device bytes moved around it (payload / meta words)
     double secs[MKV_COLL_KINDS] = {};
-    uint64_t calls[MKV_COLL_KINDS] = {}, nbytes[MKV_COLL_KINDS] = {};
+    uint64_t calls[MKV_COLL_KINDS] = {}, nbytes[MKV_COLL_KINDS] = {}, staged[MKV_COLL_KINDS] = {},
+             metab[MKV_COLL_KINDS] = {};
     int kind = MKV_COLL_COUNTS;  // kind of the collectives issued next
     bool device_form() const { return nc != nullptr; }
 
+    uint64_t *pinned(uint64_t words) {
+        if (words > h_meta_cap) {
+            if (h_meta) (void)hipHostFree(h_meta);
+            h_meta = nullptr;
+            h_meta_cap = 0;
+            MKV_HIP(hipHostMalloc(reinterpret_cast<void **>(&h_meta), words * 8 + 64, hipHostMallocDefault));
+            h_meta_cap = words;
+        }
+        return h_meta;
+    }
     // All-gather of `bytes` per rank: device pointers in the RCCL form, host pointers in the host form.
     void all_gather(const void *send, void *recv, uint64_t bytes) {
         const auto t0 = std::chrono::steady_clock::now();
-        gather(send, recv, bytes);
+        if (device_form()) {
+            check_nccl(rccl().AllGather(send, recv, bytes, ncclUint8, nc, st), "ncclAllGather");
+            MKV_HIP(hipStreamSynchronize(st));
+        } else if (fn(ctx, send, recv, bytes) != 0) {
+            throw Error(ST_EINVAL, "host all-gather callback failed");
+        }
         secs[kind] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         calls[kind] += 1;
         nbytes[kind] += bytes;
     }
-    void gather(const void *send, void *recv, uint64_t bytes) {
+    // META all-gather: {status, w1, w2, w3} of every rank (host result, rank order).
+    std::vector<uint64_t> gather_meta(uint64_t status, uint64_t w1, uint64_t w2, uint64_t w3) {
+        std::vector<uint64_t> out(4ull * world);
+        const uint64_t mine[4] = {status, w1, w2, w3};
         if (device_form()) {
-            check_nccl(rccl().AllGather(send, recv, bytes, ncclUint8, nc, st), "ncclAllGather");
+            uint8_t *a = reinterpret_cast<uint8_t *>(din.ensure(HDR));
+            uint8_t *b = reinterpret_cast<uint8_t *>(dout.ensure(HDR * world));
+            hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, st, reinterpret_cast<uint64_t *>(a), status, w1, w2,
+                               w3);
+            MKV_LAUNCH_CHECK();
+            all_gather(a, b, HDR);
+            uint64_t *h = pinned(4ull * world);
+            MKV_HIP(hipMemcpyAsync(h, b, HDR * world, hipMemcpyDeviceToHost, st));
             MKV_HIP(hipStreamSynchronize(st));
+            std::memcpy(out.data(), h, HDR * world);
+            metab[kind] += HDR * world;
         } else {
-            if (fn(ctx, send, recv, bytes) != 0) throw Error(ST_EINVAL, "host all-gather callback failed");
-        }
-    }
-    // All-gather of host bytes (any form); result on the host, rank order.
-    std::vector<uint8_t> all_gather_host(const void *send, uint64_t bytes) {
-        std::vector<uint8_t> out((size_t)bytes * world);
-        if (!bytes) return out;
-        if (device_form()) {
-            uint8_t *a = reinterpret_cast<uint8_t *>(din.ensure(bytes));
-            uint8_t *b = reinterpret_cast<uint8_t *>(dout.ensure(bytes * world));
-            MKV_HIP(hipMemcpyAsync(a, send, bytes, hipMemcpyHostToDevice, st));
-            all_gather(a, b, bytes);
-            MKV_HIP(hipMemcpyAsync(out.data(), b, bytes * world, hipMemcpyDeviceToHost, st));
-            MKV_HIP(hipStreamSynchronize(st));
-        } else {
-            all_gather(send, out.data(), bytes);
+            all_gather(mine, out.data(), HDR);
         }
         return out;
     }
-    std::vector<uint64_t> all_gather_u64(uint64_t v) {
-        const std::vector<uint8_t> raw = all_gather_host(&v, sizeof v);
-        std::vector<uint64_t> out(world);
-        std::memcpy(out.data(), raw.data(), 8ull * world);
-        return out;
+    // Every rank throws the same way when any rank's status word is non-zero: its own error when it
+    // failed itself, else the first failing rank's code.
+    void raise_if_failed(const uint64_t *statuses, uint64_t stride_words, int my_code, const std::string &my_err,
+                         const char *op) {
+        for (int r = 0; r < world; ++r) {
+            const uint64_t s = statuses[(uint64_t)r * stride_words];
+            if (!s) continue;
+            if (my_code) throw Error(my_code, my_err);
+            throw Error((int)s, std::string(op) + ": rank " + std::to_string(r) + " failed (status " +
+                                    std::to_string(s) + "); every rank returns the error");
+        }
+    }
+    // Verdict of gathered device blocks (k_check_blocks), read back as meta.
+    void check_device_blocks(const uint8_t *recv, uint64_t stride, bool ranges, uint64_t W, int my_code,
+                             const std::string &my_err, const char *op, uint64_t *order_bad) {
+        uint64_t *v = reinterpret_cast<uint64_t *>(dverdict.ensure(64));
+        hipLaunchKernelGGL(k_check_blocks, dim3(1), dim3(64), 0, st, recv, stride, (uint32_t)world, ranges ? 1 : 0, W, v);
+        MKV_LAUNCH_CHECK();
+        uint64_t *h = pinned(4);
+        MKV_HIP(hipMemcpyAsync(h, v, 24, hipMemcpyDeviceToHost, st));
+        MKV_HIP(hipStreamSynchronize(st));
+        metab[kind] += 24;
+        if (h[0] != ~0ull) {
+            if (my_code) throw Error(my_code, my_err);
+            throw Error((int)h[1], std::string(op) + ": rank " + std::to_string(h[0]) + " failed (status " +
+                                       std::to_string(h[1]) + "); every rank returns the error");
+        }
+        if (order_bad) *order_bad = h[2];
+    }
+    // Host form: all-gather of host blocks whose first u64 is the status word.
+    std::vector<uint8_t> gather_host_blocks(const std::vector<uint8_t> &mine, int my_code, const std::string &my_err,
+                                            const char *op) {
+        std::vector<uint8_t> all(mine.size() * world);
+        all_gather(mine.data(), all.data(), mine.size());
+        std::vector<uint64_t> st(world);
+        for (int r = 0; r < world; ++r) std::memcpy(&st[r], all.data() + mine.size() * r, 8);
+        raise_if_failed(st.data(), 1, my_code, my_err, op);
+        return all;
     }
 };
 
@@ -143,6 +307,21 @@ void call(mkv_status s) {
     if (s != MKV_OK) throw Error(s, mkv_last_error());
 }
 
+// Runs a local step of a collective operation; a failure is recorded (code + message), not thrown, so
+// the rank still joins the operation's next collective with its status word set.
+template <class F> void local_step(int &code, std::string &err, F f) {
+    if (code) return;
+    try {
+        f();
+    } catch (const Error &e) {
+        code = e.code ? e.code : ST_EINVAL;
+        err = e.what();
+    } catch (const std::exception &e) {
+        code = ST_EINVAL;
+        err = e.what();
+    }
+}
+
 struct Guard {
     int prev = -1;
     explicit Guard(int d) {
@@ -154,7 +333,7 @@ struct Guard {
     }
 };
 
-// Keys at sorted positions 0 and n-1 of a shard (host bytes), for the range check.
+// Keys at sorted positions 0 and n-1 of a shard (host bytes), for the host form's range check.
 std::pair<std::string, std::string> shard_ends(const mkv_tree *t, uint64_t n) {
     if (!n) return {};
     const uint64_t pos[2] = {0, n - 1};
@@ -170,59 +349,109 @@ std::pair<std::string, std::string> shard_ends(const mkv_tree *t, uint64_t n) {
     return r;
 }
 
-// The seam protocol is exact only when rank r's keys all sort below rank r+1's (Rust String order =
-// bytes order): every non-empty shard's last key < the next non-empty shard's first key.
-void check_ranges(mkv_comm *c, const mkv_tree *t, const std::vector<uint64_t> &counts) {
-    const auto ends = shard_ends(t, counts[c->rank]);
-    const std::vector<uint64_t> lens0 = c->all_gather_u64(ends.first.size());
-    const std::vector<uint64_t> lens1 = c->all_gather_u64(ends.second.size());
-    uint64_t width = 1;
-    for (int r = 0; r < c->world; ++r) width = std::max({width, lens0[r], lens1[r]});
-    std::vector<uint8_t> pay(2 * width, 0);
-    std::memcpy(pay.data(), ends.first.data(), ends.first.size());
-    std::memcpy(pay.data() + width, ends.second.data(), ends.second.size());
-    const std::vector<uint8_t> all = c->all_gather_host(pay.data(), pay.size());
+[[noreturn]] void throw_range(int prev_rank, int r) {
+    throw Error(ST_EINVAL, "shard key ranges overlap or are out of rank order (rank " + std::to_string(prev_rank) +
+                               " vs rank " + std::to_string(r) +
+                               "): the seam protocol needs contiguous key ranges ordered by rank");
+}
+
+// The seam protocol is exact only when rank r's keys all sort below rank r+1's (Rust String order = bytes
+// order): every non-empty shard's last key < the next non-empty shard's first key. ONE collective: each
+// rank's boundary keys padded to the widest rank's (the widths came with the counts' meta gather).
+void check_ranges(mkv_comm *c, const mkv_tree *t, const std::vector<uint64_t> &meta) {
+    c->kind = MKV_COLL_RANGE;
+    uint64_t W = 1;
+    for (int r = 0; r < c->world; ++r) W = std::max({W, meta[4 * r + 2], meta[4 * r + 3]});
+    W = up16(W);
+    const uint64_t n = meta[4 * c->rank + 1];
+    int code = 0;
+    std::string err;
+    if (c->device_form()) {
+        const uint64_t blk = HDR + 2 * W;
+        uint8_t *src = reinterpret_cast<uint8_t *>(c->din.ensure(blk));
+        uint8_t *dst = reinterpret_cast<uint8_t *>(c->dout.ensure(blk * c->world));
+        DevKeys ends;
+        local_step(code, err, [&] {
+            if (n) {
+                const uint64_t pos[2] = {0, n - 1};
+                ends = tree_keys_at_device(t, pos, 2);
+                MKV_HIP(hipStreamSynchronize(tree_stream(t)));
+            }
+        });
+        hipLaunchKernelGGL(k_pack_ends, dim3(1), dim3(256), 0, c->st, src, (uint64_t)code, code ? 0 : n, ends.off, ends.kb,
+                           W);
+        MKV_LAUNCH_CHECK();
+        c->all_gather(src, dst, blk);
+        uint64_t bad = ~0ull;
+        c->check_device_blocks(dst, blk, true, W, code, err, "sharded build (range check)", &bad);
+        if (bad != ~0ull) {
+            int prev = -1;
+            for (int r = 0; r < (int)bad; ++r)
+                if (meta[4 * r + 1]) prev = r;
+            throw_range(prev, (int)bad);
+        }
+        return;
+    }
+    std::vector<uint8_t> pay(HDR + 2 * W, 0);
+    local_step(code, err, [&] {
+        const auto ends = shard_ends(t, n);
+        std::memcpy(pay.data() + HDR, ends.first.data(), ends.first.size());
+        std::memcpy(pay.data() + HDR + W, ends.second.data(), ends.second.size());
+    });
+    const uint64_t st = (uint64_t)code;
+    std::memcpy(pay.data(), &st, 8);
+    const std::vector<uint8_t> all = c->gather_host_blocks(pay, code, err, "sharded build (range check)");
     std::string prev;
     int prev_rank = -1;
     for (int r = 0; r < c->world; ++r) {
-        if (!counts[r]) continue;
-        const uint8_t *p = all.data() + 2 * width * r;
-        const std::string first(reinterpret_cast<const char *>(p), lens0[r]);
-        const std::string last(reinterpret_cast<const char *>(p + width), lens1[r]);
-        if (prev_rank >= 0 && !(prev < first))
-            throw Error(ST_EINVAL, "shard key ranges overlap or are out of rank order (rank " +
-                                       std::to_string(prev_rank) + " vs rank " + std::to_string(r) +
-                                       "): the seam protocol needs contiguous key ranges ordered by rank");
+        if (!meta[4 * r + 1]) continue;
+        const uint8_t *p = all.data() + pay.size() * r;
+        const std::string first(reinterpret_cast<const char *>(p + HDR), meta[4 * r + 2]);
+        const std::string last(reinterpret_cast<const char *>(p + HDR + W), meta[4 * r + 3]);
+        if (prev_rank >= 0 && !(prev < first)) throw_range(prev_rank, r);
         prev = last;
         prev_rank = r;
     }
 }
 
 // Fringe all-gather + device seam combine of k trees (replicas of one key range) in ONE collective: the
-// global roots on every rank.
-void recombine(mkv_comm *c, mkv_tree *const *ts, uint32_t k, uint8_t *roots, int *has_root) {
-    const uint64_t blk = (uint64_t)k * MKV_FRINGE_BYTES;
+// global roots on every rank. Block per rank = [status header | k fringes]; a rank whose earlier step
+// failed (code != 0) sends only its status.
+void recombine(mkv_comm *c, mkv_tree *const *ts, uint32_t k, uint8_t *roots, int *has_root, int code,
+               std::string err) {
+    const uint64_t blk = HDR + (uint64_t)k * MKV_FRINGE_BYTES;
     c->kind = MKV_COLL_FRINGE;
     if (c->device_form()) {
         uint8_t *src = reinterpret_cast<uint8_t *>(c->din.ensure(blk));
         uint8_t *dst = reinterpret_cast<uint8_t *>(c->dout.ensure(blk * c->world));
-        for (uint32_t i = 0; i < k; ++i) call(mkv_shard_fringe_device(ts[i], src + (uint64_t)i * MKV_FRINGE_BYTES));
+        local_step(code, err, [&] {
+            for (uint32_t i = 0; i < k; ++i)
+                call(mkv_shard_fringe_device(ts[i], src + HDR + (uint64_t)i * MKV_FRINGE_BYTES));
+        });
+        hipLaunchKernelGGL(k_put_header, dim3(1), dim3(64), 0, c->st, reinterpret_cast<uint64_t *>(src), (uint64_t)code,
+                           (uint64_t)k, 0ull, 0ull);
+        MKV_LAUNCH_CHECK();
         c->all_gather(src, dst, blk);
+        c->check_device_blocks(dst, blk, false, 0, code, err, "sharded root (fringe all-gather)", nullptr);
         for (uint32_t i = 0; i < k; ++i)
-            call(mkv_shard_combine_device(ts[i], dst + (uint64_t)i * MKV_FRINGE_BYTES, (uint32_t)c->world, blk,
+            call(mkv_shard_combine_device(ts[i], dst + HDR + (uint64_t)i * MKV_FRINGE_BYTES, (uint32_t)c->world, blk,
                                           tree_global_n(ts[i]), roots + 32ull * i, has_root + i));
-    } else {
-        std::vector<uint8_t> fr(blk);
-        for (uint32_t i = 0; i < k; ++i) call(mkv_shard_fringe(ts[i], fr.data() + (uint64_t)i * MKV_FRINGE_BYTES));
-        const std::vector<uint8_t> all = c->all_gather_host(fr.data(), fr.size());
-        std::vector<uint8_t> mine((uint64_t)MKV_FRINGE_BYTES * c->world);
-        for (uint32_t i = 0; i < k; ++i) {
-            for (int r = 0; r < c->world; ++r)
-                std::memcpy(mine.data() + (uint64_t)r * MKV_FRINGE_BYTES, all.data() + r * blk + (uint64_t)i * MKV_FRINGE_BYTES,
-                            MKV_FRINGE_BYTES);
-            call(mkv_shard_combine(ts[i], mine.data(), (uint32_t)c->world, tree_global_n(ts[i]), roots + 32ull * i,
-                                   has_root + i));
-        }
+        return;
+    }
+    std::vector<uint8_t> fr(blk, 0);
+    local_step(code, err, [&] {
+        for (uint32_t i = 0; i < k; ++i) call(mkv_shard_fringe(ts[i], fr.data() + HDR + (uint64_t)i * MKV_FRINGE_BYTES));
+    });
+    const uint64_t st = (uint64_t)code;
+    std::memcpy(fr.data(), &st, 8);
+    const std::vector<uint8_t> all = c->gather_host_blocks(fr, code, err, "sharded root (fringe all-gather)");
+    std::vector<uint8_t> mine((uint64_t)MKV_FRINGE_BYTES * c->world);
+    for (uint32_t i = 0; i < k; ++i) {
+        for (int r = 0; r < c->world; ++r)
+            std::memcpy(mine.data() + (uint64_t)r * MKV_FRINGE_BYTES, all.data() + r * blk + HDR + (uint64_t)i * MKV_FRINGE_BYTES,
+                        MKV_FRINGE_BYTES);
+        call(mkv_shard_combine(ts[i], mine.data(), (uint32_t)c->world, tree_global_n(ts[i]), roots + 32ull * i,
+                               has_root + i));
     }
 }
 
@@ -287,13 +516,27 @@ mkv_status mkv_comm_rank(const mkv_comm *c, int *rank, int *world) {
 mkv_status mkv_comm_all_gather(mkv_comm *c, const void *send, void *recv, uint64_t bytes) {
     COMM_TRY({
         if (!c || (bytes && (!send || !recv))) throw Error(ST_EINVAL, "null argument");
-        if (c->dev >= 0) {
-            Guard g(c->dev);
-            const std::vector<uint8_t> all = c->all_gather_host(send, bytes);
-            if (bytes) std::memcpy(recv, all.data(), all.size());
-        } else if (bytes) {
-            c->all_gather(send, recv, bytes);
+        if (!bytes) return MKV_OK;
+        const int saved = c->kind;
+        c->kind = MKV_COLL_USER;  // the caller's own bytes, counted apart from the sharded operations
+        try {
+            if (c->device_form()) {
+                Guard g(c->dev);
+                uint8_t *a = reinterpret_cast<uint8_t *>(c->din.ensure(bytes));
+                uint8_t *b = reinterpret_cast<uint8_t *>(c->dout.ensure(bytes * c->world));
+                MKV_HIP(hipMemcpyAsync(a, send, bytes, hipMemcpyHostToDevice, c->st));
+                c->all_gather(a, b, bytes);
+                MKV_HIP(hipMemcpyAsync(recv, b, bytes * c->world, hipMemcpyDeviceToHost, c->st));
+                MKV_HIP(hipStreamSynchronize(c->st));
+                c->staged[MKV_COLL_USER] += bytes * (1 + c->world);  // host payloads by definition
+            } else {
+                c->all_gather(send, recv, bytes);
+            }
+        } catch (...) {
+            c->kind = saved;
+            throw;
         }
+        c->kind = saved;
     });
 }
 
@@ -305,7 +548,17 @@ mkv_status mkv_comm_stats(mkv_comm *c, double secs[MKV_COLL_KINDS], uint64_t cal
             if (secs) secs[i] = c->secs[i];
             if (calls) calls[i] = c->calls[i];
             if (bytes) bytes[i] = c->nbytes[i];
-            if (reset) c->secs[i] = 0, c->calls[i] = 0, c->nbytes[i] = 0;
+            if (reset) c->secs[i] = 0, c->calls[i] = 0, c->nbytes[i] = 0, c->staged[i] = 0, c->metab[i] = 0;
+        }
+    });
+}
+
+mkv_status mkv_comm_traffic(const mkv_comm *c, uint64_t staged[MKV_COLL_KINDS], uint64_t meta[MKV_COLL_KINDS]) {
+    COMM_TRY({
+        if (!c) throw Error(ST_EINVAL, "null argument");
+        for (int i = 0; i < MKV_COLL_KINDS; ++i) {
+            if (staged) staged[i] = c->staged[i];
+            if (meta) meta[i] = c->metab[i];
         }
     });
 }
@@ -317,8 +570,12 @@ void mkv_comm_destroy(mkv_comm *c) {
         (void)rccl().CommDestroy(c->nc);
     }
     if (c->st) (void)hipStreamDestroy(c->st);
+    if (c->h_meta) (void)hipHostFree(c->h_meta);
     c->din.release();
     c->dout.release();
+    c->dres_off.release();
+    c->dres_kb.release();
+    c->dverdict.release();
     delete c;
 }
 
@@ -327,22 +584,37 @@ mkv_status mkv_sharded_build(mkv_tree *t, mkv_comm *c, mkv_blob keys, mkv_blob v
     COMM_TRY({
         if (!t || !c) throw Error(ST_EINVAL, "null argument");
         Guard g(c->dev);
-        uint64_t n_local = 0;
-        call(mkv_shard_prepare(t, keys, values, on_device, &n_local));
+        int code = 0;
+        std::string err;
+        uint64_t n_local = 0, lf = 0, ll = 0;
+        local_step(code, err, [&] {
+            call(mkv_shard_prepare(t, keys, values, on_device, &n_local));
+            if (range_check && n_local) {  // the boundary keys' lengths ride on the count gather
+                const uint64_t pos[2] = {0, n_local - 1};
+                const DevKeys e = tree_keys_at_device(t, pos, 2);
+                uint64_t o[3] = {0, 0, 0};
+                MKV_HIP(hipMemcpyAsync(o, e.off, 24, hipMemcpyDeviceToHost, tree_stream(t)));
+                MKV_HIP(hipStreamSynchronize(tree_stream(t)));
+                lf = o[1] - o[0];
+                ll = o[2] - o[1];
+                c->metab[MKV_COLL_RANGE] += 24;
+            }
+        });
         c->kind = MKV_COLL_COUNTS;
-        const std::vector<uint64_t> counts = c->all_gather_u64(n_local);
-        c->kind = MKV_COLL_RANGE;
-        if (range_check) check_ranges(c, t, counts);
+        const std::vector<uint64_t> meta = c->gather_meta((uint64_t)code, code ? 0 : n_local, lf, ll);
+        c->raise_if_failed(meta.data(), 4, code, err, "sharded build");
+        if (range_check) check_ranges(c, t, meta);
         uint64_t offset = 0, total = 0;
         for (int r = 0; r < c->world; ++r) {
-            if (r < c->rank) offset += counts[r];
-            total += counts[r];
+            if (r < c->rank) offset += meta[4 * r + 1];
+            total += meta[4 * r + 1];
         }
-        call(mkv_shard_reduce(t, offset, total));
+        local_step(code, err, [&] { call(mkv_shard_reduce(t, offset, total)); });
         uint8_t root[32];
         int has = 0;
-        recombine(c, &t, 1, root, &has);
-        if (counts_out) std::memcpy(counts_out, counts.data(), 8ull * c->world);
+        recombine(c, &t, 1, root, &has, code, err);
+        if (counts_out)
+            for (int r = 0; r < c->world; ++r) counts_out[r] = meta[4 * r + 1];
     });
 }
 
@@ -350,7 +622,7 @@ mkv_status mkv_sharded_root(mkv_tree *t, mkv_comm *c, uint8_t out32[32], int *ha
     COMM_TRY({
         if (!t || !c || !out32 || !has_root) throw Error(ST_EINVAL, "null argument");
         Guard g(c->dev);
-        recombine(c, &t, 1, out32, has_root);
+        recombine(c, &t, 1, out32, has_root, 0, std::string());
     });
 }
 
@@ -361,7 +633,7 @@ mkv_status mkv_sharded_root_many(mkv_tree *const *ts, uint32_t k, mkv_comm *c, u
             if (!ts[i]) throw Error(ST_EINVAL, "null tree");
         if (!k) return MKV_OK;
         Guard g(c->dev);
-        recombine(c, ts, k, roots, has_root);
+        recombine(c, ts, k, roots, has_root, 0, std::string());
     });
 }
 
@@ -370,50 +642,122 @@ mkv_status mkv_sharded_diff(const mkv_tree *a, const mkv_tree *b, mkv_comm *c, m
         if (!a || !b || !c || !out) throw Error(ST_EINVAL, "null argument");
         *out = nullptr;
         Guard g(c->dev);
+        int code = 0;
+        std::string err;
+        c->kind = MKV_COLL_DIFF;
+        if (c->device_form()) {
+            // local diff left on the device -> (count, bytes) meta -> one all-gather of device blocks
+            // [header | offsets | key bytes] -> compaction kernel -> ONE device -> host copy of the result
+            DevKeys loc;
+            local_step(code, err, [&] {
+                loc = tree_diff_device(a, b);
+                MKV_HIP(hipStreamSynchronize(tree_stream(a)));
+            });
+            const std::vector<uint64_t> meta = c->gather_meta((uint64_t)code, loc.n, loc.bytes, 0);
+            c->raise_if_failed(meta.data(), 4, code, err, "sharded diff");
+            uint64_t mn = 0, mb = 0, tn = 0, tb = 0;
+            for (int r = 0; r < c->world; ++r) {
+                mn = std::max(mn, meta[4 * r + 1]);
+                mb = std::max(mb, meta[4 * r + 2]);
+                tn += meta[4 * r + 1];
+                tb += meta[4 * r + 2];
+            }
+            const uint64_t boff = up16(HDR + 8 * (mn + 1)), blk = up16(boff + mb);
+            uint8_t *src = reinterpret_cast<uint8_t *>(c->din.ensure(blk));
+            uint8_t *dst = reinterpret_cast<uint8_t *>(c->dout.ensure(blk * c->world));
+            hipLaunchKernelGGL(k_pack_list, dim3((uint32_t)std::min<uint64_t>(ceil_div(mn + 1, 256), 1024)), dim3(256), 0,
+                               c->st, src, 0ull, loc.n, loc.bytes, loc.off, mn);
+            MKV_LAUNCH_CHECK();
+            if (loc.bytes) MKV_HIP(hipMemcpyAsync(src + boff, loc.kb, loc.bytes, hipMemcpyDeviceToDevice, c->st));
+            c->all_gather(src, dst, blk);
+            uint64_t *ro = reinterpret_cast<uint64_t *>(c->dres_off.ensure(8 * (tn + 1)));
+            uint8_t *rk = reinterpret_cast<uint8_t *>(c->dres_kb.ensure(tb + 16));
+            if (tn) {
+                const uint32_t gx = (uint32_t)std::min<uint64_t>(ceil_div(std::max(mn, mb) + 1, 256 * 4), 1024);
+                hipLaunchKernelGGL(k_compact_lists, dim3(gx, (uint32_t)c->world), dim3(256), 0, c->st, dst, blk, boff, ro,
+                                   rk, tn);
+                MKV_LAUNCH_CHECK();
+            }
+            *out = keylist_from_device(ro, rk, tn, tb, c->st);
+            return MKV_OK;
+        }
+        // host form: local diff on the host, then (count, bytes) and one all-gather of padded blocks
         mkv_keylist *loc = nullptr;
-        call(mkv_tree_diff(a, b, &loc));
+        local_step(code, err, [&] { call(mkv_tree_diff(a, b, &loc)); });
         uint64_t n = 0;
         const uint8_t *kb = nullptr;
         const uint64_t *ko = nullptr;
-        mkv_keylist_get(loc, &n, &kb, &ko);
+        if (loc) mkv_keylist_get(loc, &n, &kb, &ko);
         const uint64_t nb = n ? ko[n] - ko[0] : 0;
-        // (count, bytes) of every rank, then one block per rank: [u32 lengths (padded to the largest
-        // count) | key bytes (padded to the largest byte count)]; rank order = key order (R7)
-        c->kind = MKV_COLL_DIFF;
-        const uint64_t meta[2] = {n, nb};
-        const std::vector<uint8_t> mraw = c->all_gather_host(meta, sizeof meta);
-        std::vector<uint64_t> cnt(c->world), byt(c->world);
+        std::vector<uint64_t> meta;
+        try {
+            meta = c->gather_meta((uint64_t)code, n, nb, 0);
+            c->raise_if_failed(meta.data(), 4, code, err, "sharded diff");
+        } catch (...) {
+            mkv_keylist_free(loc);
+            throw;
+        }
         uint64_t mn = 0, mb = 0, tn = 0, tb = 0;
         for (int r = 0; r < c->world; ++r) {
-            std::memcpy(&cnt[r], mraw.data() + 16 * r, 8);
-            std::memcpy(&byt[r], mraw.data() + 16 * r + 8, 8);
-            mn = std::max(mn, cnt[r]);
-            mb = std::max(mb, byt[r]);
-            tn += cnt[r];
-            tb += byt[r];
+            mn = std::max(mn, meta[4 * r + 1]);
+            mb = std::max(mb, meta[4 * r + 2]);
+            tn += meta[4 * r + 1];
+            tb += meta[4 * r + 2];
         }
-        std::vector<uint8_t> blk(4 * mn + mb, 0);
+        std::vector<uint8_t> blk(HDR + 4 * mn + mb, 0);
         for (uint64_t i = 0; i < n; ++i) {
             const uint32_t len = (uint32_t)(ko[i + 1] - ko[i]);
-            std::memcpy(blk.data() + 4 * i, &len, 4);
+            std::memcpy(blk.data() + HDR + 4 * i, &len, 4);
         }
-        if (nb) std::memcpy(blk.data() + 4 * mn, kb + ko[0], nb);
+        if (nb) std::memcpy(blk.data() + HDR + 4 * mn, kb + ko[0], nb);
         mkv_keylist_free(loc);
-        const std::vector<uint8_t> all = c->all_gather_host(blk.data(), blk.size());
+        const std::vector<uint8_t> all = c->gather_host_blocks(blk, 0, std::string(), "sharded diff");
         std::vector<uint64_t> offs(tn + 1, 0);
         std::vector<uint8_t> bytes(tb);
         uint64_t k = 0, at = 0;
         for (int r = 0; r < c->world; ++r) {
             const uint8_t *p = all.data() + blk.size() * r;
-            for (uint64_t i = 0; i < cnt[r]; ++i, ++k) {
+            for (uint64_t i = 0; i < meta[4 * r + 1]; ++i, ++k) {
                 uint32_t len;
-                std::memcpy(&len, p + 4 * i, 4);
+                std::memcpy(&len, p + HDR + 4 * i, 4);
                 offs[k + 1] = offs[k] + len;
             }
-            if (byt[r]) std::memcpy(bytes.data() + at, p + 4 * mn, byt[r]);
-            at += byt[r];
+            if (meta[4 * r + 2]) std::memcpy(bytes.data() + at, p + HDR + 4 * mn, meta[4 * r + 2]);
+            at += meta[4 * r + 2];
         }
         *out = keylist_from_host(bytes.data(), offs.data(), tn);
+    });
+}
+
+mkv_status mkv_sharded_diff_local(const mkv_tree *a, const mkv_tree *b, mkv_comm *c, mkv_keylist **out,
+                                  uint64_t *global_offset, uint64_t *global_total) {
+    COMM_TRY({
+        if (!a || !b || !c || !out || !global_offset) throw Error(ST_EINVAL, "null argument");
+        *out = nullptr;
+        Guard g(c->dev);
+        int code = 0;
+        std::string err;
+        mkv_keylist *loc = nullptr;
+        local_step(code, err, [&] { call(mkv_tree_diff(a, b, &loc)); });
+        uint64_t n = 0;
+        if (loc) mkv_keylist_get(loc, &n, nullptr, nullptr);
+        c->kind = MKV_COLL_DIFF;
+        std::vector<uint64_t> meta;
+        try {
+            meta = c->gather_meta((uint64_t)code, n, 0, 0);
+            c->raise_if_failed(meta.data(), 4, code, err, "sharded diff (local slice)");
+        } catch (...) {
+            mkv_keylist_free(loc);
+            throw;
+        }
+        uint64_t off = 0, tot = 0;
+        for (int r = 0; r < c->world; ++r) {
+            if (r < c->rank) off += meta[4 * r + 1];
+            tot += meta[4 * r + 1];
+        }
+        *global_offset = off;
+        if (global_total) *global_total = tot;
+        *out = loc;
     });
 }
 

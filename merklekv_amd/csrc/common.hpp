@@ -77,5 +77,20 @@ namespace mkv {
 mkv_keylist *keylist_from_host(const uint8_t *bytes, const uint64_t *offsets, uint64_t n);
 void set_last_error(const char *msg);
 uint64_t tree_global_n(const mkv_tree *t);
+// A key list in device memory: offsets[0..n] (offsets[0] == 0) and the key bytes (`bytes` of them).
+struct DevKeys {
+    uint64_t n = 0, bytes = 0;
+    const uint64_t *off = nullptr;
+    const uint8_t *kb = nullptr;
+};
+// diff_keys of a pair / the keys at sorted positions, left in the tree's device scratch (valid until the
+// tree's next diff or keys call); the tree's stream, device and local leaf count; one device -> pinned
+// copy of a device key list on stream st (complete on return).
+DevKeys tree_diff_device(const mkv_tree *a, const mkv_tree *b);
+DevKeys tree_keys_at_device(const mkv_tree *t, const uint64_t *pos, uint64_t m);
+hipStream_t tree_stream(const mkv_tree *t);
+int tree_device(const mkv_tree *t);
+uint64_t tree_len(const mkv_tree *t);
+mkv_keylist *keylist_from_device(const uint64_t *d_off, const uint8_t *d_kb, uint64_t n, uint64_t bytes, hipStream_t st);
 
 }  // namespace mkv

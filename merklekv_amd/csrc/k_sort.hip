@@ -436,8 +436,16 @@ __global__ __launch_bounds__(MT_THREADS) void k_mark_ties(const uint64_t *__rest
                                                          uint32_t *__restrict__ heads, uint32_t *__restrict__ zero,
                                                          uint32_t nzero) {
     sort_prio();
-    if (blockIdx.x == 0)  // the sort's histogram / control words, ready (zero) for the next sort
+    if (blockIdx.x == 0) {
+        // A pass whose look-back hit the spin limit flagged ctl[4p + 1] (words 2048 + 4p + 1) and went on with
+        // a partial prefix: fold those flags into count[7] (read back with the tie counts; the host throws)
+        // before the words are cleared for the next sort.
+        if (threadIdx.x < 8 && nzero >= 8 * 256 + 32 && zero[8 * 256 + 4 * threadIdx.x + 1])
+            atomicOr(&count[7], 1u);
+        __syncthreads();
+        // the sort's histogram / control words, ready (zero) for the next sort
         for (uint32_t i = threadIdx.x; i < nzero; i += MT_THREADS) zero[i] = 0;
+    }
     __shared__ uint32_t buf[MT_BUF];
     __shared__ uint32_t wcnt[MT_THREADS / 64];
     __shared__ uint32_t sbase;

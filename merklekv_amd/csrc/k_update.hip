@@ -8,20 +8,17 @@
 //
 //   k_locate        batch key -> sorted leaf position (binary search on the u64 prefixes, full-key
 //                   compare inside equal-prefix runs); counts keys that are not leaves (caller falls
-//                   back to the full rebuild for those batches).
-//   (radix sort of (position, batch index); stable, so the last write of a key is the last of its run)
-//   k_dirty_leaves  last write per position wins (merkle.rs:54); scatters the new leaf digests into
-//                   level 0, sets the node's dirty bit and appends it to the level's dirty list.
-//   k_dirty_level   one launch per level: every dirty node whose parent is owned hashes that parent
-//                   unless its left sibling is also dirty (the left one owns the pair), promotes it
-//                   unchanged past an odd level end (R5), marks the parent dirty and appends it. The
-//                   level-l launch also clears the level-(l-1) bits of its entries' children, so the
-//                   bitmap is all-zero again after the last level and no clearing pass is needed.
-//
-// Dirty lists are unordered (block-aggregated atomic append); the dirty bitmap (one bit per stored
-// node) is what deduplicates parents, so no per-level sort or scan is needed. Parents outside the
-// shard's owned range (sharded trees) stop the climb: their seam is recomputed by the
-// fringe all-gather + mkv_shard_combine exactly as after a full build.
+//                   back to the batch merge for those batches).
+//   (radix sort of (tree << pbits | position, batch index); stable, so the last write of a key is the
+//   last of its run)
+//   k_dirty_climb   ONE launch for the whole climb of every replica (round 5): a lane per changed leaf
+//                   writes the new leaf digest and climbs with the node's digest in registers, reading
+//                   only clean siblings from HBM; where both children are dirty the two lanes meet on the
+//                   parent's bit (write-through stores + an agent-scope fetch_or: the second arriver goes
+//                   on). Parents outside the shard's owned range (sharded trees) stop the
+//                   climb: their seam is recomputed by the fringe all-gather + mkv_shard_combine exactly as
+//                   after a full build. The rendezvous bitmap is all-zero again when the launch ends.
+
 #include "common.hpp"
 #include "dev_util.hpp"
 #include "kernels.hpp"
@@ -210,183 +207,324 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
     if ((threadIdx.x & 63) == 0 && nmiss) atomicAdd(L.missing[t], nmiss);
 }
 
-__device__ __forceinline__ void set_bit(uint32_t *bm, uint64_t b) { atomicOr(bm + (b >> 5), 1u << (b & 31)); }
-__device__ __forceinline__ void clear_bit(uint32_t *bm, uint64_t b) { atomicAnd(bm + (b >> 5), ~(1u << (b & 31))); }
-__device__ __forceinline__ bool get_bit(const uint32_t *bm, uint64_t b) {
-    return (__atomic_load_n(bm + (b >> 5), __ATOMIC_RELAXED) >> (b & 31)) & 1u;
+// ---------------------------------------------------------------------------------------------------
+// k_dirty_climb (round 5): the dirty-path rehash of k replicas, one wave per batch of 64 consecutive
+// entries, climbing level-synchronously with the batch's dirty nodes compacted in the wave's lanes.
+//
+// Entries: the batch positions sorted by (tree << pbits | leaf) — a run of equal keys is one leaf written
+// several times; its LAST entry is the last write (merkle.rs:54). Lane k of a wave holds the batch's k-th
+// dirty node (l, x) in key order: tree, the index range [lo, hi] of the entries under it with the
+// neighbouring entries pn = key[hi + 1], pp = key[lo - 1], its digest (registers) and its sibling's digest
+// read one level ahead. Per level (classify):
+//   * parent not owned (root, or a shard's seam): store the digest, done;
+//   * x is an odd level's last node: store it, the parent is the digest unchanged (R5 promotion);
+//   * sibling clean (no entry inside its leaf range: one compare of pn or pp): store the digest, parent =
+//     SHA-256(left || right) (R4) with the sibling's 32 B, read one level ahead (it lands while the
+//     previous level hashes): 32 B read + 32 B written per rehashed node, the dirty child is never re-read;
+//   * sibling dirty and held by lane k +/- 1 (the entries are sorted, so a dirty sibling's entries are the
+//     neighbouring lane's): the left lane stores and stops, the right one takes its digest across lanes
+//     (ds_bpermute) and hashes the parent — no memory round trip, no barrier;
+//   * sibling dirty beyond the batch (first / last lane only): a rendezvous with the other wave through a
+//     mailbox per entry boundary — both sides publish {digest, outer entry bound, its neighbour}
+//     write-through (sc1), drain, then fetch_or the boundary's bit at agent scope; the first arriver stops,
+//     the second clears the bit, reads the other side with sc1 loads (the hand-off form of
+//     MI355X_MICROARCH.md: sc1 payload -> vmcnt(0) -> atomic; consumer: returned atomic -> sc1 loads) and
+//     goes on. The bits are all-zero again when the launch ends.
+// After each level the survivors are compacted into the low lanes (ds_permute). A wave's lanes thin out as
+// its batch merges, so a pass stops at level `lstop` and writes its survivors (start key + digest); they are
+// compacted across waves and the next pass climbs on from them in full waves (passes: levels 0-10, 10-16,
+// 16-top for 1e8-leaf trees). Per-level dirty counts (mkv_tree_update_counts) are kept in LDS and added to
+// the trees' counters once per workgroup.
+// ---------------------------------------------------------------------------------------------------
+constexpr int CW_THREADS = 256;  // four independent waves
+constexpr uint32_t CW_MAX_BLOCKS = 1024;  // 4 waves per SIMD x 1,024 SIMDs / 4 waves per block
+
+__device__ __forceinline__ void load_raw(const uint8_t *p, uint4 &a, uint4 &b) {
+    const uint4 *q = reinterpret_cast<const uint4 *>(p);
+    a = q[0];
+    b = q[1];
+}
+__device__ __forceinline__ void raw_to_words(const uint4 &a, const uint4 &b, uint32_t w[8]) {
+    w[0] = bswap32(a.x); w[1] = bswap32(a.y); w[2] = bswap32(a.z); w[3] = bswap32(a.w);
+    w[4] = bswap32(b.x); w[5] = bswap32(b.y); w[6] = bswap32(b.z); w[7] = bswap32(b.w);
 }
 
-// Level 0: sorted (position, batch index) pairs; the last entry of each equal-position run is the last
-// write of that key. nodes0: local leaf level; bm bit index of leaf p = p (level 0 starts the bitmap).
-__device__ __forceinline__ void dirty_leaves_block(const uint64_t *__restrict__ pos, const uint32_t *__restrict__ bidx,
-                                                   uint64_t m, const uint8_t *__restrict__ bdig,
-                                                   uint8_t *__restrict__ nodes0, uint32_t *__restrict__ bm,
-                                                   uint32_t *__restrict__ list, uint32_t *__restrict__ count,
-                                                   uint64_t pmask, uint32_t *sapp) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool act = false;
-    uint32_t p = 0;
-    if (s < m) {
-        const uint64_t q = pos[s];
-        act = (s + 1 == m) || pos[s + 1] != q;
-        p = (uint32_t)(q & pmask);
-        if (act) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(bdig + 32ull * bidx[s]);
-            uint4 *dst = reinterpret_cast<uint4 *>(nodes0 + 32ull * p);
-            dst[0] = src[0];
-            dst[1] = src[1];
-            set_bit(bm, p);
+struct ClimbPlan {
+    const uint64_t *base, *cnt, *off, *S;
+    int L;
+    uint64_t goff, N;
+    int pbits;
+};
+enum : int { CL_TOP = 0, CL_PROMO = 1, CL_CLEAN = 2, CL_DIRTY = 3 };
+// What node (l, x) of tree t does at this level; sib = its sibling's node slot (the dirty test compares
+// the neighbouring entries with the sibling's leaf range).
+__device__ __forceinline__ int classify(const ClimbPlan &P, uint32_t t, int l, uint64_t x, uint64_t pn, uint64_t pp1,
+                                        uint64_t *sib) {
+    const uint64_t qg = x >> 1;
+    if (l + 1 >= P.L || !(qg >= P.base[l + 1] && qg < P.base[l + 1] + P.cnt[l + 1])) return CL_TOP;
+    if (!(x & 1) && x + 1 >= P.S[l]) return CL_PROMO;
+    const uint64_t tb = (uint64_t)t << P.pbits;
+    *sib = P.off[l] + ((x ^ 1) - P.base[l]);
+    if (!(x & 1)) {  // right sibling covers leaves [(x+1) << l, min((x+2) << l, N))
+        const uint64_t e = ((x + 2) << l) < P.N ? ((x + 2) << l) : P.N;
+        return pn < tb + (e - P.goff) ? CL_DIRTY : CL_CLEAN;
+    }
+    return pp1 > tb + (((x - 1) << l) - P.goff) ? CL_DIRTY : CL_CLEAN;  // left sibling: [(x-1) << l, x << l)
+}
+
+// Mailbox of entry boundary b (between entries b-1 and b): side 0 = the left subtree's {digest, lo, pp1},
+// side 1 = the right subtree's {digest, hi, pn}; 8-B words, written with sc1 atomic stores.
+constexpr uint64_t MBOX_SIDE_WORDS = 6, MBOX_WORDS = 2 * MBOX_SIDE_WORDS;
+
+template <bool FIRST>
+__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_dirty_climb(ClimbArgs A,
+                                                                                                      ClimbPass Q) {
+    __shared__ uint32_t s_lc[DIRTY_MAX_TREES * MKV_MAXLEV];
+    __shared__ uint8_t *s_nodes[DIRTY_MAX_TREES];
+    __shared__ uint32_t s_done;
+    // per wave: the batch's dirty nodes in key order (slot k = dirty node k), rewritten every level
+    __shared__ uint64_t s_qx[CW_THREADS / 64][64], s_qpn[CW_THREADS / 64][64], s_qpp[CW_THREADS / 64][64];
+    __shared__ uint32_t s_qlo[CW_THREADS / 64][64], s_qhi[CW_THREADS / 64][64], s_qt[CW_THREADS / 64][64];
+    __shared__ uint32_t s_qd[CW_THREADS / 64][8][64], s_qs[CW_THREADS / 64][8][64];
+    const int L = A.P.L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint64_t *q_x = s_qx[wv], *q_pn = s_qpn[wv], *q_pp = s_qpp[wv];
+    uint32_t *q_lo = s_qlo[wv], *q_hi = s_qhi[wv], *q_t = s_qt[wv];
+    uint32_t(*q_d)[64] = s_qd[wv];
+    uint32_t(*q_s)[64] = s_qs[wv];
+    __shared__ uint64_t s_base[MKV_MAXLEV], s_cnt[MKV_MAXLEV], s_off[MKV_MAXLEV], s_S[MKV_MAXLEV];
+    for (int i = tid; i < L; i += CW_THREADS) {
+        s_base[i] = A.P.base[i];
+        s_cnt[i] = A.P.cnt[i];
+        s_off[i] = A.P.off[i];
+        s_S[i] = A.P.S[i];
+    }
+    for (uint32_t i = tid; i < A.k * (uint32_t)L; i += CW_THREADS) s_lc[i] = 0;
+    __shared__ uint32_t s_miss[DIRTY_MAX_TREES];
+    __shared__ uint32_t *s_cntp[DIRTY_MAX_TREES];
+    if (tid < A.k) {
+        s_nodes[tid] = A.nodes[tid];
+        s_miss[tid] = *A.missing[tid];
+        s_cntp[tid] = A.cnt[tid];
+    }
+    if (tid == 0) s_done = 0;
+    __syncthreads();  // the only barrier: the waves work on their own batches from here on
+    const ClimbPlan P{s_base, s_cnt, s_off, s_S, L, s_base[0], s_S[0], A.pbits};
+    const uint64_t pmask = (1ull << A.pbits) - 1ull;
+    const uint32_t n = FIRST ? A.M : *Q.in_n;
+    const uint64_t *__restrict__ keys = FIRST ? A.pos : Q.in_key;
+    const uint32_t nb_cap = (uint32_t)((Q.in_cap + 63) / 64), nwaves = gridDim.x * (CW_THREADS / 64);
+    for (uint32_t bt = blockIdx.x * (CW_THREADS / 64) + (tid >> 6); bt < nb_cap; bt += nwaves) {
+        // ---- the batch's entries / survivors that climb ----
+        const uint32_t s = bt * 64 + lane;
+        bool surv = false;
+        uint32_t t = 0, lo = 0, hi = 0, have = 0;
+        uint64_t x = 0, pn = 0, pp1 = 0;
+        uint32_t d[8];
+        uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+        int l = Q.l0;
+        if (s < n) {
+            const uint64_t key = keys[s];
+            t = (uint32_t)(key >> A.pbits);
+            if (FIRST) {
+                if ((s + 1 == n || keys[s + 1] != key) && t < A.k && s_miss[t] == 0) {
+                    lo = s;
+                    while (lo > 0 && keys[lo - 1] == key) --lo;  // earlier writes of the same key
+                    load_digest(A.bdig + 32ull * A.bidx[s], d);
+                    surv = true;
+                }
+            } else {
+                lo = s;
+                const uint4 *dp = reinterpret_cast<const uint4 *>(Q.in_dig) + 2ull * s;
+                const uint4 a = dp[0], b = dp[1];
+                d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+                d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+                surv = true;
+            }
+            if (surv) {
+                hi = s;
+                pn = s + 1 < n ? keys[s + 1] : ~0ull;
+                pp1 = lo > 0 ? keys[lo - 1] + 1 : 0;
+                x = (P.goff + (key & pmask)) >> l;
+                uint64_t sib = 0;
+                if (classify(P, t, l, x, pn, pp1, &sib) == CL_CLEAN) {
+                    load_raw(s_nodes[t] + 32 * sib, n0, n1);
+                    have = 1;
+                }
+            }
         }
-    }
-    block_append<uint32_t>(act, p, list, count, sapp);
-}
-
-__global__ __launch_bounds__(256) void k_dirty_leaves(const uint64_t *__restrict__ pos,
-                                                      const uint32_t *__restrict__ bidx, uint64_t m,
-                                                      const uint8_t *__restrict__ bdig, uint8_t *__restrict__ nodes0,
-                                                      uint32_t *__restrict__ bm, uint32_t *__restrict__ list,
-                                                      uint32_t *__restrict__ count, const uint32_t *__restrict__ missing,
-                                                      uint64_t pmask) {
-    __shared__ uint32_t sapp[17];
-    if (*missing) return;  // some batch key is not a leaf: the caller takes the merge path, tree untouched
-    dirty_leaves_block(pos, bidx, m, bdig, nodes0, bm, list, count, pmask, sapp);
-}
-
-// k trees' level-0 scatters in one launch (grid.y = tree): tree q's sorted entries are
-// pos[S.base[q], S.base[q] + S.m[q]).
-__global__ __launch_bounds__(256) void k_dirty_leaves_multi(const uint64_t *__restrict__ pos,
-                                                            const uint32_t *__restrict__ bidx, DirtySegs S,
-                                                            const uint8_t *__restrict__ bdig, DirtyTrees T,
-                                                            uint64_t pmask) {
-    __shared__ uint32_t sapp[17];
-    const DirtyTree &D = T.t[blockIdx.y];
-    const uint64_t m = S.m[blockIdx.y], b = S.base[blockIdx.y];
-    if (*D.missing || (uint64_t)blockIdx.x * blockDim.x >= m) return;  // workgroup-uniform exits
-    dirty_leaves_block(pos + b, bidx + b, m, bdig, D.nodes, D.bm, D.l0, D.cnt, pmask, sapp);
-}
-
-// One dirty entry x (local index at level l): clears its children's bits, and, when its parent is owned
-// and its left sibling is not dirty (the left one owns the pair), rehashes the parent (or promotes past
-// an odd level end, R5), marks it dirty and returns true with the parent's local index in *qloc.
-// SHORT: the short-chain round form (latency-bound fused top); the per-level launches are throughput-bound
-// and take the plain form (fewer instructions).
-template <bool SHORT>
-__device__ __forceinline__ bool dirty_step(const DirtyLevel &L, uint64_t x, uint8_t *nodes, uint32_t *bm,
-                                           uint32_t *qloc) {
-    const uint64_t xg = L.a + x;
-    // children of this entry at level l-1: their bits are no longer read by anyone
-    if (L.has_child) {
-        const uint64_t c0 = 2 * xg - L.a_child;
-        if (c0 < L.c_child) clear_bit(bm, L.off_child + c0);
-        if (c0 + 1 < L.c_child) clear_bit(bm, L.off_child + c0 + 1);
-    }
-    const uint64_t qg = xg >> 1;
-    const bool owned = L.has_parent && qg >= L.a_par && qg < L.a_par + L.c_par;
-    if (!owned) {
-        clear_bit(bm, L.off + x);  // top of the local climb (root, or a seam parent)
-        return false;
-    }
-    if ((xg & 1) && get_bit(bm, L.off + x - 1)) return false;
-    const uint64_t lg = 2 * qg;  // left child (global); owned because the parent is
-    const uint8_t *lp = nodes + 32 * (L.off + (lg - L.a));
-    uint32_t lw[8], ow[8];
-    load_digest(lp, lw);
-    if (lg + 1 < L.S) {
-        uint32_t rw[8];
-        load_digest(lp + 32, rw);
-        sha_node<SHORT>(lw, rw, ow);
-    } else {
+        for (;; ++l) {
+            // ---- compaction: survivor k -> slot k / lane k (key order kept), through the wave's LDS ----
+            const uint64_t m = __ballot(surv);
+            const uint32_t c = (uint32_t)__popcll(m);
+            if (c == 0) {
+                if (Q.out_cnt && lane == 0) Q.out_cnt[bt] = 0;
+                break;
+            }
+            if (surv) {
+                const uint32_t k = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                q_x[k] = x;
+                q_pn[k] = pn;
+                q_pp[k] = pp1;
+                q_lo[k] = lo;
+                q_hi[k] = hi;
+                q_t[k] = t | (have << 31);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) ow[q] = lw[q];  // R5 promotion
-    }
-    *qloc = (uint32_t)(qg - L.a_par);
-    store_digest(nodes + 32 * (L.off_par + *qloc), ow);
-    set_bit(bm, L.off_par + *qloc);
-    return true;
-}
-
-__global__ __launch_bounds__(256) void k_dirty_level(DirtyLevel L, int l, DirtyTrees T) {
-    __shared__ uint32_t sapp[17];
-    const DirtyTree &D = T.t[blockIdx.y];
-    if (*D.missing) return;
-    const uint32_t *lin = (l & 1) ? D.l1 : D.l0;
-    uint32_t *lout = (l & 1) ? D.l0 : D.l1;
-    const uint32_t cnt = D.cnt[l];
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if ((uint64_t)blockIdx.x * blockDim.x >= cnt) return;  // whole workgroup idle (wave-uniform exit)
-    bool act = false;
-    uint32_t qloc = 0;
-    if (i < cnt) act = dirty_step<false>(L, lin[i], D.nodes, D.bm, &qloc);
-    block_append<uint32_t>(act, qloc, lout, D.cnt + l + 1, sapp);
-}
-
-__device__ __forceinline__ DirtyLevel level_of(const LevelPlan &P, int l) {
-    DirtyLevel D{};
-    D.a = P.base[l];
-    D.c = P.cnt[l];
-    D.off = P.off[l];
-    D.S = P.S[l];
-    D.has_parent = l + 1 < P.L && P.cnt[l + 1] > 0;
-    if (D.has_parent) {
-        D.a_par = P.base[l + 1];
-        D.c_par = P.cnt[l + 1];
-        D.off_par = P.off[l + 1];
-    }
-    D.has_child = l > 0 && !P.keep_bits;
-    if (l > 0) {
-        D.a_child = P.base[l - 1];
-        D.c_child = P.cnt[l - 1];
-        D.off_child = P.off[l - 1];
-    }
-    return D;
-}
-
-// All levels from l0 up in one workgroup, once a level's dirty set fits DIRTY_TOP_CAP (it never grows
-// going up): the dirty lists live in LDS, levels are separated by a device-scope fence + barrier instead
-// of a kernel boundary. Replaces the ~13 latency-bound single-workgroup launches at the top of a 1e8-leaf
-// tree, and every launch above level 0 for batches of at most DIRTY_TOP_CAP keys.
-__global__ __launch_bounds__(DIRTY_TOP_THREADS) void k_dirty_top(LevelPlan P, int l0, DirtyTrees T) {
-    const DirtyTree &Dt = T.t[blockIdx.x];  // one workgroup per tree
-    uint8_t *nodes = Dt.nodes;
-    uint32_t *bm = Dt.bm;
-    const uint32_t *lin = (l0 & 1) ? Dt.l1 : Dt.l0;
-    const uint32_t *nin = Dt.cnt + l0;
-    const uint32_t *missing = Dt.missing;
-    __shared__ uint32_t list[2][DIRTY_TOP_CAP];
-    __shared__ uint32_t ncnt[2];
-    if (*missing) return;
-    uint32_t n = *nin;
-    if (n > DIRTY_TOP_CAP) n = DIRTY_TOP_CAP;  // cannot happen: the host bounds the level's dirty count
-    for (uint32_t e = threadIdx.x; e < n; e += DIRTY_TOP_THREADS) list[0][e] = lin[e];
-    if (threadIdx.x == 0) ncnt[1] = 0;
-    __syncthreads();
-    int cur = 0;
-    for (int l = l0; l < P.L; ++l) {
-        const DirtyLevel D = level_of(P, l);
-        for (uint32_t e = threadIdx.x; e < n; e += DIRTY_TOP_THREADS) {
-            uint32_t q;
-            if (dirty_step<true>(D, list[cur][e], nodes, bm, &q)) list[cur ^ 1][atomicAdd(&ncnt[cur ^ 1], 1u)] = q;
+                for (int i = 0; i < 8; ++i) q_d[i][k] = d[i];
+                q_s[0][k] = n0.x; q_s[1][k] = n0.y; q_s[2][k] = n0.z; q_s[3][k] = n0.w;
+                q_s[4][k] = n1.x; q_s[5][k] = n1.y; q_s[6][k] = n1.z; q_s[7][k] = n1.w;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const bool act = lane < c;
+            if (act) {
+                x = q_x[lane];
+                pn = q_pn[lane];
+                pp1 = q_pp[lane];
+                lo = q_lo[lane];
+                hi = q_hi[lane];
+                const uint32_t tq = q_t[lane];
+                t = tq & 0x7FFFFFFFu;
+                have = tq >> 31;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) d[i] = q_d[i][lane];
+            }
+            if (l == Q.lstop) {  // hand the batch's dirty nodes at this level to the next pass
+                if (act) {
+                    Q.out_key[bt * 64ull + lane] = ((uint64_t)t << A.pbits) | ((x << l) - P.goff);
+                    uint4 *dp = reinterpret_cast<uint4 *>(Q.out_dig) + 2ull * (bt * 64ull + lane);
+                    dp[0] = make_uint4(d[0], d[1], d[2], d[3]);
+                    dp[1] = make_uint4(d[4], d[5], d[6], d[7]);
+                }
+                if (lane == 0) Q.out_cnt[bt] = c;
+                break;
+            }
+            // ---- this level: lane k holds dirty node k ----
+            uint64_t sib = 0;
+            const int cls = act ? classify(P, t, l, x, pn, pp1, &sib) : CL_TOP;
+            surv = false;
+            bool hash = false;
+            uint32_t sg[8];
+            if (act) {
+                uint8_t *np = s_nodes[t] + 32 * (P.off[l] + (x - P.base[l]));
+                atomicAdd(&s_lc[t * L + l], 1u);  // node (l, x) is dirty: stored below in every branch
+                if (cls == CL_TOP) {
+                    store_digest(np, d);
+                } else if (cls == CL_PROMO) {
+                    store_digest(np, d);
+                    surv = true;
+                } else if (cls == CL_CLEAN) {
+                    if (have) {
+                        const uint4 a = make_uint4(q_s[0][lane], q_s[1][lane], q_s[2][lane], q_s[3][lane]);
+                        const uint4 b = make_uint4(q_s[4][lane], q_s[5][lane], q_s[6][lane], q_s[7][lane]);
+                        raw_to_words(a, b, sg);
+                    }
+                    else load_digest(s_nodes[t] + 32 * sib, sg);  // (not expected: read one level ahead)
+                    store_digest(np, d);
+                    hash = surv = true;
+                } else if ((x & 1) && lane > 0) {  // right sibling of lane - 1, which stops: merge here
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) sg[i] = q_d[i][lane - 1];
+                    lo = q_lo[lane - 1];
+                    pp1 = q_pp[lane - 1];
+                    store_digest(np, d);
+                    hash = surv = true;
+                } else if (!(x & 1) && lane + 1 < c) {
+                    store_digest(np, d);  // left sibling of lane + 1, which goes on
+                } else {
+                    // the sibling's entries belong to another batch: rendezvous at entry boundary b
+                    const bool right = x & 1;
+                    const uint64_t b = right ? lo : (uint64_t)hi + 1;
+                    store_digest(np, d);
+                    uint64_t *mb = reinterpret_cast<uint64_t *>(Q.mbox) + b * MBOX_WORDS;
+                    uint64_t *mine = mb + (right ? MBOX_SIDE_WORDS : 0), *other = mb + (right ? 0 : MBOX_SIDE_WORDS);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        __hip_atomic_store(mine + i, ((uint64_t)d[2 * i + 1] << 32) | d[2 * i], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(mine + 4, right ? (uint64_t)hi : (uint64_t)lo, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(mine + 5, right ? pn : pp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    uint32_t *bw = Q.bflags + (b >> 5);
+                    const uint32_t bit = 1u << (b & 31);
+                    const uint32_t old = __hip_atomic_fetch_or(bw, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (old & bit) {  // second arriver: the other side's data is complete
+                        __hip_atomic_fetch_and(bw, ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the atomic
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint64_t v = __hip_atomic_load(other + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            sg[2 * i] = (uint32_t)v;
+                            sg[2 * i + 1] = (uint32_t)(v >> 32);
+                        }
+                        const uint64_t oi = __hip_atomic_load(other + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t ok = __hip_atomic_load(other + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (right) {
+                            lo = (uint32_t)oi;
+                            pp1 = ok;
+                        } else {
+                            hi = (uint32_t)oi;
+                            pn = ok;
+                        }
+                        hash = surv = true;
+                    }
+                }
+                // the parent's clean sibling, read now: it lands while this level hashes
+                have = 0;
+                if (surv) {
+                    uint64_t sib2 = 0;
+                    if (l + 1 != Q.lstop && classify(P, t, l + 1, x >> 1, pn, pp1, &sib2) == CL_CLEAN) {
+                        load_raw(s_nodes[t] + 32 * sib2, n0, n1);
+                        have = 1;
+                    }
+                }
+                if (hash) {
+                    const bool right = x & 1;
+                    uint32_t lw[8], rw[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        lw[i] = right ? sg[i] : d[i];
+                        rw[i] = right ? d[i] : sg[i];
+                    }
+                    sha_node<false>(lw, rw, d);
+                }
+                if (surv) x >>= 1;
+            }
+            __builtin_amdgcn_wave_barrier();  // this level's slot reads come before the next level's writes
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
-        // parents' digests and bits visible to every wave of the next level: one workgroup, one CU, so a
-        // workgroup-scope fence (its stores complete) instead of an agent-scope one
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __syncthreads();
-        if (!D.has_parent) break;
-        n = ncnt[cur ^ 1];
-        cur ^= 1;
-        __syncthreads();
-        if (threadIdx.x == 0) ncnt[cur ^ 1] = 0;
-        __syncthreads();
+    }
+    // ---- level counts: the last wave of the workgroup adds them to the trees' counters ----
+    uint32_t done = 0;
+    if (lane == 0) done = atomicAdd(&s_done, 1u);
+    done = __builtin_amdgcn_readfirstlane(done);
+    if (done == CW_THREADS / 64 - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (uint32_t i = lane; i < A.k * (uint32_t)L; i += 64) {
+            const uint32_t v = __hip_atomic_load(&s_lc[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (v) atomicAdd(s_cntp[i / L] + i % L, v);
+        }
     }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Batch merge (key-set changes): the tree's sorted leaves A and a sorted unique batch B
-// (last write per key already chosen, tombstones flagged) merged into the new sorted leaf set. An A
-// leaf survives unless B's cursor holds the same key (replaced or removed, merkle.rs:52-62); a B
-// record survives unless it is a remove. Same merge-path tiling as the diff (k_diff.hip): one binary
-// search per 2048-output tile, 8 outputs per lane, two passes around a scan of the kept counts.
-// ---------------------------------------------------------------------------------------------
+// Survivors of a pass, batch by batch (count per batch, records at batch * 64 + r), packed in order:
+// record j of batch b goes to off[b] + j (off = exclusive scan of the counts). One wave per batch.
+__global__ __launch_bounds__(256) void k_climb_pack(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ off,
+                                                    uint32_t nb, const uint64_t *__restrict__ key,
+                                                    const uint32_t *__restrict__ dig, uint64_t *__restrict__ okey,
+                                                    uint32_t *__restrict__ odig) {
+    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= nb || lane >= cnt[b]) return;
+    const uint64_t i = b * 64ull + lane, o = off[b] + lane;
+    okey[o] = key[i];
+    const uint4 *s = reinterpret_cast<const uint4 *>(dig) + 2 * i;
+    uint4 *d = reinterpret_cast<uint4 *>(odig) + 2 * o;
+    d[0] = s[0];
+    d[1] = s[1];
+}
+
+
 constexpr int UM_THREADS = 256, UM_ITEMS = 8, UM_TILE = UM_THREADS * UM_ITEMS;
 
 __device__ __forceinline__ int cmp_sides(const DiffSide &A, uint64_t i, const DiffSide &B, uint64_t j) {
@@ -538,23 +676,6 @@ void launch_locate_samples(const uint64_t *pfx, uint64_t n, uint64_t *ps, hipStr
     MKV_LAUNCH_CHECK();
 }
 
-void launch_dirty_leaves_multi(const uint64_t *pos, const uint32_t *bidx, const DirtySegs &S, uint64_t mmax,
-                               const uint8_t *bdig, const DirtyTrees &T, uint32_t k, hipStream_t st, uint64_t pmask) {
-    if (!mmax || !k) return;
-    hipLaunchKernelGGL(k_dirty_leaves_multi, dim3((uint32_t)ceil_div(mmax, 256), k), dim3(256), 0, st, pos, bidx, S,
-                       bdig, T, pmask);
-    MKV_LAUNCH_CHECK();
-}
-
-void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
-                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st,
-                         uint64_t pmask) {
-    if (!m) return;
-    hipLaunchKernelGGL(k_dirty_leaves, grid1d(m), dim3(256), 0, st, pos, bidx, m, bdig, nodes0, bm, list, count,
-                       missing, pmask);
-    MKV_LAUNCH_CHECK();
-}
-
 void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
                          uint64_t *pos, uint32_t *idx, hipStream_t st) {
     if (!k || !mmax) return;
@@ -563,16 +684,22 @@ void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k,
     MKV_LAUNCH_CHECK();
 }
 
-void launch_dirty_level(const DirtyLevel &L, int l, uint64_t max_entries, const DirtyTrees &T, uint32_t k,
-                        hipStream_t st) {
-    if (!max_entries || !k) return;
-    hipLaunchKernelGGL(k_dirty_level, dim3((uint32_t)ceil_div(max_entries, 256), k), dim3(256), 0, st, L, l, T);
+uint32_t climb_grid(uint64_t m) {
+    return (uint32_t)std::min<uint64_t>(ceil_div(ceil_div(m ? m : 1, 64), CW_THREADS / 64), CW_MAX_BLOCKS);
+}
+size_t climb_mbox_bytes(uint64_t m) { return (m + 2) * MBOX_WORDS * 8; }
+
+void launch_dirty_climb_pass(const ClimbArgs &A, const ClimbPass &Q, bool first, hipStream_t st) {
+    if (!A.M || !A.k || !Q.in_cap) return;
+    const uint32_t g = climb_grid(Q.in_cap);
+    if (first) hipLaunchKernelGGL(k_dirty_climb<true>, dim3(g), dim3(CW_THREADS), 0, st, A, Q);
+    else hipLaunchKernelGGL(k_dirty_climb<false>, dim3(g), dim3(CW_THREADS), 0, st, A, Q);
     MKV_LAUNCH_CHECK();
 }
-
-void launch_dirty_top(const LevelPlan &P, int l0, const DirtyTrees &T, uint32_t k, hipStream_t st) {
-    if (!k) return;
-    hipLaunchKernelGGL(k_dirty_top, dim3(k), dim3(DIRTY_TOP_THREADS), 0, st, P, l0, T);
+void launch_climb_pack(const uint32_t *cnt, const uint32_t *off, uint32_t nb, const uint64_t *key, const uint32_t *dig,
+                       uint64_t *okey, uint32_t *odig, hipStream_t st) {
+    if (!nb) return;
+    hipLaunchKernelGGL(k_climb_pack, dim3((uint32_t)ceil_div(nb, 4)), dim3(256), 0, st, cnt, off, nb, key, dig, okey, odig);
     MKV_LAUNCH_CHECK();
 }
 

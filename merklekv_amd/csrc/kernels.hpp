@@ -283,52 +283,51 @@ struct LocateMulti {
 };
 void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
                          uint64_t *pos, uint32_t *idx, hipStream_t st);
-// (pos, bidx) sorted by pos (stable): scatter the last write per position into level 0, mark dirty.
-// Positions are pos & pmask (multi-tree sort keys carry the tree above the position bits).
-void launch_dirty_leaves(const uint64_t *pos, const uint32_t *bidx, uint64_t m, const uint8_t *bdig, uint8_t *nodes0,
-                         uint32_t *bm, uint32_t *list, uint32_t *count, const uint32_t *missing, hipStream_t st,
-                         uint64_t pmask = ~0ull);
-// Level l of the local plan: owned global range [a, a+c) stored at node offset off, global size S;
-// parent level (l+1) and child level (l-1) ranges for ownership tests and bit clearing.
-struct DirtyLevel {
-    uint64_t a, c, off, S;
-    uint64_t a_par, c_par, off_par;
-    uint64_t a_child, c_child, off_child;
-    int has_parent, has_child;
-};
-// One tree of a batched climb: its nodes, bitmap, the two dirty-list buffers (level l reads l0 when l is
-// even, l1 when odd), the per-level counts and the device missing-key count (non-zero: do nothing).
-struct DirtyTree {
-    uint8_t *nodes;
-    uint32_t *bm;
-    uint32_t *l0, *l1;
-    uint32_t *cnt;
-    const uint32_t *missing;
-};
 constexpr int DIRTY_MAX_TREES = 16;
-struct DirtyTrees {
-    DirtyTree t[DIRTY_MAX_TREES];
-};
-// Sorted (tree, position) entries of k trees: tree q's run starts at base[q] and holds m[q] entries.
-struct DirtySegs {
-    uint64_t base[DIRTY_MAX_TREES], m[DIRTY_MAX_TREES];
-};
-void launch_dirty_leaves_multi(const uint64_t *pos, const uint32_t *bidx, const DirtySegs &S, uint64_t mmax,
-                               const uint8_t *bdig, const DirtyTrees &T, uint32_t k, hipStream_t st, uint64_t pmask);
-// Level l of k trees sharing the level plan (grid.y = tree).
-void launch_dirty_level(const DirtyLevel &L, int l, uint64_t max_entries, const DirtyTrees &T, uint32_t k,
-                        hipStream_t st);
-// Level plan of a tree handle for the fused top-level climb (k_dirty_top).
+// Level plan of a tree handle (owned global range [base, base + cnt) of a level of S nodes, stored at
+// node offset off), shared by the replicas of one batched update.
 constexpr int MKV_MAXLEV = 48;
 struct LevelPlan {
     uint64_t base[MKV_MAXLEV], cnt[MKV_MAXLEV], off[MKV_MAXLEV], S[MKV_MAXLEV];
     int L;
-    int keep_bits;  // 1: entries leave their children's dirty bits set (the caller clears the bitmap)
 };
-constexpr int DIRTY_TOP_THREADS = 1024;
-constexpr uint64_t DIRTY_TOP_CAP = 4096;  // dirty entries per level the fused climb holds in LDS
-// Levels l0 .. top in one workgroup; requires every level >= l0 to have at most DIRTY_TOP_CAP dirty entries.
-void launch_dirty_top(const LevelPlan &P, int l0, const DirtyTrees &T, uint32_t k, hipStream_t st);
+// The dirty climb of k replicas sharing a level plan (k_update.hip k_dirty_climb), in passes: pos / bidx
+// = the batch entries sorted by (tree << pbits | leaf position) with their batch indices, bdig = the batch
+// digests; cnt[q][l]: tree q's dirty nodes per level (added to; zeroed by the caller).
+struct ClimbArgs {
+    const uint64_t *pos;
+    const uint32_t *bidx;
+    const uint8_t *bdig;
+    uint32_t M;
+    int pbits;
+    uint32_t k;
+    uint8_t *nodes[DIRTY_MAX_TREES];
+    const uint32_t *missing[DIRTY_MAX_TREES];  // non-zero: a batch key of that tree is not a leaf, tree untouched
+    uint32_t *cnt[DIRTY_MAX_TREES];
+    LevelPlan P;
+};
+// One pass: inputs = the sorted batch entries (first pass) or the previous pass's packed survivors
+// (in_key = tree << pbits | first leaf, in_dig = 8 big-endian digest words, *in_n of them, at most in_cap),
+// all nodes at level l0; survivors reaching level lstop are written per 64-input batch b at b * 64 + r
+// (out_cnt[b] of them; out_* null when the pass climbs to the top). bflags: one bit per input boundary,
+// all-zero before and after; mbox: climb_mbox_bytes(in_cap) of scratch.
+struct ClimbPass {
+    const uint64_t *in_key;
+    const uint32_t *in_dig;
+    const uint32_t *in_n;
+    uint64_t in_cap;
+    int l0, lstop;
+    uint64_t *out_key;
+    uint32_t *out_dig;
+    uint32_t *out_cnt;
+    uint32_t *bflags;
+    uint8_t *mbox;
+};
+uint32_t climb_grid(uint64_t m);
+size_t climb_mbox_bytes(uint64_t m);
+void launch_dirty_climb_pass(const ClimbArgs &A, const ClimbPass &Q, bool first, hipStream_t st);
+void launch_climb_pack(const uint32_t *cnt, const uint32_t *off, uint32_t nb, const uint64_t *key, const uint32_t *dig,
+                       uint64_t *okey, uint32_t *odig, hipStream_t st);
 
 // Batch merge (k_update.hip): A = the tree's sorted leaves (dig = leaf level, indexed by position),
 // B = sorted unique batch (perm = batch storage index, dig = batch digests in storage order, tomb =

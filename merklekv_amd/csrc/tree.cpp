@@ -289,11 +289,11 @@ struct mkv_tree {
     const uint8_t *rt_kb = nullptr, *rt_vb = nullptr;
     const uint64_t *rt_koff = nullptr, *rt_voff = nullptr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
-    DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_l0, u_l1, u_cnt, u_bm;
+    DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_cnt, u_bf, u_mbox;
+    DevBuf u_ckey, u_cdig, u_ccnt, u_coff, u_pk0, u_pd0, u_pk1, u_pd1;  // dirty climb: pass outputs / packed inputs
     // batch merge (key-set changes): batch tombstones, merged prefixes / permutation / levels, count
     DevBuf u_tomb, m_pfx, m_perm, m_nodes, m_cnt;
-    uint64_t bm_bits = 0;
-    bool bm_dirty = false;
+    uint64_t bf_words = 0;  // words of u_bf known to be zero (every climb leaves them all-zero)
     uint64_t *h_small = nullptr;  // pinned host scalars (1 KB: bytes [512, 1024) = batched-walk counters)
     uint8_t *h_small_dev = nullptr;  // h_small as the device sees it (readbacks are kernel stores)
     uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
@@ -383,9 +383,10 @@ __global__ __launch_bounds__(64) void k_copy_small_many(SmallCopies C) {
 // Zero-fill of up to 32 device ranges in one launch (grid.y = range): a multi-replica update clears
 // every replica's dirty bitmap and level counters with one launch instead of one memset call each
 // (each ~10 µs of host enqueue and ~5 µs of device time, serialised).
+constexpr int ZERO_MAX_RANGES = 40;
 struct ZeroRanges {
-    uint8_t *p[32];
-    uint64_t bytes[32];
+    uint8_t *p[ZERO_MAX_RANGES];
+    uint64_t bytes[ZERO_MAX_RANGES];
 };
 __global__ __launch_bounds__(256) void k_zero_many(ZeroRanges Z) {
     uint8_t *p = Z.p[blockIdx.y];
@@ -1004,6 +1005,8 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     wait_stream(t, st);
     const uint32_t *hm = reinterpret_cast<const uint32_t *>(t->h_small);
     const uint32_t nties = n_in ? hm[0] : 0, dups = hm[4], long_runs = hm[5];
+    if (n_in > 1 && hm[7])  // a radix pass's look-back stalled past its spin limit: the order is not trustworthy
+        throw Error(ST_EHIP, "sort: a radix pass's look-back exceeded its spin limit (device stalled)");
     if (kbytes_out) *kbytes_out = n_in ? t->h_small[4] : 0;
     static const bool dbg_sort = getenv("MKV_DEBUG_SORT") != nullptr;
     if (dbg_sort)
@@ -1656,45 +1659,12 @@ static const uint64_t *locate_samples_of(mkv_tree *t, hipStream_t st, uint64_t *
     return ps;
 }
 
-// Phase 1 on the tree's own stream: locate the batch keys, hash the batch, sort by position, scatter the
-// last write per position into level 0 (level-0 dirty list in u_l0, counts in u_cnt).
-static DirtyTree dirty_prepare(mkv_tree *t, const DirtyBatch &b) {
-    const size_t L = t->lev_S.size();
-    const uint64_t nn = total_nodes(t), m = b.m;
-    hipStream_t st = t->st;
-    // bitmap: one bit per stored node, zero between calls
-    const uint64_t words = (nn + 63) / 32 + 2;
-    uint32_t *bm = ens<uint32_t>(t->u_bm, words);
-    if (t->bm_bits < nn || t->bm_dirty) {
-        MKV_HIP(hipMemsetAsync(bm, 0, words * 4, st));
-        t->bm_bits = words * 32 - 64;
-    }
-    uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);  // cnt[l]: dirty entries at level l; cnt[L+1]: missing
-    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, st));
-    uint64_t *pos = ens<uint64_t>(t->u_pos, m + 1), *pos2 = ens<uint64_t>(t->u_pos2, m + 1);
-    uint32_t *idx = ens<uint32_t>(t->u_idx, m + 1), *idx2 = ens<uint32_t>(t->u_idx2, m + 1);
-    // Keys that are not leaves are counted in cnt[L+1]; every dirty kernel checks that count on the
-    // device and does nothing when it is non-zero, so the whole climb is enqueued without a host round
-    // trip and the host reads the count once at the end (then the caller takes the merge path).
-    const uint32_t *missing = cnt + L + 1;
-    uint64_t ns = 0;
-    const uint64_t *ps = locate_samples_of(t, st, &ns);
-    launch_locate(b.kb, b.koff, m, side_of(t), ps, ns, pos, idx, cnt + L + 1, st);
-    uint8_t *bdig = ens<uint8_t>(t->u_dig, m * 32);
-    launch_leaf_hash(b.kb, b.koff, b.vb, b.voff, m, bdig, ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(m)), st);
-    void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
-    const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, m, 0, std::max(8, bits_for(t->n)), radix, st);
-    uint32_t *l0 = ens<uint32_t>(t->u_l0, m + 1), *l1 = ens<uint32_t>(t->u_l1, m + 1);
-    t->bm_dirty = true;
-    uint8_t *nodes = t->nodes.as<uint8_t>();
-    launch_dirty_leaves(sw ? pos2 : pos, sw ? idx2 : idx, m, bdig, nodes, bm, l0, cnt, missing, st);
-    return DirtyTree{nodes, bm, l0, l1, cnt, missing};
-}
-
-// k dirty-path updates at once (mkv_tree_upsert_device_many; k = 1 is mkv_tree_upsert_device): phase 1
-// runs per tree on its own stream, then trees sharing one level plan climb together — one launch per
-// level for all of them (grid.y = tree) and one fused top launch — instead of k interleaved chains of
-// small launches. ok[i] = false: tree i had a key that is not a leaf and is unchanged.
+// k dirty-path updates at once (mkv_tree_upsert_device_many; k = 1 is mkv_tree_upsert_device). Trees
+// sharing one level plan (replicas of one key set) form a group and run together on the first tree's
+// stream: one locate (grid.y = tree) beside one hash of every batch on the aux stream, one radix sort of
+// (tree << pbits | position) keys, then ONE k_dirty_climb launch for the whole climb of every tree (round 5;
+// it replaced a level-0 scatter, one launch per level and a fused top launch) and one readback of every
+// tree's missing-key count and root. ok[i] = false: tree i had a key that is not a leaf and is unchanged.
 static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_t k, bool *ok) {
     std::vector<uint32_t> act;
     for (uint32_t i = 0; i < k; ++i) {
@@ -1703,7 +1673,6 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         if (t->n > 0 && !t->prepared && bs[i].m > 0) act.push_back(i);
     }
     if (act.empty()) return;
-    // group by level plan (replicas of one key set share it); each group climbs together
     std::vector<std::vector<uint32_t>> groups;
     for (uint32_t i : act) {
         bool placed = false;
@@ -1720,6 +1689,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         DevGuard dg(t0->dev);
         hipStream_t st = t0->st;
         const size_t L = t0->lev_S.size();
+        if (L > (size_t)MKV_MAXLEV) throw Error(ST_EINVAL, "tree too deep for the dirty climb");
         std::vector<size_t> prof(g.size());
         std::vector<char> had_root(g.size()), had_pending(g.size());
         for (size_t q = 0; q < g.size(); ++q) {
@@ -1728,144 +1698,138 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             had_root[q] = t->has_root;
             had_pending[q] = t->combine_pending;
         }
-        DirtyTrees T{};
-        uint64_t mmax = 0;
+        // any earlier work on the other trees' streams first. Only a busy stream gets the event: HIP
+        // multiplexes every stream onto a few hardware queues (GPU_MAX_HW_QUEUES, 4), so a marker on an
+        // idle tree's stream can sit behind unrelated work sharing its queue — e.g. another tree's
+        // asynchronous key-list copy, which then held the whole update back (configs[4]: 0.65 ms).
+        for (size_t q = 1; q < g.size(); ++q) {
+            mkv_tree *t = ts[g[q]];
+            const hipError_t e = hipStreamQuery(t->st);
+            if (e == hipSuccess) continue;
+            if (e != hipErrorNotReady) MKV_HIP(e);
+            MKV_HIP(hipEventRecord(t->ev_in, t->st));
+            MKV_HIP(hipStreamWaitEvent(st, t->ev_in, 0));
+        }
         const uint32_t k2 = (uint32_t)g.size();
-        if (k2 == 1) {
-            T.t[0] = dirty_prepare(t0, bs[g[0]]);
-            mmax = bs[g[0]].m;
-        } else {
-            // Phase 1 of all k2 trees in single launches on st (round 2): one locate (grid.y = tree), one
-            // hash of all batches, one sort of (tree, position) keys, then per-tree scatters. One launch
-            // chain per tree on its own stream serialised on the device's few hardware queues (~1.06 ms
-            // for 7 replicas at 125K keys each).
-            // any earlier work on the other trees' streams first. Only a busy stream gets the event: HIP
-            // multiplexes every stream onto a few hardware queues (GPU_MAX_HW_QUEUES, 4), so a marker on an
-            // idle tree's stream can sit behind unrelated work sharing its queue — e.g. another tree's
-            // asynchronous key-list copy, which then held the whole update back (configs[4]: 0.65 ms).
-            for (size_t q = 1; q < g.size(); ++q) {
-                mkv_tree *t = ts[g[q]];
-                const hipError_t e = hipStreamQuery(t->st);
-                if (e == hipSuccess) continue;
-                if (e != hipErrorNotReady) MKV_HIP(e);
-                MKV_HIP(hipEventRecord(t->ev_in, t->st));
-                MKV_HIP(hipStreamWaitEvent(st, t->ev_in, 0));
-            }
-            LeafBatches B{};
-            LocateMulti LM{};
-            static_assert(2 * DIRTY_MAX_TREES <= 32, "ZeroRanges holds two ranges per tree");
-            ZeroRanges Z{};
-            uint32_t nz = 0;
-            uint64_t M = 0;
-            for (size_t q = 0; q < g.size(); ++q) {
-                mkv_tree *t = ts[g[q]];
-                const DirtyBatch &b = bs[g[q]];
-                B.kb[q] = b.kb;
-                B.koff[q] = b.koff;
-                B.vb[q] = b.vb;
-                B.voff[q] = b.voff;
-                B.m[q] = b.m;
-                B.base[q] = M;
-                M += b.m;
-                mmax = std::max(mmax, b.m);
-                const uint64_t nn = total_nodes(t);
-                const uint64_t words = (nn + 63) / 32 + 2;
-                uint32_t *bm = ens<uint32_t>(t->u_bm, words);
-                if (t->bm_bits < nn || t->bm_dirty) {
-                    Z.p[nz] = reinterpret_cast<uint8_t *>(bm);
-                    Z.bytes[nz++] = words * 4;
-                    t->bm_bits = words * 32 - 64;
-                }
-                uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);
-                Z.p[nz] = reinterpret_cast<uint8_t *>(cnt);
-                Z.bytes[nz++] = (L + 2) * 4;
-                uint32_t *l0 = ens<uint32_t>(t->u_l0, b.m + 1), *l1 = ens<uint32_t>(t->u_l1, b.m + 1);
-                T.t[q] = DirtyTree{t->nodes.as<uint8_t>(), bm, l0, l1, cnt, cnt + L + 1};
-                // replicas sharing t0's key-set id hold the same sorted keys, so their batches are located
-                // in t0: one tree's prefix / permutation / key arrays serve all lookups (a 1/k working set
-                // for the caches and the TLB instead of k copies of the same data)
-                mkv_tree *lt = same_keyset(t, t0) ? t0 : t;
-                LM.T[q] = side_of(lt);
-                LM.ps[q] = locate_samples_of(lt, st, &LM.ns[q]);
-                LM.missing[q] = cnt + L + 1;
-                t->bm_dirty = true;
-            }
-            launch_zero_many(Z, nz, st);
-            HTRACE("setup-queued");
-            const int pbits = bits_for(t0->n);
-            uint64_t *pos = ens<uint64_t>(t0->u_pos, M + 1), *pos2 = ens<uint64_t>(t0->u_pos2, M + 1);
-            uint32_t *idx = ens<uint32_t>(t0->u_idx, M + 1), *idx2 = ens<uint32_t>(t0->u_idx2, M + 1);
-            uint8_t *bdig = ens<uint8_t>(t0->u_dig, M * 32);
-            // the batch hash (VALU) runs beside the locate (random prefix / key reads) on the aux stream
-            MKV_HIP(hipEventRecord(t0->ev_in, st));
-            MKV_HIP(hipStreamWaitEvent(t0->st2, t0->ev_in, 0));
-            launch_leaf_hash_multi(B, k2, mmax, bdig, t0->st2);
-            MKV_HIP(hipEventRecord(t0->ev_join, t0->st2));
-            launch_locate_multi(B, LM, k2, mmax, pbits, pos, idx, st);
-            MKV_HIP(hipStreamWaitEvent(st, t0->ev_join, 0));
-            void *radix = t0->s_radix.ensure(std::max(radix_scratch_bytes(M), scan_scratch_bytes(M + 1)));
-            const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, M, 0, std::max(8, pbits + bits_for(k2 - 1)), radix, st);
-            const uint64_t *ps = sw ? pos2 : pos;
-            const uint32_t *is = sw ? idx2 : idx;
-            const uint64_t pmask = (1ull << pbits) - 1ull;
-            DirtySegs S{};
-            for (size_t q = 0; q < g.size(); ++q) {
-                S.base[q] = B.base[q];
-                S.m[q] = B.m[q];
-            }
-            launch_dirty_leaves_multi(ps, is, S, mmax, bdig, T, k2, st, pmask);
-            HTRACE("phase1-queued");
+        LeafBatches B{};
+        LocateMulti LM{};
+        ClimbArgs CA{};
+        static_assert(DIRTY_MAX_TREES + 1 <= ZERO_MAX_RANGES, "ZeroRanges: the counters of every tree + the boundary bits");
+        ZeroRanges Z{};
+        uint32_t nz = 0;
+        uint64_t M = 0, mmax = 0;
+        for (size_t q = 0; q < g.size(); ++q) {
+            mkv_tree *t = ts[g[q]];
+            const DirtyBatch &b = bs[g[q]];
+            B.kb[q] = b.kb;
+            B.koff[q] = b.koff;
+            B.vb[q] = b.vb;
+            B.voff[q] = b.voff;
+            B.m[q] = b.m;
+            B.base[q] = M;
+            M += b.m;
+            mmax = std::max(mmax, b.m);
+            uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);  // cnt[l] < L: dirty nodes per level; cnt[L+1]: missing
+            Z.p[nz] = reinterpret_cast<uint8_t *>(cnt);
+            Z.bytes[nz++] = (L + 2) * 4;
+            // replicas sharing t0's key-set id hold the same sorted keys, so their batches are located
+            // in t0: one tree's prefix / permutation / key arrays serve all lookups (a 1/k working set
+            // for the caches and the TLB instead of k copies of the same data)
+            mkv_tree *lt = same_keyset(t, t0) ? t0 : t;
+            LM.T[q] = side_of(lt);
+            LM.ps[q] = locate_samples_of(lt, st, &LM.ns[q]);
+            LM.missing[q] = cnt + L + 1;
+            CA.nodes[q] = t->nodes.as<uint8_t>();
+            CA.missing[q] = cnt + L + 1;
+            CA.cnt[q] = cnt;
         }
-        // per-level launches while a level's dirty set may exceed one workgroup's LDS lists, then the rest
-        // of the climb in one fused launch (the dirty count never exceeds min(m, level size))
-        size_t ltop = 0;
-        // The fused top runs in one workgroup per tree: a level of more than ~1K dirty nodes takes it
-        // several serial hash rounds on one CU (4,096 nodes: ~70 us), while a per-level launch spreads
-        // them over the chip; so the per-level launches continue down to 1,024
-        // entries (configs[4]: fused top 227 -> ~110 us per step).
-        constexpr uint64_t top_switch = 1024;
-        while (ltop < L && std::min<uint64_t>(mmax, t0->lev_cnt[ltop]) > top_switch) ++ltop;
-        // Large batches: entries do not clear their children's dirty bits (two device atomics per entry
-        // and level, serialised per address); the bitmap is cleared by one memset before the next update
-        // instead (nn / 8 bytes). Taken when the batches hold at least one key per 4,096 bitmap bits
-        // (configs[4]: update 2.18 -> 2.04 ms).
-        uint64_t msum = 0;
-        for (size_t q = 0; q < g.size(); ++q) msum += bs[g[q]].m;
-        const bool keep_bits = msum * 4096 >= total_nodes(t0);
-        if (L > (size_t)MKV_MAXLEV) ltop = L;  // (cannot happen below 2^47 leaves)
+        if (M >= (1ull << 32) - 2) throw Error(ST_EINVAL, "dirty path: too many batch entries");
+        // entry-boundary bits of the climb's cross-workgroup rendezvous: all-zero after every climb, so
+        // zeroed only when (re)allocated
+        const uint64_t bfw = (M + 1) / 32 + 2;
+        uint32_t *bflags = ens<uint32_t>(t0->u_bf, bfw);
+        if (t0->bf_words < bfw) {
+            Z.p[nz] = reinterpret_cast<uint8_t *>(bflags);
+            Z.bytes[nz++] = t0->u_bf.cap;
+            t0->bf_words = t0->u_bf.cap / 4;
+        }
+        launch_zero_many(Z, nz, st);
+        HTRACE("setup-queued");
+        const int pbits = bits_for(t0->n);
+        uint64_t *pos = ens<uint64_t>(t0->u_pos, M + 1), *pos2 = ens<uint64_t>(t0->u_pos2, M + 1);
+        uint32_t *idx = ens<uint32_t>(t0->u_idx, M + 1), *idx2 = ens<uint32_t>(t0->u_idx2, M + 1);
+        uint8_t *bdig = ens<uint8_t>(t0->u_dig, M * 32);
+        // the batch hash (VALU) runs beside the locate (random prefix / key reads) on the aux stream
+        MKV_HIP(hipEventRecord(t0->ev_in, st));
+        MKV_HIP(hipStreamWaitEvent(t0->st2, t0->ev_in, 0));
+        launch_leaf_hash_multi(B, k2, mmax, bdig, t0->st2);
+        MKV_HIP(hipEventRecord(t0->ev_join, t0->st2));
+        launch_locate_multi(B, LM, k2, mmax, pbits, pos, idx, st);
+        MKV_HIP(hipStreamWaitEvent(st, t0->ev_join, 0));
+        void *radix = t0->s_radix.ensure(std::max(radix_scratch_bytes(M), scan_scratch_bytes(M + 1)));
+        const bool sw = radix_sort_pairs(pos, idx, pos2, idx2, M, 0, std::max(8, pbits + bits_for(k2 - 1)), radix, st);
+        HTRACE("phase1-queued");
+        CA.pos = sw ? pos2 : pos;
+        CA.bidx = sw ? idx2 : idx;
+        CA.bdig = bdig;
+        CA.M = (uint32_t)M;
+        CA.pbits = pbits;
+        CA.k = k2;
+        CA.P.L = (int)L;
+        for (size_t l = 0; l < L; ++l) {
+            CA.P.base[l] = t0->lev_base[l];
+            CA.P.cnt[l] = t0->lev_cnt[l];
+            CA.P.off[l] = t0->lev_off[l];
+            CA.P.S[l] = t0->lev_S[l];
+        }
+        // Passes: a wave climbs its 64 entries while they are spread (one dirty node per lane), and stops
+        // where they start to merge (the level whose nodes span the mean gap between dirty leaves, + 1);
+        // the survivors are packed across waves and the next pass climbs 6 more levels in full waves, and
+        // so on to the top.
+        const uint64_t gap = std::max<uint64_t>(1, t0->n / std::max<uint64_t>(1, mmax));
+        int lstop = std::max(1, bits_for(gap));  // floor(log2(gap)) + 1
         const size_t pclimb = prof_begin(t0, "climb", st);
-        for (size_t l = 0; l < ltop; ++l) {
-            DirtyLevel D{};
-            D.a = t0->lev_base[l];
-            D.c = t0->lev_cnt[l];
-            D.off = t0->lev_off[l];
-            D.S = t0->lev_S[l];
-            D.has_parent = l + 1 < L && t0->lev_cnt[l + 1] > 0;
-            if (D.has_parent) {
-                D.a_par = t0->lev_base[l + 1];
-                D.c_par = t0->lev_cnt[l + 1];
-                D.off_par = t0->lev_off[l + 1];
+        ClimbPass Q{};
+        Q.bflags = bflags;
+        Q.mbox = reinterpret_cast<uint8_t *>(t0->u_mbox.ensure(climb_mbox_bytes(M)));
+        Q.in_cap = M;
+        Q.l0 = 0;
+        bool first = true;
+        int cur = 0;  // which packed buffer holds this pass's inputs
+        while (true) {
+            const bool last = lstop >= (int)L - 1;
+            Q.lstop = last ? -1 : lstop;
+            const uint64_t nb = ceil_div(Q.in_cap, 64);
+            if (!last) {
+                Q.out_key = ens<uint64_t>(t0->u_ckey, nb * 64);
+                Q.out_dig = ens<uint32_t>(t0->u_cdig, nb * 64 * 8);
+                Q.out_cnt = ens<uint32_t>(t0->u_ccnt, nb + 1);
+            } else {
+                Q.out_key = nullptr;
+                Q.out_dig = nullptr;
+                Q.out_cnt = nullptr;
             }
-            D.has_child = l > 0 && !keep_bits;
-            if (l > 0) {
-                D.a_child = t0->lev_base[l - 1];
-                D.c_child = t0->lev_cnt[l - 1];
-                D.off_child = t0->lev_off[l - 1];
-            }
-            launch_dirty_level(D, (int)l, std::min<uint64_t>(mmax, t0->lev_cnt[l]), T, k2, st);
-            if (!D.has_parent) break;  // every entry at this level cleared its own bit: bitmap is zero again
-        }
-        if (ltop < L) {
-            LevelPlan P{};
-            P.L = (int)L;
-            P.keep_bits = keep_bits ? 1 : 0;
-            for (size_t l = 0; l < L; ++l) {
-                P.base[l] = t0->lev_base[l];
-                P.cnt[l] = t0->lev_cnt[l];
-                P.off[l] = t0->lev_off[l];
-                P.S[l] = t0->lev_S[l];
-            }
-            launch_dirty_top(P, (int)ltop, T, k2, st);
+            launch_dirty_climb_pass(CA, Q, first, st);
+            if (last) break;
+            // pack the survivors (dirty nodes at level lstop) for the next pass
+            DevBuf &pk = cur ? t0->u_pk0 : t0->u_pk1, &pd = cur ? t0->u_pd0 : t0->u_pd1;
+            uint64_t bound = 0;
+            for (uint32_t q = 0; q < k2; ++q) bound += t0->lev_cnt[lstop];
+            bound = std::min<uint64_t>(bound, nb * 64);
+            uint32_t *off = ens<uint32_t>(t0->u_coff, nb + 2);
+            void *scr = t0->s_radix.ensure(std::max(radix_scratch_bytes(M), scan_scratch_bytes(nb + 1)));
+            exclusive_scan_u32(Q.out_cnt, off, nb, off + nb + 1, scr, st);
+            uint64_t *nkey = ens<uint64_t>(pk, bound + 1);
+            uint32_t *ndig = ens<uint32_t>(pd, (bound + 1) * 8);
+            launch_climb_pack(Q.out_cnt, off, (uint32_t)nb, Q.out_key, Q.out_dig, nkey, ndig, st);
+            Q.in_key = nkey;
+            Q.in_dig = ndig;
+            Q.in_n = off + nb + 1;
+            Q.in_cap = bound;
+            Q.l0 = lstop;
+            lstop += 6;
+            first = false;
+            cur ^= 1;
         }
         prof_end(t0, pclimb);
         // every tree's missing-key count and root, read back by one launch
@@ -1873,7 +1837,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         uint32_t nc = 0;
         for (size_t q = 0; q < g.size(); ++q) {
             mkv_tree *t = ts[g[q]];
-            SC.src[nc] = reinterpret_cast<const uint8_t *>(T.t[q].missing);
+            SC.src[nc] = reinterpret_cast<const uint8_t *>(CA.missing[q]);
             SC.dst[nc] = t->h_small_dev;
             SC.bytes[nc++] = sizeof(uint32_t);
             if (!t->sharded) {
@@ -1897,7 +1861,6 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             // later query of that stream ~15 µs), and their profiling pairs were recorded on st
             if (q == 0) sync(t);
             else prof_collect(t);
-            t->bm_dirty = keep_bits;
             ok[g[q]] = reinterpret_cast<volatile uint32_t *>(t->h_small)[0] == 0;
             if (ok[g[q]] && !t->sharded) std::memcpy(t->root, t->h_small + 16, 32);
             if (!ok[g[q]]) {  // tree untouched
@@ -2512,6 +2475,42 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
     return l;
 }
 
+// Device-resident form of keylist_from_refs (the sharded collectives, comm.cpp): the same gather into
+// d_outoff / d_out, left on the device — offsets[0..m] (offsets[0] == 0) and the key bytes, valid until the
+// tree's next diff / keys call. false when `reject` (optional device u32) is non-zero (nothing gathered).
+static bool keys_from_refs_dev(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B,
+                               const uint32_t *reject, DevKeys *out) {
+    *out = DevKeys{};
+    uint64_t *off = ens<uint64_t>(t->d_outoff, m + 1);
+    if (!m) {
+        MKV_HIP(hipMemsetAsync(off, 0, 8, t->st));
+        out->off = off;
+        out->kb = ens<uint8_t>(t->d_out, 16);
+        if (reject) {
+            small_d2h(t, t->h_small + 1, reject, 4, t->st);
+            wait_stream(t, t->st);
+            if (reinterpret_cast<const uint32_t *>(t->h_small + 1)[0] != 0) return false;
+        }
+        return true;
+    }
+    uint64_t *lens = ens<uint64_t>(t->s_lens, m + 1);
+    void *scr = t->d_diffscr.ensure(scan_scratch_bytes(m + 1));
+    launch_diff_keylens(refs, m, A, B, lens, t->st);
+    exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
+    small_d2h(t, t->h_small, off + m, 8, t->st);
+    if (reject) small_d2h(t, t->h_small + 1, reject, 4, t->st);
+    wait_stream(t, t->st);
+    const uint64_t bytes = t->h_small[0];
+    if (reject && reinterpret_cast<const uint32_t *>(t->h_small + 1)[0] != 0) return false;
+    uint8_t *ob = ens<uint8_t>(t->d_out, bytes + 16);
+    launch_diff_keys(refs, m, A, B, off, ob, t->st);
+    out->n = m;
+    out->bytes = bytes;
+    out->off = off;
+    out->kb = ob;
+    return true;
+}
+
 // The batched diff's key list (configs[4]: one list for every replica of the 1-vs-k walk): keys gathered
 // on st as in keylist_from_refs, then the device -> pinned copy (PCIe-bound: ~28 MB for 7 x 125K keys)
 // runs on st3 and the call returns without waiting for it; mkv_keylist_get waits when the bytes are
@@ -2559,7 +2558,8 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
     return l;
 }
 
-static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
+// dev != nullptr: the divergent keys stay in device memory (*dev; sharded collectives), returns nullptr.
+static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev = nullptr) {
     mkv_tree *t = const_cast<mkv_tree *>(a);
     t->walk_L = 0;  // td_cnt is about to hold a pair walk's counters: no batched-walk stats any more
     // b's last work must be complete before a's stream reads it
@@ -2571,7 +2571,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
     uint64_t m = 0;
     bool done = false;
     const uint64_t nwords = (A.n + 31) / 32;
-    if (A.n > 0 && same_plan(a, b) && !a->sharded && !b->sharded && a->lev_S.size() > 1 &&
+    if (!dev && A.n > 0 && same_plan(a, b) && !a->sharded && !b->sharded && a->lev_S.size() > 1 &&
         ceil_div(nwords, 1024) <= 8192) {
         int fb = 0;
         mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);
@@ -2588,8 +2588,12 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
         HTRACE("topdown-done");
         if (done) {
             // the leaf-key check (nbad) comes back with the key list's byte count
-            mkv_keylist *l = keylist_from_refs(t, refs, m, A, B, nbad);
-            if (l) return l;
+            if (dev) {
+                if (keys_from_refs_dev(t, refs, m, A, B, nbad, dev)) return nullptr;
+            } else {
+                mkv_keylist *l = keylist_from_refs(t, refs, m, A, B, nbad);
+                if (l) return l;
+            }
             m = 0;  // a divergent position holds different keys: the key sets differ
             done = false;
         }
@@ -2609,6 +2613,10 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b) {
             prof_end(t, pd);
             m = d2h_u64(t, cnt);
         }
+    }
+    if (dev) {
+        keys_from_refs_dev(t, refs, m, A, B, nullptr, dev);
+        return nullptr;
     }
     return keylist_from_refs(t, refs, m, A, B);
 }
@@ -3473,3 +3481,51 @@ mkv_status mkv_leaf_digests(int hip_device, mkv_blob keys, mkv_blob values, uint
 }
 
 }  // extern "C"
+
+// ---------------- internals shared with comm.cpp (device-resident sharded collectives) ----------------
+namespace mkv {
+DevKeys tree_diff_device(const mkv_tree *a, const mkv_tree *b) {
+    if (!a || !b) throw Error(ST_EINVAL, "null argument");
+    if (a->dev != b->dev) throw Error(ST_EINVAL, "trees on different devices");
+    if (a->prepared || b->prepared) throw Error(ST_ESTATE, "shard_reduce pending");
+    DevGuard g(a->dev);
+    DevKeys d;
+    diff_pair(a, b, &d);
+    return d;
+}
+DevKeys tree_keys_at_device(const mkv_tree *tc, const uint64_t *pos, uint64_t m) {
+    mkv_tree *t = const_cast<mkv_tree *>(tc);
+    for (uint64_t i = 0; i < m; ++i)
+        if (pos[i] >= t->n) throw Error(ST_EINVAL, "leaf position out of range");
+    DevGuard g(t->dev);
+    uint64_t *refs = ens<uint64_t>(t->x_idx, m + 1);
+    if (m) MKV_HIP(hipMemcpyAsync(refs, pos, m * 8, hipMemcpyHostToDevice, t->st));
+    const DiffSide A = side_of(t);
+    DevKeys d;
+    keys_from_refs_dev(t, refs, m, A, A, nullptr, &d);
+    return d;
+}
+hipStream_t tree_stream(const mkv_tree *t) { return t->st; }
+int tree_device(const mkv_tree *t) { return t->dev; }
+uint64_t tree_len(const mkv_tree *t) { return t->n; }
+// One copy of a device key list (offsets[0..n], offsets[0] == 0, then the bytes) into a pinned block on
+// stream st; complete on return.
+mkv_keylist *keylist_from_device(const uint64_t *d_off, const uint8_t *d_kb, uint64_t n, uint64_t bytes, hipStream_t st) {
+    auto *l = new mkv_keylist();
+    if (!n) return l;
+    try {
+        const uint64_t kpos = (8 * (n + 1) + 15) & ~uint64_t(15);
+        l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
+        MKV_HIP(hipMemcpyAsync(l->blk->p, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+        if (bytes) MKV_HIP(hipMemcpyAsync(l->blk->p + kpos, d_kb, bytes, hipMemcpyDeviceToHost, st));
+        MKV_HIP(hipStreamSynchronize(st));
+        l->offsets = reinterpret_cast<const uint64_t *>(l->blk->p);
+        l->bytes = l->blk->p + kpos;
+        l->n = n;
+    } catch (...) {
+        delete l;
+        throw;
+    }
+    return l;
+}
+}  // namespace mkv

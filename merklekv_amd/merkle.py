@@ -685,6 +685,16 @@ class MerkleTree:
         comm.check(lib().mkv_sharded_diff(self._h, other._h, comm.handle, C.byref(kl)))
         return KeyList(kl)
 
+    def sharded_diff_local(self, other: "MerkleTree", comm):
+        """mkv_sharded_diff_local: this rank's slice of the global divergent-key list, its global offset
+        and the global length — one 32-B all-gather. Returns (KeyList, offset, total)."""
+        self._flush()
+        other._flush()
+        kl, off, tot = C.c_void_p(), C.c_uint64(), C.c_uint64()
+        comm.check(lib().mkv_sharded_diff_local(self._h, other._h, comm.handle, C.byref(kl), C.byref(off),
+                                                C.byref(tot)))
+        return KeyList(kl), off.value, tot.value
+
     # ------------------------------------------------------------------ redistribution (f-3)
     # Tensor arguments are device tensors on this tree's GPU: key / value bytes (uint8), offsets (int64,
     # n + 1 entries), lengths (int32 holding u32). See shard.redistribute for the collective flow.

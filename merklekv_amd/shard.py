@@ -34,6 +34,8 @@ _bufs: dict = {}
 # Wall time of each collective kind (host clock around the collective and the wait for its result):
 # name -> [seconds, calls, payload bytes per rank]. Read by bench.py (per-collective timings).
 coll_stats: dict = {}
+# Library communicator only: name -> [host-staged payload bytes, meta bytes] (mkv_comm_traffic).
+coll_traffic: dict = {}
 
 
 def _coll_add(name: str, secs: float, nbytes: int) -> None:
@@ -45,6 +47,7 @@ def _coll_add(name: str, secs: float, nbytes: int) -> None:
 
 def coll_stats_reset() -> None:
     coll_stats.clear()
+    coll_traffic.clear()
 
 
 def _is_gpu(device) -> bool:
@@ -130,7 +133,13 @@ def _comm(dist, device, group):
 
 
 def _absorb(comm) -> None:
-    """Move the communicator's collective timings into coll_stats."""
+    """Move the communicator's collective timings (and host <-> device bytes: coll_traffic) into
+    coll_stats."""
+    for name, (staged, meta) in comm.traffic().items():
+        if staged or meta:
+            s = coll_traffic.setdefault(name, [0, 0])
+            s[0] += int(staged)
+            s[1] += int(meta)
     for name, (secs, calls, nbytes) in comm.stats(reset=True).items():
         if calls:
             s = coll_stats.setdefault(name, [0.0, 0, 0])
@@ -161,6 +170,31 @@ def sharded_root(tree, keys, values, dist, device="cpu", group=None, on_device: 
     offset, total = sum(counts[:rank]), sum(counts)
     tree.shard_reduce(offset, total)
     return shard_recombine_many([tree], dist, total, device, group)[0], counts
+
+
+def sequential_root(tree, shard_blobs, global_n: int):
+    """Global root of key-range shards built one after another on ONE GPU (configs[3]'s 1B keys on a single
+    MI355X: 8 x 125M records never reside together; each shard's records and scratch can be dropped before
+    the next one is produced). Per shard g, in key order: mkv_shard_prepare (hash + sort + dedup) ->
+    mkv_shard_reduce at offset o_g = the leaves of shards < g inside a tree of global_n leaves ->
+    mkv_shard_fringe (<= MKV_FRINGE_BYTES to the host); then one mkv_shard_combine of every fringe —
+    rebuild() over the union (/root/reference/src/store/merkle.rs:73-121). shard_blobs yields
+    (kb, koff, vb, voff, n) device blobs (tensors or pointers); it may generate each shard lazily.
+    global_n is the total leaf count after dedup; a mismatch (duplicate keys inside a shard) raises
+    ValueError, because the offsets of later shards would have been wrong. Returns (root, counts)."""
+    counts, fringes = [], []
+    off = 0
+    for blob in shard_blobs:
+        n_g = tree.shard_prepare(blob, None, on_device=True)
+        if off + n_g > global_n:
+            raise ValueError(f"shards hold more than global_n = {global_n} leaves")
+        tree.shard_reduce(off, global_n)
+        fringes.append(tree.shard_fringe())
+        counts.append(n_g)
+        off += n_g
+    if off != global_n:
+        raise ValueError(f"shards hold {off} leaves, not global_n = {global_n}")
+    return tree.shard_combine(b"".join(fringes), len(fringes), global_n), counts
 
 
 def shard_recombine_many(trees, dist, total: int, device="cpu", group=None) -> list:
@@ -208,6 +242,11 @@ def sharded_diff(a, b, dist, device="cpu", group=None):
     differ), then the divergence counts are all-gathered (8 B/rank) so every rank knows where its keys
     sit in the global sorted list (ranges are ordered by rank, so the concatenation is sorted).
     Returns (this rank's packed keys (bytes array, offsets), global offset, global count)."""
+    if _native(a, b):  # the library's own slice + offset (mkv_sharded_diff_local: one 32-B all-gather)
+        comm = _comm(dist, device, group)
+        kl, off, tot = a.sharded_diff_local(b, comm)
+        _absorb(comm)
+        return (kl.raw.copy(), kl.offs.copy()), off, tot
     rank = dist.get_rank(group)
     raw, offs = a.diff_keys_packed(b)
     counts = shard_counts(dist, len(offs) - 1, device, group)

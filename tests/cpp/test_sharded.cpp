@@ -2,10 +2,13 @@
 // non-Python host would drive them (the reference's SyncManager is Rust, sync.rs:56-87):
 //   1. RCCL communicator at world 1 (unique id -> init_rank): sharded build, root, multi-replica root
 //      and sharded diff equal the unsharded tree and an OpenSSL restatement of rebuild()/diff_keys();
+//      mkv_sharded_diff_local gives the slice at its global offset; mkv_comm_traffic shows no host-staged
+//      payload byte; a failing local step returns an error and the communicator stays usable;
 //   2. host communicator at world 3 (three threads, one tree each, the host's own all-gather): every
 //      rank's global root equals the unsharded root, the gathered divergent-key list is the whole sorted
-//      diff on every rank, in-range updates + mkv_sharded_root_many track the new root, and overlapping
-//      ranges are rejected (MKV_EINVAL) on every rank.
+//      diff on every rank, the local slices sit at their global offsets, in-range updates +
+//      mkv_sharded_root_many track the new root, overlapping ranges are rejected (MKV_EINVAL) on every
+//      rank, and an invalid blob on ONE rank makes every rank's call fail (status words) without a hang.
 // Built by __graft_entry__.build_cpp_tests(); run by tests/test_cpp_ports_gpu.py.
 #include <openssl/evp.h>
 
@@ -170,11 +173,30 @@ static void test_rccl_world1(int dev) {
     mkv_keylist *l = nullptr;
     OK(mkv_sharded_diff(a, b, c, &l));
     if (l) CHECK(keylist(l) == model_diff(ra, rb));
+    // this rank's slice and its place in the global list (world 1: the whole list at offset 0)
+    mkv_keylist *ls = nullptr;
+    uint64_t goff = 99, gtot = 0;
+    OK(mkv_sharded_diff_local(a, b, c, &ls, &goff, &gtot));
+    const std::vector<std::string> want_d = model_diff(ra, rb);
+    if (ls) CHECK(keylist(ls) == want_d);
+    CHECK(goff == 0 && gtot == want_d.size());
     double secs[MKV_COLL_KINDS];
-    uint64_t calls[MKV_COLL_KINDS], bytes[MKV_COLL_KINDS];
+    uint64_t calls[MKV_COLL_KINDS], bytes[MKV_COLL_KINDS], staged[MKV_COLL_KINDS], meta[MKV_COLL_KINDS];
+    OK(mkv_comm_traffic(c, staged, meta));
     OK(mkv_comm_stats(c, secs, calls, bytes, 1));
-    CHECK(calls[MKV_COLL_COUNTS] == 3 && calls[MKV_COLL_FRINGE] == 5 && calls[MKV_COLL_DIFF] == 2);
-    CHECK(bytes[MKV_COLL_FRINGE] == 7ull * MKV_FRINGE_BYTES);  // 1 + 1 + 1 + 1 + 3 trees
+    // one meta gather per build (3), 5 fringe gathers, the diff's meta + block gathers, the slice's meta
+    CHECK(calls[MKV_COLL_COUNTS] == 3 && calls[MKV_COLL_FRINGE] == 5 && calls[MKV_COLL_DIFF] == 3);
+    CHECK(calls[MKV_COLL_RANGE] == 2);  // one boundary-key gather per range-checked build
+    CHECK(bytes[MKV_COLL_FRINGE] == 7ull * MKV_FRINGE_BYTES + 5 * 32);  // 1 + 1 + 1 + 1 + 3 trees + headers
+    // RCCL form: no payload byte crossed between host and device; only status / count words came back
+    for (int k = 0; k < MKV_COLL_KINDS; ++k) CHECK(staged[k] == 0);
+    CHECK(meta[MKV_COLL_COUNTS] == 3 * 32 && meta[MKV_COLL_DIFF] > 0);
+    // a failing local step (keys.n != values.n) returns an error and leaves the communicator usable
+    mkv_blob bad_v = va.blob();
+    bad_v.n = bad_v.n - 1;
+    CHECK(mkv_sharded_build(b, c, ka.blob(), bad_v, 0, 1, nullptr) == MKV_EINVAL);
+    OK(mkv_sharded_build(b, c, kb.blob(), vb.blob(), 0, 1, nullptr));
+    CHECK(root_of(b) == model_root(rb));
     for (mkv_tree *t : {a, b, a2, u}) mkv_tree_destroy(t);
     mkv_comm_destroy(c);
     std::printf("rccl world 1: %s\n", g_fail ? "FAILED" : "ok");
@@ -237,7 +259,9 @@ static void test_host_world3(int dev) {
     const Digest want_upd = model_root(upd);
     std::vector<std::string> got_a(world), got_b(world), got_upd(world);
     std::vector<std::vector<std::string>> got_diff(world);
-    std::vector<int> bad_status(world, -1);
+    std::vector<int> bad_status(world, -1), fail_status(world, -1);
+    std::vector<std::vector<std::string>> got_slice(world);
+    std::vector<uint64_t> got_off(world), got_tot(world);
     std::vector<std::thread> th;
     for (int r = 0; r < world; ++r)
         th.emplace_back([&, r] {
@@ -258,6 +282,22 @@ static void test_host_world3(int dev) {
             mkv_keylist *l = nullptr;
             OK(mkv_sharded_diff(a, b, c, &l));
             if (l) got_diff[r] = keylist(l);
+            mkv_keylist *ls = nullptr;
+            uint64_t goff = 0, gtot = 0;
+            OK(mkv_sharded_diff_local(a, b, c, &ls, &goff, &gtot));
+            if (ls) got_slice[r] = keylist(ls);
+            got_off[r] = goff;
+            got_tot[r] = gtot;
+            // rank 1's blob is invalid (keys.n != values.n): EVERY rank gets an error from this call (rank 1
+            // its own EINVAL, the others rank 1's code through the status word), nobody waits forever
+            {
+                Packed bk, bv;
+                pack(sb[r], bk, bv);
+                mkv_blob vbl = bv.blob();
+                if (r == 1) vbl.n -= 1;
+                fail_status[r] = mkv_sharded_build(b, c, bk.blob(), vbl, 0, 1, nullptr);
+                OK(mkv_sharded_build(b, c, bk.blob(), bv.blob(), 0, 1, nullptr));  // back in step
+            }
             // in-range update of this shard, then the global root of both replicas in one all-gather
             Packed uk, uv;
             uk.add(sa[r].begin()->first);
@@ -284,7 +324,15 @@ static void test_host_world3(int dev) {
         CHECK(got_diff[r] == want_diff);
         CHECK(got_upd[r] == want_upd);
         CHECK(bad_status[r] == MKV_EINVAL);
+        CHECK(fail_status[r] == MKV_EINVAL);
+        // the slices are the global list cut at the global offsets (ranges ordered by rank)
+        CHECK(got_tot[r] == want_diff.size());
+        CHECK(got_off[r] + got_slice[r].size() <= want_diff.size());
+        CHECK(std::vector<std::string>(want_diff.begin() + got_off[r], want_diff.begin() + got_off[r] + got_slice[r].size()) ==
+              got_slice[r]);
     }
+    CHECK(got_off[0] == 0 && got_off[1] == got_slice[0].size() && got_off[2] == got_off[1] + got_slice[1].size());
+    CHECK(got_off[2] + got_slice[2].size() == want_diff.size());
     std::printf("host world 3: %s (diff %zu keys)\n", g_fail ? "FAILED" : "ok", want_diff.size());
 }
 

@@ -174,3 +174,41 @@ def test_cpu_baselines_match_oracle(oracle_lib):
     assert co.ref_diff((kb, ko, vb, vo), (kb2, ko2, vb2, vo2))[1] == want
     for th in (1, 3, 8):
         assert co.mt_diff(ta, tb, th)[1] == want
+
+
+@pytest.mark.parametrize("G,nper,blog", [(8, 12345, 10), (4, 1000, 3), (8, 1, 1), (2, 3, 1), (8, 4096, 8),
+                                         (1, 777, 4), (8, 2048, 11)])
+def test_root_stream_matches_tree_build(oracle_lib, G, nper, blog):
+    """oracle/root_stream (the streaming restatement that computes the configs[3] golden root,
+    tests/golden/roots_sharded.json) equals orc_tree_build over the union of the G key-range shards:
+    aligned-block pushes, leaf pushes at unaligned shard seams and the final R5 promotions
+    (/root/reference/src/store/merkle.rs:94-118)."""
+    import json
+    import os
+    import subprocess
+
+    from oracle import coracle
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "oracle", "root_stream")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", os.path.join(root, "oracle"), "root_stream"])
+    parts = [coracle.gen_records(DEFAULT_SEED, g * nper, nper, shard=g, nshards=G) for g in range(G)]
+    kb = np.concatenate([p[0] for p in parts])
+    vb = np.concatenate([p[2] for p in parts])
+    n = G * nper
+    want = coracle.OracleTree.build(kb, np.arange(n + 1, dtype=np.uint64) * 32, vb,
+                                    np.arange(n + 1, dtype=np.uint64) * 100).root().hex()
+    out = json.loads(subprocess.check_output([exe, str(DEFAULT_SEED), str(G), str(nper), "32", "100", str(blog), "3"]))
+    assert out["n"] == n and out["counts"] == [nper] * G
+    assert out["root"] == want
+
+
+def test_roots_sharded_golden_file():
+    """The committed configs[3] roots name the generator cases the GPU test rebuilds."""
+    import json
+    import os
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "roots_sharded.json")))
+    cases = {(c["shards"], c["per_shard"]): c for c in d["cases"]}
+    big = cases[(8, 125_000_000)]
+    assert big["n"] == 1_000_000_000 and big["seed"] == DEFAULT_SEED and len(big["root"]) == 64
+    assert cases[(8, 15_625_000)]["n"] == 125_000_000

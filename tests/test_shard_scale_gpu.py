@@ -150,6 +150,7 @@ def test_sharded_8way_125m_device_fringe():
     del whole, uko, uvo
     torch.cuda.empty_cache()
     assert roots_a == [want_root] * W
+    assert want_root == _golden_root(W, ng)  # pinned by the CPU oracle (tests/golden/roots_sharded.json)
     # replicas: value-only (top-down per shard) and mixed (merge-join per shard), 0.1 % per shard
     g_ = torch.Generator(device="cuda")
     g_.manual_seed(31)
@@ -204,3 +205,43 @@ def test_sharded_8way_125m_device_fringe():
         assert (np.lexsort(g_all.T[::-1]) == np.arange(len(g_all))).all()  # globally sorted
         del trees_b, bl
         torch.cuda.empty_cache()
+
+
+def _golden_root(shards, per_shard):
+    import json
+    import os
+    d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "roots_sharded.json")))
+    for c in d["cases"]:
+        if c["shards"] == shards and c["per_shard"] == per_shard and c["seed"] == DEFAULT_SEED:
+            return bytes.fromhex(c["root"])
+    raise KeyError((shards, per_shard))
+
+
+def test_configs3_1b_root_sequential_shards_vs_golden():
+    """configs[3] at its full size: 1B keys = 8 key ranges x 125M records (generator shard g of 8, records
+    [g * 125M, (g + 1) * 125M)), built on ONE GPU shard after shard (shard.sequential_root: prepare ->
+    reduce at the shard's global offset -> fringe; each shard's records regenerated into the same buffers),
+    then the seam combine of the 8 fringes. The root equals the golden root the CPU oracle computed over
+    the same 1B records (tests/golden/roots_sharded.json, oracle/root_stream.c, merkle.rs:73-121)."""
+    import torch
+
+    from merklekv_amd.merkle import gen_records_device
+    from merklekv_amd.shard import sequential_root
+    ng, nsh = 125_000_000, 8
+    kb = torch.empty(ng * K + 64, dtype=torch.uint8, device="cuda")
+    vb = torch.empty(ng * V + 64, dtype=torch.uint8, device="cuda")
+    ko = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    vo = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+
+    def shards():
+        for g in range(nsh):
+            gen_records_device(0, DEFAULT_SEED, g * ng, ng, K, V, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
+                               vo.data_ptr(), shard=g, nshards=nsh)
+            torch.cuda.synchronize()
+            yield (kb, ko, vb, vo, ng)
+
+    t = MerkleTree()
+    root, counts = sequential_root(t, shards(), ng * nsh)
+    assert counts == [ng] * nsh
+    assert root == _golden_root(nsh, ng)
+    del t, kb, vb, ko, vo
