@@ -12,8 +12,11 @@ every rank. The N>1 line also carries `sharded_125m_per_rank` (the same sharded 
 per rank: configs[3] = 1B keys at N=8) and `diff_sharded`; the N=1 line carries `anchor_125m` (125M
 keys on one GPU: the per-GPU anchor of the 125M-per-rank curve),
 `diff_100m` (configs[2], both divergence modes, exactness vs construction), `configs0` (the 100K CPU
-config on the GPU) and the CPU baselines (cpu_ref: the reference's data structures, single thread;
-cpu_mt: all host cores).
+config on the GPU), `configs4` (configs[4]: 125M keys x 8 replicas, 125K-key value batches per variant —
+the same measurement as `--workload incremental`, with the dirty climb's roofline), `configs3_1b_sequential`
+(configs[3]'s 1B keys on ONE GPU: 8 key-range shards resident in HBM, built shard after shard and combined,
+root checked against the CPU oracle's golden root) and the CPU baselines (cpu_ref: the reference's data
+structures, single thread; cpu_mt: all host cores).
 
 Other BASELINE configs (run explicitly; their JSON lines are committed under profiles/):
   --workload diff         configs[2]: two 100M-key replicas, (a) 0.1 % value-only divergence (top-down
@@ -929,7 +932,7 @@ def configs4_measure(ctx, n, m, R, steps, warmup):
     pmc_ok = pmc_inc.get("tree_keys") == N and pmc_inc.get("replicas") == R and pmc_inc.get("batch") == m
     comp = 2 * rehashed          # one full + one constant-schedule compression per node
     roofline = {
-        "bound": "hbm", "kernel": "k_dirty_climb (one launch: every replica's whole climb)",
+        "bound": "hbm", "kernel": "k_dirty_climb + k_reduce_fused/top above its stop level (every replica per launch)",
         "achieved": climb_bytes / (climb_ms * 1e-3) / 1e9 if climb_ms else None, "peak": HBM_PEAK_GBS,
         "unit": "GB/s", "frac": climb_bytes / (climb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if climb_ms else None,
         "traffic": pmc_inc.get("climb_hbm_bytes_per_step") if pmc_ok else None,

@@ -32,6 +32,7 @@ template <bool SHORT, int THREADS>
 __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
     const uint64_t t = p.tile0 + blockIdx.x;
+    const uint64_t dz = p.ztab ? p.ztab[blockIdx.y] : 0;  // this tree's arrays (several trees: grid.y)
     for (int k = 1; k <= p.nl; ++k) {
       const uint64_t Tk = (uint64_t)RD_TILE >> (k - 1);
       // THREADS < RD_TILE: a thread takes several parents of the first fused levels, so the upper fused
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
                 r[0] = bswap32(x1.x); r[1] = bswap32(x1.y); r[2] = bswap32(x1.z); r[3] = bswap32(x1.w);
                 r[4] = bswap32(y1.x); r[5] = bswap32(y1.y); r[6] = bswap32(y1.z); r[7] = bswap32(y1.w);
             } else if (k == 1) {
-                const uint8_t *src = p.in + 32 * (c0 - p.a[0]);
+                const uint8_t *src = p.in + dz + 32 * (c0 - p.a[0]);
                 load_digest(src, l);
                 if (pair) load_digest(src + 32, r);
             } else {
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(THREADS) void k_reduce_fused(FusePlan p) {
             uint32_t *dst = buf[k & 1] + 8 * i;
 #pragma unroll
             for (int q = 0; q < 8; ++q) dst[q] = o[q];
-            store_digest(p.out[k - 1] + 32 * (j - p.a[k]), o);
+            store_digest(p.out[k - 1] + dz + 32 * (j - p.a[k]), o);
         }
       }
       __syncthreads();
@@ -110,6 +111,8 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
     __shared__ __attribute__((aligned(16))) uint32_t buf[2][RD_TILE * 8];
     __shared__ uint32_t last;
     const uint64_t t = p.tile0 + blockIdx.x;
+    const uint64_t dz = p.ztab ? p.ztab[blockIdx.y] : 0;  // this tree's arrays (several trees: grid.y)
+    uint32_t *const arrive = p.arrive + 16 * blockIdx.y;
     const int nf = p.nf;
     for (int k = 1; k <= nf; ++k) {
         const uint64_t Tk = (uint64_t)RD_TILE >> (k - 1);
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
                 r[0] = bswap32(x1.x); r[1] = bswap32(x1.y); r[2] = bswap32(x1.z); r[3] = bswap32(x1.w);
                 r[4] = bswap32(y1.x); r[5] = bswap32(y1.y); r[6] = bswap32(y1.z); r[7] = bswap32(y1.w);
             } else if (k == 1) {
-                const uint8_t *src = p.in + 32 * (c0 - p.a[0]);
+                const uint8_t *src = p.in + dz + 32 * (c0 - p.a[0]);
                 load_digest(src, l);
                 if (pair) load_digest(src + 32, r);
             } else {
@@ -160,7 +163,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
             uint32_t *dst = buf[k & 1] + 8 * i;
 #pragma unroll
             for (int q = 0; q < 8; ++q) dst[q] = o[q];
-            store_digest(p.out[k - 1] + 32 * (j - p.a[k]), o);
+            store_digest(p.out[k - 1] + dz + 32 * (j - p.a[k]), o);
         }
         lds_barrier();
     }
@@ -170,9 +173,9 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
         __threadfence();  // this thread's level writes, visible device-wide before the arrival
         __syncthreads();
         if (threadIdx.x == 0) {
-            const uint32_t prev = __hip_atomic_fetch_add(p.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t prev = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
             last = prev + 1 == (uint32_t)p.ntiles;
-            if (last) __hip_atomic_store(p.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (last) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         if (!last) return;
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
             const uint64_t c0 = 2 * j;
             const bool pair = c0 + 1 < p.S[k - 1];
             if (k == nf + 1) {
-                const uint32_t *src = reinterpret_cast<const uint32_t *>(p.out[nf - 1]) + 8 * (c0 - p.a[nf]);
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(p.out[nf - 1] + dz) + 8 * (c0 - p.a[nf]);
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
                     l[q] = bswap32(__hip_atomic_load(src + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(RD_TILE) void k_reduce_top(TopPlan p) {
             uint32_t *dst = buf[k & 1] + 8 * i;
 #pragma unroll
             for (int q = 0; q < 8; ++q) dst[q] = o[q];
-            store_digest(p.out[k - 1] + 32 * i, o);
+            store_digest(p.out[k - 1] + dz + 32 * i, o);
         }
         lds_barrier();
     }
@@ -419,10 +422,11 @@ void launch_reduce_fused(const FusePlan &p, hipStream_t st) {
     if (p.ntiles == 0) return;
     // Few tiles = latency-bound (each fused level waits one full node hash): the short dependency chain
     // there; many tiles = throughput-bound: fewer instructions win (profiles/r01_valu_microbench.md).
-    if (p.ntiles < 256)
-        hipLaunchKernelGGL((k_reduce_fused<true, RD_TILE>), dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+    const dim3 g((uint32_t)p.ntiles, p.nz ? p.nz : 1);
+    if (p.ntiles * g.y < 256)
+        hipLaunchKernelGGL((k_reduce_fused<true, RD_TILE>), g, dim3(RD_TILE), 0, st, p);
     else
-        hipLaunchKernelGGL((k_reduce_fused<false, RD_TILE>), dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+        hipLaunchKernelGGL((k_reduce_fused<false, RD_TILE>), g, dim3(RD_TILE), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 
@@ -431,7 +435,7 @@ void launch_reduce_top(const TopPlan &p, hipStream_t st) {
     // Plain rounds: one wave per SIMD is bound by its own issue rate (~4 cycles per VALU instruction), not
     // by the round's dependency chain, so the form with fewer instructions wins even here (10M build: 110
     // vs 116 us for the short-chain form).
-    hipLaunchKernelGGL(k_reduce_top<false>, dim3((uint32_t)p.ntiles), dim3(RD_TILE), 0, st, p);
+    hipLaunchKernelGGL(k_reduce_top<false>, dim3((uint32_t)p.ntiles, p.nz ? p.nz : 1), dim3(RD_TILE), 0, st, p);
     MKV_LAUNCH_CHECK();
 }
 

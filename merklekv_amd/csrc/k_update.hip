@@ -208,8 +208,9 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
 }
 
 // ---------------------------------------------------------------------------------------------------
-// k_dirty_climb (round 5): the dirty-path rehash of k replicas, one wave per batch of 64 consecutive
-// entries, climbing level-synchronously with the batch's dirty nodes compacted in the wave's lanes.
+// k_dirty_climb (round 5): the sparse part of the dirty-path rehash of k replicas, one wave per batch of 64
+// consecutive entries, climbing level-synchronously with the batch's dirty nodes compacted in the wave's
+// lanes; the dense part above it is the ordinary reduction (see the end of this comment).
 //
 // Entries: the batch positions sorted by (tree << pbits | leaf) — a run of equal keys is one leaf written
 // several times; its LAST entry is the last write (merkle.rs:54). Lane k of a wave holds the batch's k-th
@@ -222,23 +223,44 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
 //     SHA-256(left || right) (R4) with the sibling's 32 B, read one level ahead (it lands while the
 //     previous level hashes): 32 B read + 32 B written per rehashed node, the dirty child is never re-read;
 //   * sibling dirty and held by lane k +/- 1 (the entries are sorted, so a dirty sibling's entries are the
-//     neighbouring lane's): the left lane stores and stops, the right one takes its digest across lanes
-//     (ds_bpermute) and hashes the parent — no memory round trip, no barrier;
+//     neighbouring lane's): the left lane stores and stops, the right one reads its digest from the wave's
+//     LDS slots and hashes the parent — no memory round trip, no barrier;
 //   * sibling dirty beyond the batch (first / last lane only): a rendezvous with the other wave through a
 //     mailbox per entry boundary — both sides publish {digest, outer entry bound, its neighbour}
 //     write-through (sc1), drain, then fetch_or the boundary's bit at agent scope; the first arriver stops,
 //     the second clears the bit, reads the other side with sc1 loads (the hand-off form of
 //     MI355X_MICROARCH.md: sc1 payload -> vmcnt(0) -> atomic; consumer: returned atomic -> sc1 loads) and
 //     goes on. The bits are all-zero again when the launch ends.
-// After each level the survivors are compacted into the low lanes (ds_permute). A wave's lanes thin out as
-// its batch merges, so a pass stops at level `lstop` and writes its survivors (start key + digest); they are
-// compacted across waves and the next pass climbs on from them in full waves (passes: levels 0-10, 10-16,
-// 16-top for 1e8-leaf trees). Per-level dirty counts (mkv_tree_update_counts) are kept in LDS and added to
-// the trees' counters once per workgroup.
+// After each level the survivors are compacted into the low lanes through the wave's LDS slots. A wave's
+// lanes thin out as its batch merges, so the climb stops at level `lstop`, the first level whose nodes span
+// the mean gap between dirty leaves (about half of its nodes are dirty): it stores its dirty nodes there,
+// and every level above is rehashed whole by the build's reduction kernels (run_reduce from lstop, all k
+// trees in one launch per step, full waves, a few % more hashes than the dirty ones). Round 5 measured the
+// alternative — more climb passes over the survivors packed across waves — at 0.47 ms for the levels above
+// lstop of configs[4]; the waves still thinned out within each pass. Per-level dirty counts
+// (mkv_tree_update_counts) are kept in LDS and added to the trees' counters once per workgroup.
 // ---------------------------------------------------------------------------------------------------
 constexpr int CW_THREADS = 256;  // four independent waves
-constexpr uint32_t CW_MAX_BLOCKS = 1024;  // 4 waves per SIMD x 1,024 SIMDs / 4 waves per block
+constexpr uint32_t CW_MAX_BLOCKS = 768;  // 3 waves per SIMD x 1,024 SIMDs / 4 waves per block
 
+// Tree node arrays are addressed through GLOBAL-address-space pointers: a pointer read back from LDS is a
+// generic (flat) pointer, and a flat load also counts in lgkmcnt — every LDS wait of the level would then
+// wait for the sibling read issued one level ahead, serialising what the read-ahead overlaps.
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) u4v g_u4v;
+__device__ __forceinline__ g_u8 *gptr(uint64_t a) { return (g_u8 *)a; }
+__device__ __forceinline__ void g_load_raw(const g_u8 *p, uint4 &a, uint4 &b) {
+    const g_u4v *q = (const g_u4v *)p;
+    const u4v x = q[0], y = q[1];
+    a = make_uint4(x.x, x.y, x.z, x.w);
+    b = make_uint4(y.x, y.y, y.z, y.w);
+}
+__device__ __forceinline__ void g_store_digest(g_u8 *p, const uint32_t w[8]) {
+    g_u4v *q = (g_u4v *)p;
+    q[0] = u4v{bswap32(w[0]), bswap32(w[1]), bswap32(w[2]), bswap32(w[3])};
+    q[1] = u4v{bswap32(w[4]), bswap32(w[5]), bswap32(w[6]), bswap32(w[7])};
+}
 __device__ __forceinline__ void load_raw(const uint8_t *p, uint4 &a, uint4 &b) {
     const uint4 *q = reinterpret_cast<const uint4 *>(p);
     a = q[0];
@@ -276,11 +298,9 @@ __device__ __forceinline__ int classify(const ClimbPlan &P, uint32_t t, int l, u
 // side 1 = the right subtree's {digest, hi, pn}; 8-B words, written with sc1 atomic stores.
 constexpr uint64_t MBOX_SIDE_WORDS = 6, MBOX_WORDS = 2 * MBOX_SIDE_WORDS;
 
-template <bool FIRST>
-__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_dirty_climb(ClimbArgs A,
-                                                                                                      ClimbPass Q) {
+__global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_dirty_climb(ClimbArgs A) {
     __shared__ uint32_t s_lc[DIRTY_MAX_TREES * MKV_MAXLEV];
-    __shared__ uint8_t *s_nodes[DIRTY_MAX_TREES];
+    __shared__ uint64_t s_nodes[DIRTY_MAX_TREES];  // addresses: used as global pointers (gptr)
     __shared__ uint32_t s_done;
     // per wave: the batch's dirty nodes in key order (slot k = dirty node k), rewritten every level
     __shared__ uint64_t s_qx[CW_THREADS / 64][64], s_qpn[CW_THREADS / 64][64], s_qpp[CW_THREADS / 64][64];
@@ -303,17 +323,18 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
     __shared__ uint32_t s_miss[DIRTY_MAX_TREES];
     __shared__ uint32_t *s_cntp[DIRTY_MAX_TREES];
     if (tid < A.k) {
-        s_nodes[tid] = A.nodes[tid];
+        s_nodes[tid] = reinterpret_cast<uint64_t>(A.nodes[tid]);
         s_miss[tid] = *A.missing[tid];
         s_cntp[tid] = A.cnt[tid];
     }
     if (tid == 0) s_done = 0;
+    if (blockIdx.x == 0 && tid < A.k && A.ztab) A.ztab[tid] = (uint64_t)(A.nodes[tid] - A.nodes[0]);
     __syncthreads();  // the only barrier: the waves work on their own batches from here on
     const ClimbPlan P{s_base, s_cnt, s_off, s_S, L, s_base[0], s_S[0], A.pbits};
     const uint64_t pmask = (1ull << A.pbits) - 1ull;
-    const uint32_t n = FIRST ? A.M : *Q.in_n;
-    const uint64_t *__restrict__ keys = FIRST ? A.pos : Q.in_key;
-    const uint32_t nb_cap = (uint32_t)((Q.in_cap + 63) / 64), nwaves = gridDim.x * (CW_THREADS / 64);
+    const uint32_t n = A.M;
+    const uint64_t *__restrict__ keys = A.pos;
+    const uint32_t nb_cap = (n + 63) / 64, nwaves = gridDim.x * (CW_THREADS / 64);
     for (uint32_t bt = blockIdx.x * (CW_THREADS / 64) + (tid >> 6); bt < nb_cap; bt += nwaves) {
         // ---- the batch's entries / survivors that climb ----
         const uint32_t s = bt * 64 + lane;
@@ -322,23 +343,14 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
         uint64_t x = 0, pn = 0, pp1 = 0;
         uint32_t d[8];
         uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
-        int l = Q.l0;
+        int l = 0;
         if (s < n) {
             const uint64_t key = keys[s];
             t = (uint32_t)(key >> A.pbits);
-            if (FIRST) {
-                if ((s + 1 == n || keys[s + 1] != key) && t < A.k && s_miss[t] == 0) {
-                    lo = s;
-                    while (lo > 0 && keys[lo - 1] == key) --lo;  // earlier writes of the same key
-                    load_digest(A.bdig + 32ull * A.bidx[s], d);
-                    surv = true;
-                }
-            } else {
+            if ((s + 1 == n || keys[s + 1] != key) && t < A.k && s_miss[t] == 0) {
                 lo = s;
-                const uint4 *dp = reinterpret_cast<const uint4 *>(Q.in_dig) + 2ull * s;
-                const uint4 a = dp[0], b = dp[1];
-                d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
-                d[4] = b.x; d[5] = b.y; d[6] = b.z; d[7] = b.w;
+                while (lo > 0 && keys[lo - 1] == key) --lo;  // earlier writes of the same key
+                load_digest(A.bdig + 32ull * A.bidx[s], d);
                 surv = true;
             }
             if (surv) {
@@ -348,7 +360,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 x = (P.goff + (key & pmask)) >> l;
                 uint64_t sib = 0;
                 if (classify(P, t, l, x, pn, pp1, &sib) == CL_CLEAN) {
-                    load_raw(s_nodes[t] + 32 * sib, n0, n1);
+                    g_load_raw(gptr(s_nodes[t]) + 32 * sib, n0, n1);
                     have = 1;
                 }
             }
@@ -357,10 +369,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             // ---- compaction: survivor k -> slot k / lane k (key order kept), through the wave's LDS ----
             const uint64_t m = __ballot(surv);
             const uint32_t c = (uint32_t)__popcll(m);
-            if (c == 0) {
-                if (Q.out_cnt && lane == 0) Q.out_cnt[bt] = 0;
-                break;
-            }
+            if (c == 0) break;
             if (surv) {
                 const uint32_t k = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 q_x[k] = x;
@@ -389,14 +398,11 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
 #pragma unroll
                 for (int i = 0; i < 8; ++i) d[i] = q_d[i][lane];
             }
-            if (l == Q.lstop) {  // hand the batch's dirty nodes at this level to the next pass
+            if (l == A.lstop) {  // dense from here: the reduction rehashes the levels above whole
                 if (act) {
-                    Q.out_key[bt * 64ull + lane] = ((uint64_t)t << A.pbits) | ((x << l) - P.goff);
-                    uint4 *dp = reinterpret_cast<uint4 *>(Q.out_dig) + 2ull * (bt * 64ull + lane);
-                    dp[0] = make_uint4(d[0], d[1], d[2], d[3]);
-                    dp[1] = make_uint4(d[4], d[5], d[6], d[7]);
+                    g_store_digest(gptr(s_nodes[t]) + 32 * (P.off[l] + (x - P.base[l])), d);
+                    atomicAdd(&s_lc[t * L + l], 1u);
                 }
-                if (lane == 0) Q.out_cnt[bt] = c;
                 break;
             }
             // ---- this level: lane k holds dirty node k ----
@@ -406,12 +412,12 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             bool hash = false;
             uint32_t sg[8];
             if (act) {
-                uint8_t *np = s_nodes[t] + 32 * (P.off[l] + (x - P.base[l]));
+                g_u8 *np = gptr(s_nodes[t]) + 32 * (P.off[l] + (x - P.base[l]));
                 atomicAdd(&s_lc[t * L + l], 1u);  // node (l, x) is dirty: stored below in every branch
                 if (cls == CL_TOP) {
-                    store_digest(np, d);
+                    g_store_digest(np, d);
                 } else if (cls == CL_PROMO) {
-                    store_digest(np, d);
+                    g_store_digest(np, d);
                     surv = true;
                 } else if (cls == CL_CLEAN) {
                     if (have) {
@@ -419,24 +425,28 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                         const uint4 b = make_uint4(q_s[4][lane], q_s[5][lane], q_s[6][lane], q_s[7][lane]);
                         raw_to_words(a, b, sg);
                     }
-                    else load_digest(s_nodes[t] + 32 * sib, sg);  // (not expected: read one level ahead)
-                    store_digest(np, d);
+                    else {  // (not expected: read one level ahead)
+                        uint4 a, b;
+                        g_load_raw(gptr(s_nodes[t]) + 32 * sib, a, b);
+                        raw_to_words(a, b, sg);
+                    }
+                    g_store_digest(np, d);
                     hash = surv = true;
                 } else if ((x & 1) && lane > 0) {  // right sibling of lane - 1, which stops: merge here
 #pragma unroll
                     for (int i = 0; i < 8; ++i) sg[i] = q_d[i][lane - 1];
                     lo = q_lo[lane - 1];
                     pp1 = q_pp[lane - 1];
-                    store_digest(np, d);
+                    g_store_digest(np, d);
                     hash = surv = true;
                 } else if (!(x & 1) && lane + 1 < c) {
-                    store_digest(np, d);  // left sibling of lane + 1, which goes on
+                    g_store_digest(np, d);  // left sibling of lane + 1, which goes on
                 } else {
                     // the sibling's entries belong to another batch: rendezvous at entry boundary b
                     const bool right = x & 1;
                     const uint64_t b = right ? lo : (uint64_t)hi + 1;
-                    store_digest(np, d);
-                    uint64_t *mb = reinterpret_cast<uint64_t *>(Q.mbox) + b * MBOX_WORDS;
+                    g_store_digest(np, d);
+                    uint64_t *mb = reinterpret_cast<uint64_t *>(A.mbox) + b * MBOX_WORDS;
                     uint64_t *mine = mb + (right ? MBOX_SIDE_WORDS : 0), *other = mb + (right ? 0 : MBOX_SIDE_WORDS);
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
@@ -446,7 +456,7 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                                        __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(mine + 5, right ? pn : pp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    uint32_t *bw = Q.bflags + (b >> 5);
+                    uint32_t *bw = A.bflags + (b >> 5);
                     const uint32_t bit = 1u << (b & 31);
                     const uint32_t old = __hip_atomic_fetch_or(bw, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (old & bit) {  // second arriver: the other side's data is complete
@@ -474,8 +484,8 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                 have = 0;
                 if (surv) {
                     uint64_t sib2 = 0;
-                    if (l + 1 != Q.lstop && classify(P, t, l + 1, x >> 1, pn, pp1, &sib2) == CL_CLEAN) {
-                        load_raw(s_nodes[t] + 32 * sib2, n0, n1);
+                    if (l + 1 != A.lstop && classify(P, t, l + 1, x >> 1, pn, pp1, &sib2) == CL_CLEAN) {
+                        g_load_raw(gptr(s_nodes[t]) + 32 * sib2, n0, n1);
                         have = 1;
                     }
                 }
@@ -507,23 +517,6 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
         }
     }
 }
-
-// Survivors of a pass, batch by batch (count per batch, records at batch * 64 + r), packed in order:
-// record j of batch b goes to off[b] + j (off = exclusive scan of the counts). One wave per batch.
-__global__ __launch_bounds__(256) void k_climb_pack(const uint32_t *__restrict__ cnt, const uint32_t *__restrict__ off,
-                                                    uint32_t nb, const uint64_t *__restrict__ key,
-                                                    const uint32_t *__restrict__ dig, uint64_t *__restrict__ okey,
-                                                    uint32_t *__restrict__ odig) {
-    const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (b >= nb || lane >= cnt[b]) return;
-    const uint64_t i = b * 64ull + lane, o = off[b] + lane;
-    okey[o] = key[i];
-    const uint4 *s = reinterpret_cast<const uint4 *>(dig) + 2 * i;
-    uint4 *d = reinterpret_cast<uint4 *>(odig) + 2 * o;
-    d[0] = s[0];
-    d[1] = s[1];
-}
-
 
 constexpr int UM_THREADS = 256, UM_ITEMS = 8, UM_TILE = UM_THREADS * UM_ITEMS;
 
@@ -689,17 +682,9 @@ uint32_t climb_grid(uint64_t m) {
 }
 size_t climb_mbox_bytes(uint64_t m) { return (m + 2) * MBOX_WORDS * 8; }
 
-void launch_dirty_climb_pass(const ClimbArgs &A, const ClimbPass &Q, bool first, hipStream_t st) {
-    if (!A.M || !A.k || !Q.in_cap) return;
-    const uint32_t g = climb_grid(Q.in_cap);
-    if (first) hipLaunchKernelGGL(k_dirty_climb<true>, dim3(g), dim3(CW_THREADS), 0, st, A, Q);
-    else hipLaunchKernelGGL(k_dirty_climb<false>, dim3(g), dim3(CW_THREADS), 0, st, A, Q);
-    MKV_LAUNCH_CHECK();
-}
-void launch_climb_pack(const uint32_t *cnt, const uint32_t *off, uint32_t nb, const uint64_t *key, const uint32_t *dig,
-                       uint64_t *okey, uint32_t *odig, hipStream_t st) {
-    if (!nb) return;
-    hipLaunchKernelGGL(k_climb_pack, dim3((uint32_t)ceil_div(nb, 4)), dim3(256), 0, st, cnt, off, nb, key, dig, okey, odig);
+void launch_dirty_climb(const ClimbArgs &A, hipStream_t st) {
+    if (!A.M || !A.k) return;
+    hipLaunchKernelGGL(k_dirty_climb, dim3(climb_grid(A.M)), dim3(CW_THREADS), 0, st, A);
     MKV_LAUNCH_CHECK();
 }
 

@@ -153,6 +153,10 @@ struct FusePlan {
     // also written to in[c], so the sorted leaf level is produced by the reduction itself.
     const uint32_t *perm;
     const uint8_t *dig;
+    // Several trees of one level plan in one launch (grid.y = nz, the dirty update's rehash above the
+    // climb): tree z's arrays sit ztab[z] bytes (two's complement) from the ones named above. null: one.
+    const uint64_t *ztab;
+    uint32_t nz;
 };
 void launch_reduce_fused(const FusePlan &p, hipStream_t st);
 // Every remaining level in one launch (k_reduce_top): ntiles <= RD_TOP_TILES tiles of 512 parents fuse
@@ -172,7 +176,9 @@ struct TopPlan {
     uint64_t tile0, ntiles;
     const uint32_t *perm;
     const uint8_t *dig;
-    uint32_t *arrive;
+    uint32_t *arrive;        // tree z: arrive[16 z] (one 64-B line per tree)
+    const uint64_t *ztab;    // as FusePlan
+    uint32_t nz;
 };
 void launch_reduce_top(const TopPlan &p, hipStream_t st);
 
@@ -291,9 +297,13 @@ struct LevelPlan {
     uint64_t base[MKV_MAXLEV], cnt[MKV_MAXLEV], off[MKV_MAXLEV], S[MKV_MAXLEV];
     int L;
 };
-// The dirty climb of k replicas sharing a level plan (k_update.hip k_dirty_climb), in passes: pos / bidx
-// = the batch entries sorted by (tree << pbits | leaf position) with their batch indices, bdig = the batch
-// digests; cnt[q][l]: tree q's dirty nodes per level (added to; zeroed by the caller).
+// The dirty climb of k replicas sharing a level plan (k_update.hip k_dirty_climb): pos / bidx = the batch
+// entries sorted by (tree << pbits | leaf position) with their batch indices, bdig = the batch digests;
+// cnt[q][l]: tree q's dirty nodes per level (added to; zeroed by the caller). The climb stops at level
+// lstop (-1: the top), where the dirty nodes are dense; the levels above are rehashed whole by the
+// reduction (run_reduce from lstop, every tree in one launch: ztab = the trees' node-array offsets from
+// tree 0's, written by the climb). bflags: one bit per entry boundary, all-zero before and after; mbox:
+// climb_mbox_bytes(M) of scratch.
 struct ClimbArgs {
     const uint64_t *pos;
     const uint32_t *bidx;
@@ -305,29 +315,14 @@ struct ClimbArgs {
     const uint32_t *missing[DIRTY_MAX_TREES];  // non-zero: a batch key of that tree is not a leaf, tree untouched
     uint32_t *cnt[DIRTY_MAX_TREES];
     LevelPlan P;
-};
-// One pass: inputs = the sorted batch entries (first pass) or the previous pass's packed survivors
-// (in_key = tree << pbits | first leaf, in_dig = 8 big-endian digest words, *in_n of them, at most in_cap),
-// all nodes at level l0; survivors reaching level lstop are written per 64-input batch b at b * 64 + r
-// (out_cnt[b] of them; out_* null when the pass climbs to the top). bflags: one bit per input boundary,
-// all-zero before and after; mbox: climb_mbox_bytes(in_cap) of scratch.
-struct ClimbPass {
-    const uint64_t *in_key;
-    const uint32_t *in_dig;
-    const uint32_t *in_n;
-    uint64_t in_cap;
-    int l0, lstop;
-    uint64_t *out_key;
-    uint32_t *out_dig;
-    uint32_t *out_cnt;
+    int lstop;
     uint32_t *bflags;
     uint8_t *mbox;
+    uint64_t *ztab;
 };
 uint32_t climb_grid(uint64_t m);
 size_t climb_mbox_bytes(uint64_t m);
-void launch_dirty_climb_pass(const ClimbArgs &A, const ClimbPass &Q, bool first, hipStream_t st);
-void launch_climb_pack(const uint32_t *cnt, const uint32_t *off, uint32_t nb, const uint64_t *key, const uint32_t *dig,
-                       uint64_t *okey, uint32_t *odig, hipStream_t st);
+void launch_dirty_climb(const ClimbArgs &A, hipStream_t st);
 
 // Batch merge (k_update.hip): A = the tree's sorted leaves (dig = leaf level, indexed by position),
 // B = sorted unique batch (perm = batch storage index, dig = batch digests in storage order, tomb =

@@ -290,7 +290,8 @@ struct mkv_tree {
     const uint64_t *rt_koff = nullptr, *rt_voff = nullptr;
     // incremental update: batch staging, positions, dirty lists, dirty-node bitmap (all-zero between calls)
     DevBuf u_kb, u_koff, u_vb, u_voff, u_dig, u_pos, u_pos2, u_idx, u_idx2, u_cnt, u_bf, u_mbox;
-    DevBuf u_ckey, u_cdig, u_ccnt, u_coff, u_pk0, u_pd0, u_pk1, u_pd1;  // dirty climb: pass outputs / packed inputs
+    DevBuf u_ztab;        // climb -> reduction: the group's node-array offsets from t0's
+    int upd_dense_from = -1;  // last dirty update: levels above this one were rehashed whole
     // batch merge (key-set changes): batch tombstones, merged prefixes / permutation / levels, count
     DevBuf u_tomb, m_pfx, m_perm, m_nodes, m_cnt;
     uint64_t bf_words = 0;  // words of u_bf known to be zero (every climb leaves them all-zero)
@@ -738,8 +739,13 @@ uint64_t total_nodes(const mkv_tree *t) {
 // gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch. Leaves whose
 // parent is not owned (at most the first and the last of a shard) are gathered directly; a plan without
 // an owned level-1 node (single leaf, or a one-leaf shard) gathers everything directly.
-void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, const uint8_t *gdig = nullptr) {
+// l0 > 0: the levels above l0 only (level l0 is complete in nodes). ztab/nz: nz trees of t's level plan in
+// one launch per step, tree z's node array at nodes + ztab[z] (device table; the dirty update's rehash
+// above the climb).
+void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, const uint8_t *gdig = nullptr,
+                size_t l0 = 0, const uint64_t *ztab = nullptr, uint32_t nz = 1) {
     const size_t L = t->lev_S.size();
+    if (l0 > 0) gperm = nullptr;
     if (gperm) {
         if (L < 2 || t->lev_cnt[1] == 0) {
             launch_gather_digests(gperm, gdig, L ? t->lev_cnt[0] : 0, nodes, t->st);
@@ -752,7 +758,7 @@ void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, co
                 launch_gather_digests(gperm + (c0 - 1), gdig, 1, nodes + 32 * (c0 - 1), t->st);
         }
     }
-    size_t l = 0;
+    size_t l = l0;
     while (l + 1 < L && t->lev_cnt[l] > 0) {
         if (t->lev_cnt[l + 1] == 0) break;
         const uint64_t a1 = t->lev_base[l + 1], c1 = t->lev_cnt[l + 1];
@@ -764,10 +770,13 @@ void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, co
         size_t nown = 0;
         while (nown < remaining && t->lev_cnt[l + 1 + nown] > 0) ++nown;
         if (ntiles <= RD_TOP_TILES && nown <= (size_t)TOP_MAX_LEVELS) {
-            const bool fresh = t->rd_arrive.p == nullptr;
-            uint32_t *arrive = ens<uint32_t>(t->rd_arrive, 16);
-            if (fresh) MKV_HIP(hipMemsetAsync(arrive, 0, 64, t->st));
+            // one counter line per tree; every counter is 0 between launches, so zeroed on (re)allocation
+            const bool fresh = t->rd_arrive.p == nullptr || t->rd_arrive.cap < 64ull * nz;
+            uint32_t *arrive = ens<uint32_t>(t->rd_arrive, 16ull * nz);
+            if (fresh) MKV_HIP(hipMemsetAsync(arrive, 0, t->rd_arrive.cap, t->st));
             TopPlan p{};
+            p.ztab = ztab;
+            p.nz = nz;
             p.in = nodes + 32 * t->lev_off[l];
             p.a[0] = t->lev_base[l];
             p.c[0] = t->lev_cnt[l];
@@ -792,6 +801,8 @@ void run_reduce(mkv_tree *t, uint8_t *nodes, const uint32_t *gperm = nullptr, co
         }
         const size_t nl = std::min<size_t>(remaining, ntiles == 1 ? MAX_FUSE : 4);
         FusePlan p{};
+        p.ztab = ztab;
+        p.nz = nz;
         p.in = nodes + 32 * t->lev_off[l];
         p.a[0] = t->lev_base[l];
         p.c[0] = t->lev_cnt[l];
@@ -1782,55 +1793,20 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             CA.P.off[l] = t0->lev_off[l];
             CA.P.S[l] = t0->lev_S[l];
         }
-        // Passes: a wave climbs its 64 entries while they are spread (one dirty node per lane), and stops
-        // where they start to merge (the level whose nodes span the mean gap between dirty leaves, + 1);
-        // the survivors are packed across waves and the next pass climbs 6 more levels in full waves, and
-        // so on to the top.
+        // The climb (one wave per 64 entries) runs while the dirty nodes are spread, and stops at the level
+        // whose nodes span the mean gap between dirty leaves (floor(log2(gap)) + 1: about half of its nodes
+        // are dirty); the reduction then rehashes every level above it, all trees in one launch per step.
         const uint64_t gap = std::max<uint64_t>(1, t0->n / std::max<uint64_t>(1, mmax));
-        int lstop = std::max(1, bits_for(gap));  // floor(log2(gap)) + 1
+        const int lstop = std::max(1, bits_for(gap));
+        const bool dense_top = lstop < (int)L - 1;
+        CA.lstop = dense_top ? lstop : -1;
+        CA.bflags = bflags;
+        CA.mbox = reinterpret_cast<uint8_t *>(t0->u_mbox.ensure(climb_mbox_bytes(M)));
+        CA.ztab = ens<uint64_t>(t0->u_ztab, DIRTY_MAX_TREES);
         const size_t pclimb = prof_begin(t0, "climb", st);
-        ClimbPass Q{};
-        Q.bflags = bflags;
-        Q.mbox = reinterpret_cast<uint8_t *>(t0->u_mbox.ensure(climb_mbox_bytes(M)));
-        Q.in_cap = M;
-        Q.l0 = 0;
-        bool first = true;
-        int cur = 0;  // which packed buffer holds this pass's inputs
-        while (true) {
-            const bool last = lstop >= (int)L - 1;
-            Q.lstop = last ? -1 : lstop;
-            const uint64_t nb = ceil_div(Q.in_cap, 64);
-            if (!last) {
-                Q.out_key = ens<uint64_t>(t0->u_ckey, nb * 64);
-                Q.out_dig = ens<uint32_t>(t0->u_cdig, nb * 64 * 8);
-                Q.out_cnt = ens<uint32_t>(t0->u_ccnt, nb + 1);
-            } else {
-                Q.out_key = nullptr;
-                Q.out_dig = nullptr;
-                Q.out_cnt = nullptr;
-            }
-            launch_dirty_climb_pass(CA, Q, first, st);
-            if (last) break;
-            // pack the survivors (dirty nodes at level lstop) for the next pass
-            DevBuf &pk = cur ? t0->u_pk0 : t0->u_pk1, &pd = cur ? t0->u_pd0 : t0->u_pd1;
-            uint64_t bound = 0;
-            for (uint32_t q = 0; q < k2; ++q) bound += t0->lev_cnt[lstop];
-            bound = std::min<uint64_t>(bound, nb * 64);
-            uint32_t *off = ens<uint32_t>(t0->u_coff, nb + 2);
-            void *scr = t0->s_radix.ensure(std::max(radix_scratch_bytes(M), scan_scratch_bytes(nb + 1)));
-            exclusive_scan_u32(Q.out_cnt, off, nb, off + nb + 1, scr, st);
-            uint64_t *nkey = ens<uint64_t>(pk, bound + 1);
-            uint32_t *ndig = ens<uint32_t>(pd, (bound + 1) * 8);
-            launch_climb_pack(Q.out_cnt, off, (uint32_t)nb, Q.out_key, Q.out_dig, nkey, ndig, st);
-            Q.in_key = nkey;
-            Q.in_dig = ndig;
-            Q.in_n = off + nb + 1;
-            Q.in_cap = bound;
-            Q.l0 = lstop;
-            lstop += 6;
-            first = false;
-            cur ^= 1;
-        }
+        launch_dirty_climb(CA, st);
+        if (dense_top) run_reduce(t0, t0->nodes.as<uint8_t>(), nullptr, nullptr, (size_t)lstop, CA.ztab, k2);
+        for (size_t q = 0; q < g.size(); ++q) ts[g[q]]->upd_dense_from = dense_top ? lstop : -1;
         prof_end(t0, pclimb);
         // every tree's missing-key count and root, read back by one launch
         SmallCopies SC{};
@@ -1863,7 +1839,8 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             else prof_collect(t);
             ok[g[q]] = reinterpret_cast<volatile uint32_t *>(t->h_small)[0] == 0;
             if (ok[g[q]] && !t->sharded) std::memcpy(t->root, t->h_small + 16, 32);
-            if (!ok[g[q]]) {  // tree untouched
+            if (!ok[g[q]]) {  // tree untouched (the rehash above the climb rewrote the same digests)
+                t->upd_dense_from = -1;
                 t->has_root = had_root[q];
                 t->combine_pending = had_pending[q];
             }
@@ -3385,7 +3362,8 @@ mkv_status mkv_tree_update_counts(const mkv_tree *t, uint64_t *out, uint32_t cap
         std::vector<uint32_t> h(L);
         MKV_HIP(hipStreamSynchronize(t->st));
         MKV_HIP(hipMemcpy(h.data(), t->u_cnt.p, 4ull * L, hipMemcpyDeviceToHost));
-        for (uint32_t l = 0; l < L && l < cap; ++l) out[l] = h[l];
+        for (uint32_t l = 0; l < L && l < cap; ++l)  // levels above the climb: rehashed whole
+            out[l] = (t->upd_dense_from >= 0 && (int)l > t->upd_dense_from) ? t->lev_cnt[l] : h[l];
     });
 }
 

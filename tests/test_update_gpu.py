@@ -535,3 +535,44 @@ def test_value_only_diffs_take_the_topdown_walk():
         assert split_blob(raw, offs) == e
     ws = base.walk_stats()
     assert ws["launches"] > 0 and ws["divergent_positions"] == sum(len(e) for e in expect)
+
+
+@pytest.mark.parametrize("n,dens", [(300007, "sparse"), (300007, "medium"), (300007, "dense"), (4099, "dense"),
+                                    (131072, "runs")])
+def test_dirty_climb_passes_and_rendezvous_vs_oracle(n, dens):
+    """The dirty climb (k_update.hip k_dirty_climb) in every regime its passes take: sparse batches (one
+    dirty leaf per ~1000: every wave's lanes climb apart, merge at the pass boundaries and across waves),
+    medium and dense ones (most merges inside a wave; a batch 3x the tree with duplicates), and long runs
+    of one key (130 writes of a key straddle the 64-entry batches of the first pass; the last write wins,
+    merkle.rs:54). Five replicas in one batched call (upsert_device_many), then every level array of every
+    replica against the oracle's insert-then-rebuild (merkle.rs:52-56, :73-121)."""
+    import torch
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    rng = np.random.default_rng(n + len(dens))
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    trees = [base.clone() for _ in range(5)]
+    keep, batches, expect = [], [], []
+    for r in range(5):
+        m = {"sparse": max(1, n // 1000), "medium": n // 50, "dense": 3 * n, "runs": 200}[dens] + 17 * r
+        idx = list(rng.integers(0, n, size=m))
+        if dens == "runs":
+            hot = int(rng.integers(0, n))
+            idx = idx[:40] + [hot] * 130 + idx[40:] + [n - 1]
+        ks = [keys[int(i)] for i in idx]
+        vs = [b"climb-%d-%d-%d" % (r, j, int(i)) for j, i in enumerate(idx)]
+        bk, bo = pack(ks)
+        bv, bvo = pack(vs)
+        d = [torch.from_numpy(bk.copy()).cuda(), torch.from_numpy(bo.astype(np.int64)).cuda(),
+             torch.from_numpy(bv.copy()).cuda(), torch.from_numpy(bvo.astype(np.int64)).cuda()]
+        keep.append(d)
+        batches.append((d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), len(ks)))
+        expect.append(o.upsert(bk, bo, bv, bvo))
+    torch.cuda.synchronize()
+    MerkleTree.upsert_device_many(trees, batches)
+    for r in range(5):
+        assert trees[r].get_root_hash() == expect[r].root(), r
+        assert _levels(trees[r]) == _oracle_levels(expect[r]), r
+        assert sum(trees[r].update_counts()) > 0  # the dirty path ran (no fallback to the batch merge)
