@@ -96,17 +96,14 @@ __device__ __forceinline__ int cmp_merge(const DiffSide &A, uint64_t i, uint64_t
 
 // Partition, one wave per group of PART_STRIDE tiles (one launch). The group's two boundary splits
 // (tiles t0 and t1 = min(t0 + PART_STRIDE, ntiles)) by a cooperative search: lanes 0-31 search t0's
-// diagonal, lanes 32-63 t1's, each half probing PART_PROBES points per step (9-ary: 100M keys in ~9
-// dependent round trips instead of ~27 for a binary search). Then lane l computes tile t0 + l's split inside that
+// diagonal, lanes 32-63 t1's, each half probing 32 points per round (below). Then lane l computes tile t0 + l's split inside that
 // bracket: the split is monotone in the diagonal, so it lies between the two boundary splits; start at
 // their linear interpolation (exact for near-identical replicas up to the few inserts/deletes in
 // between), gallop outwards, then binary search the bracket — probes within a few cache lines that
 // neighbouring tiles share.
 constexpr uint64_t PART_STRIDE = 64;
-// Probes per boundary and step ((PART_PROBES + 1)-ary search, <= 32). The searches are bound by their
-// probe traffic (each probe pulls two cache lines for 16 B): 9-ary (~9 dependent steps at 100M) measured
-// faster than 33-ary (~6 steps, 0.5 GB of probes per diff): 100M mixed 1.70-1.72 -> 1.67-1.69 ms.
-constexpr uint32_t PART_PROBES = 8;
+// Probes per boundary and round: a half wave (the exponential first round needs all 32).
+constexpr uint32_t PART_PROBES = 32;
 
 // pred(a): A[a] precedes B[d-1-a] in the merge (A first on equal keys), i.e. the split of diagonal d is
 // > a. Valid for max(0, d - B.n) <= a < min(d, A.n).
@@ -130,29 +127,45 @@ __global__ __launch_bounds__(256) void k_diff_partition(DiffSide A, DiffSide B, 
     const uint64_t t0 = g * PART_STRIDE, t1 = t0 + PART_STRIDE < ntiles ? t0 + PART_STRIDE : ntiles;
     const uint32_t half = lane >> 5, k = lane & 31;
     // ---- boundary splits: half h searches diagonal dh; answer in [lo, hi] ----
+    // Round 0: 32 probes at exponentially spaced offsets (0, +-1, +-3, ... +-65535) around the interpolated
+    // split d * |A| / (|A| + |B|): replicas that agree on most keys have their split within a few hundred
+    // positions of it, so the bracket shrinks to about that distance in one round; then 33-ary rounds. At
+    // 100M mixed: ~3 dependent rounds instead of ~9 of the plain 9-ary search, and most probes away from the
+    // split compare unequal prefixes (no digest reads).
     const uint64_t dh = half ? (t1 * WTILE < M ? t1 * WTILE : M) : t0 * WTILE;
     uint64_t lo = dh > B.n ? dh - B.n : 0, hi = dh < A.n ? dh : A.n;
+    const uint64_t guess = (uint64_t)((double)dh * ((double)A.n / (double)(M ? M : 1)));
+    bool first = true;
     while (__any(lo < hi)) {
         const uint64_t n = hi - lo;
-        const bool act = lo < hi;
+        const bool act = lo < hi, expo = first && n > PART_PROBES;
         uint64_t p = 0;
         bool pv = false;
         if (act) {
-            p = n <= PART_PROBES ? lo + k : lo + ((uint64_t)(k + 1) * n) / (PART_PROBES + 1);
-            pv = k < PART_PROBES && (n > PART_PROBES || k < n) && part_pred(A, B, dh, p);
+            if (expo) {
+                const int64_t off = k < 16 ? -(int64_t)((1u << (16 - k)) - 1u) : (int64_t)((1u << (k - 16)) - 1u);
+                int64_t q = (int64_t)guess + off;
+                q = q < (int64_t)lo ? (int64_t)lo : q;
+                q = q > (int64_t)hi - 1 ? (int64_t)hi - 1 : q;
+                p = (uint64_t)q;
+            } else {
+                p = n <= PART_PROBES ? lo + k : lo + ((uint64_t)(k + 1) * n) / (PART_PROBES + 1);
+            }
+            pv = (n > PART_PROBES || k < n) && part_pred(A, B, dh, p);
         }
         const uint32_t m = (uint32_t)(__ballot(pv) >> (32 * half));
-        const uint32_t c = (uint32_t)__popc(m);  // preds are monotone: c leading trues
+        const uint32_t c = (uint32_t)__popc(m);  // preds are monotone in p: c leading trues
+        const uint64_t pc1 = __shfl(p, (int)(32 * half + (c ? c - 1 : 0)));            // last true probe
+        const uint64_t pc = __shfl(p, (int)(32 * half + (c < PART_PROBES ? c : 0)));  // first false probe
         if (act) {
             if (n <= PART_PROBES) {
                 lo = hi = lo + c;
             } else {
-                const uint64_t pc1 = c ? lo + ((uint64_t)c * n) / (PART_PROBES + 1) : 0;                   // p_{c-1}
-                const uint64_t pc = c < PART_PROBES ? lo + ((uint64_t)(c + 1) * n) / (PART_PROBES + 1) : hi;  // p_c
                 if (c) lo = pc1 + 1;
-                hi = pc;
+                if (c < PART_PROBES) hi = pc;
             }
         }
+        first = false;
     }
     const uint64_t s0 = __shfl(lo, 0), s1 = __shfl(lo, 32);
     if (lane == 0) split[t0] = s0;
@@ -173,17 +186,26 @@ __global__ __launch_bounds__(256) void k_diff_partition(DiffSide A, DiffSide B, 
     if (gs < lo) gs = lo;
     if (gs > hi) gs = hi;
     uint64_t L = lo, H = hi;  // answer in [L, H]
-    if (gs < hi && part_pred(A, B, d, gs)) {
+    // The split is gs exactly when pred(gs - 1) holds and pred(gs) does not: both tested at once (their
+    // prefixes are two adjacent pairs, one round trip; unequal prefixes in the common case, so no digest
+    // reads), else gallop from the side they point to.
+    const uint64_t pa0 = gs > lo ? A.pfx[gs - 1] : 0, pa1 = gs < hi ? A.pfx[gs] : 0;
+    const uint64_t pb0 = gs > lo ? B.pfx[d - gs] : 0, pb1 = gs < hi ? B.pfx[d - 1 - gs] : 0;
+    const bool below = gs == lo || (pa0 != pb0 ? pa0 < pb0 : cmp_merge(A, gs - 1, pa0, B, d - gs, pb0) <= 0);
+    const bool at = gs < hi && (pa1 != pb1 ? pa1 < pb1 : cmp_merge(A, gs, pa1, B, d - 1 - gs, pb1) <= 0);
+    if (below && !at) {
+        L = H = gs;
+    } else if (at) {
         L = gs + 1;
-        for (uint64_t step = 1;; step <<= 1) {
-            const uint64_t q = gs + step;
+        for (uint64_t step = 2;; step <<= 1) {
+            const uint64_t q = gs + step - 1;
             if (q >= hi) break;
             if (!part_pred(A, B, d, q)) { H = q; break; }
             L = q + 1;
         }
-    } else {
-        H = gs;
-        for (uint64_t step = 1;; step <<= 1) {
+    } else {  // pred(gs - 1) false: the split is below gs
+        H = gs - 1;
+        for (uint64_t step = 2;; step <<= 1) {
             if (gs < lo + step) break;
             const uint64_t q = gs - step;
             if (part_pred(A, B, d, q)) { L = q + 1; break; }
@@ -597,30 +619,46 @@ __global__ __launch_bounds__(256) void k_diff_pass2(DiffSide A, DiffSide B, cons
         }
         return;
     }
-    // one wave per 64 tiles: lane q reads tile (64 w + q)'s count, the wave then emits only the tiles
-    // with divergent outputs (~23 % at 0.1 % divergence), one after another (one workgroup per tile left
-    // ~100K mostly idle workgroups to dispatch)
+    // one wave per 64 tiles: lane q reads tile (64 w + q)'s count, output offset and split in one round
+    // trip, then the wave emits only the tiles with divergent outputs (~23 % at 0.1 % divergence), taking
+    // a tile's offset / split from its lane (shuffles), the packed words of 8 live tiles loaded at once
+    // (one workgroup per tile left ~100K mostly idle workgroups to dispatch; a dependent load chain per
+    // live tile cost ~50 us at 100M)
     const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t t0 = w * 64;
     if (t0 >= nt) return;  // wave-uniform
-    uint64_t live = __ballot(t0 + lane < nt && tilecnt[t0 + lane] != 0);
+    const bool tv = t0 + lane < nt;
+    const uint64_t mycnt = tv ? tilecnt[t0 + lane] : 0, myoff = tv ? tileoff[t0 + lane] : 0,
+                   mysplit = tv ? split[t0 + lane] : 0;
+    uint64_t live = __ballot(mycnt != 0);
     while (live) {
-        const uint64_t t = t0 + (uint64_t)__builtin_ctzll(live);
-        live &= live - 1;
-        const uint32_t pk = packed[t * 64 + lane];
-        const uint32_t div = pk & 0xFF, fromA = (pk >> 8) & 0xFF, isplit = pk >> 16;
-        const uint32_t cnt = __popc(div);
-        uint64_t off = tileoff[t] + (wave_incl_scan<uint32_t>(cnt) - cnt);
-        if (!div) continue;
-        const TileCtx c = wave_tile(A, B, split, t);
-        const uint64_t dl = (uint64_t)lane * DI;
-        uint64_t i = c.a0 + isplit, j = c.b0 + (dl - isplit);
-        for (int s = 0; s < DI; ++s) {
-            const bool fa = (fromA >> s) & 1u;
-            const uint64_t ref = fa ? i : (j | (1ull << 63));
-            if (fa) ++i; else ++j;
-            if ((div >> s) & 1u) refs[off++] = ref;
+        // the packed words of up to PASS2_AHEAD live tiles in flight at once, then their refs
+        constexpr int PASS2_AHEAD = 8;
+        uint32_t tq[PASS2_AHEAD], pk[PASS2_AHEAD];
+#pragma unroll
+        for (int u = 0; u < PASS2_AHEAD; ++u) {
+            tq[u] = live ? (uint32_t)__builtin_ctzll(live) : 64u;
+            pk[u] = live ? packed[(t0 + tq[u]) * 64 + lane] : 0u;
+            live &= live - 1;
+        }
+#pragma unroll
+        for (int u = 0; u < PASS2_AHEAD; ++u) {
+            if (tq[u] == 64u) break;  // wave-uniform
+            const uint32_t q = tq[u];
+            const uint32_t div = pk[u] & 0xFF, fromA = (pk[u] >> 8) & 0xFF, isplit = pk[u] >> 16;
+            const uint32_t cnt = __popc(div);
+            uint64_t off = (uint64_t)__shfl((long long)myoff, (int)q) + (wave_incl_scan<uint32_t>(cnt) - cnt);
+            const uint64_t a0 = (uint64_t)__shfl((long long)mysplit, (int)q), d0 = (t0 + q) * WTILE;
+            if (!div) continue;
+            const uint64_t dl = (uint64_t)lane * DI;
+            uint64_t i = a0 + isplit, j = (d0 - a0) + (dl - isplit);
+            for (int s = 0; s < DI; ++s) {
+                const bool fa = (fromA >> s) & 1u;
+                const uint64_t ref = fa ? i : (j | (1ull << 63));
+                if (fa) ++i; else ++j;
+                if ((div >> s) & 1u) refs[off++] = ref;
+            }
         }
     }
 }

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
                                                            uint64_t off, bool lcp, uint64_t *__restrict__ pfx,
                                                            uint32_t *__restrict__ counts, uint32_t *__restrict__ zero2) {
     sort_prio();
-    if (zero2 && blockIdx.x == 0 && threadIdx.x < 8) zero2[threadIdx.x] = 0;
+    if (zero2 && blockIdx.x == 0 && threadIdx.x < 12) zero2[threadIdx.x] = 0;
     __shared__ uint32_t h[8][256];
     __shared__ uint32_t lmax, lmin;
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
@@ -456,6 +456,7 @@ __global__ __launch_bounds__(MT_THREADS) void k_mark_ties(const uint64_t *__rest
     const uint64_t lo = (uint64_t)blockIdx.x * per;
     const uint64_t hi = lo + per < tot_n ? lo + per : tot_n;
     uint32_t nt = 0, nb = 0;  // nb: block-uniform count of buffered heads
+    uint64_t fsum = 0, fxor = 0;  // key-set fingerprint: sum and xor of the sort keys (count[8..11])
     auto flush = [&]() {
         if (threadIdx.x == 0) sbase = atomicAdd(&count[1], nb);
         __syncthreads();
@@ -468,7 +469,10 @@ __global__ __launch_bounds__(MT_THREADS) void k_mark_ties(const uint64_t *__rest
         const uint64_t i = i0 + threadIdx.x;
         bool t = false, h = false;
         if (i < n) {
-            const uint64_t p = pfx[i] >> shift;
+            const uint64_t full = pfx[i];
+            fsum += full;
+            fxor ^= full;
+            const uint64_t p = full >> shift;
             t = i > 0 && p == (pfx[i - 1] >> shift);
             h = !t && i + 1 < n && (pfx[i + 1] >> shift) == p;
             tie[i] = t;
@@ -492,6 +496,17 @@ __global__ __launch_bounds__(MT_THREADS) void k_mark_ties(const uint64_t *__rest
         __syncthreads();  // wcnt is rewritten by the next iteration
     }
     if (nb) flush();
+    // key-set fingerprint: wave sums, one atomic each per wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        fsum += (uint64_t)__shfl_xor((long long)fsum, o);
+        fxor ^= (uint64_t)__shfl_xor((long long)fxor, o);
+    }
+    if (lane == 0 && (fsum | fxor)) {
+        atomicAdd(reinterpret_cast<unsigned long long *>(count + 8), (unsigned long long)fsum);
+        atomicXor(&count[10], (uint32_t)fxor);
+        atomicXor(&count[11], (uint32_t)(fxor >> 32));
+    }
     // ties: wave sums, then one atomic per block
     uint32_t x = nt;
 #pragma unroll
@@ -865,7 +880,7 @@ void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uin
     uint32_t *counts = reinterpret_cast<uint32_t *>(scratch);
     if (!zeroed) MKV_HIP(hipMemsetAsync(counts, 0, (8 * 256 + 64) * sizeof(uint32_t), st));
     if (!n) {
-        if (zero2) MKV_HIP(hipMemsetAsync(zero2, 0, 32, st));
+        if (zero2) MKV_HIP(hipMemsetAsync(zero2, 0, 48, st));
         return;
     }
     const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);

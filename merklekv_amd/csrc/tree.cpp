@@ -239,6 +239,12 @@ struct mkv_tree {
     DevBuf pfx_s;                          // locate samples of pfx (every LOC_STRIDE-th), built on demand
     uint64_t pfx_gen = 1, pfx_s_gen = 0;   // pfx_s is current while pfx_s_gen == pfx_gen
     uint64_t keyset = next_keyset();       // key-set identity (see next_keyset)
+    // Key-set fingerprint of the last sort (sum and xor of the sorted key prefixes, k_mark_ties): two trees
+    // whose fingerprints differ hold different key sets, so a diff goes straight to the merge-join instead
+    // of first trying the top-down walk (which needs equal key sets). Equal fingerprints prove nothing: the
+    // walk's own key-set screen and leaf-key checks decide as before. Cleared by key-set changes.
+    uint64_t kfp[2] = {0, 0};
+    bool kfp_ok = false;
     std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
     bool has_root = false;
     uint8_t root[32] = {0};
@@ -321,6 +327,11 @@ uint64_t mkv::tree_global_n(const mkv_tree *t) { return t->sharded ? t->gN : t->
 // Same key-set id => same sorted keys. The id is a correctness input (the batched dirty path locates a
 // replica's batch in another tree, the walks skip the leaf-key check), so the cheap host-side facts that
 // must agree are checked every time: a mismatch means some key-changing path kept a stale id.
+// Different key-set fingerprints (see mkv_tree::kfp): the key sets differ for certain.
+static bool keysets_differ(const mkv_tree *a, const mkv_tree *b) {
+    return a->kfp_ok && b->kfp_ok && (a->kfp[0] != b->kfp[0] || a->kfp[1] != b->kfp[1]);
+}
+
 static bool same_keyset(const mkv_tree *a, const mkv_tree *b) {
     if (a->keyset != b->keyset) return false;
     if (a->n != b->n || a->nstore != b->nstore || a->kbytes != b->kbytes)
@@ -573,9 +584,18 @@ void launch_clear_tomb(const uint8_t *tomb, const uint32_t *perm, uint64_t n, ui
     MKV_LAUNCH_CHECK();
 }
 
+// An empty launch in front of a window that opens on an idle stream: a marker recorded on an idle HIP
+// stream takes the completion time of the stream's last command, so the window would also count the host
+// time since then (the caller's own work between two API calls: ~0.13 ms per 100M diff call measured).
+__global__ void k_prof_anchor() {}
+
 size_t prof_begin(mkv_tree *t, const char *group, hipStream_t s = nullptr) {
     if (!t->prof) return SIZE_MAX;
     if (!s) s = t->st;
+    if (hipStreamQuery(s) == hipSuccess) {
+        hipLaunchKernelGGL(k_prof_anchor, dim3(1), dim3(64), 0, s);
+        MKV_LAUNCH_CHECK();
+    }
     if (t->evfree.empty()) {
         EvPair p;
         MKV_HIP(hipEventCreate(&p.a));
@@ -939,6 +959,8 @@ uint32_t choose_prefix_digits(const uint32_t *counts, uint64_t n, int *lo_bit) {
 struct SortedSet {
     DevBuf *pk, *pm;
     uint64_t n;
+    uint64_t fp[2];  // key-set fingerprint (sum, xor of the sort keys); valid when fp_ok
+    bool fp_ok;
 };
 // kbytes_out (optional): koff[n_in], read back with the sort's own counts (one host round trip).
 SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
@@ -1011,14 +1033,17 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     // long-run counts (misc[0], [4], [5]) and, for borrowed inputs, the key-byte total.
     if (n_in > 1) launch_refine_small(kb, koff, n_in, perm, pk, tie, misc + 4, heads, misc + 1, n_in / 2 + 1, st);
     prof_end(t, ps);
-    small_d2h(t, t->h_small, misc, 32, st);
-    if (kbytes_out && n_in) small_d2h(t, t->h_small + 4, koff + n_in, 8, st);
+    small_d2h(t, t->h_small, misc, 48, st);
+    if (kbytes_out && n_in) small_d2h(t, t->h_small + 6, koff + n_in, 8, st);
     wait_stream(t, st);
     const uint32_t *hm = reinterpret_cast<const uint32_t *>(t->h_small);
     const uint32_t nties = n_in ? hm[0] : 0, dups = hm[4], long_runs = hm[5];
+    // key-set fingerprint of the sorted keys (k_mark_ties); meaningful only without duplicates (it counts
+    // every input record) and with the key window the sort chose mixed in
+    const uint64_t fp0 = t->h_small[4] ^ (win * 0x9E3779B97F4A7C15ull), fp1 = t->h_small[5];
     if (n_in > 1 && hm[7])  // a radix pass's look-back stalled past its spin limit: the order is not trustworthy
         throw Error(ST_EHIP, "sort: a radix pass's look-back exceeded its spin limit (device stalled)");
-    if (kbytes_out) *kbytes_out = n_in ? t->h_small[4] : 0;
+    if (kbytes_out) *kbytes_out = n_in ? t->h_small[6] : 0;
     static const bool dbg_sort = getenv("MKV_DEBUG_SORT") != nullptr;
     if (dbg_sort)
         fprintf(stderr, "[mkv sort] n=%llu win=%llu lo_bit=%d digits=0x%x ties=%u heads=%u\n", (unsigned long long)n_in,
@@ -1057,7 +1082,7 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         launch_pfx_from_window(pkbuf->as<uint64_t>(), n, shared8, (uint32_t)std::min<uint64_t>(win, 8), st);
         prof_end(t, pf);
     }
-    return SortedSet{pkbuf, pmbuf, n};
+    return SortedSet{pkbuf, pmbuf, n, {fp0, fp1}, dups == 0 && n == n_in};
 }
 
 // fused_kcap: the leaf kernels copied the borrowed keys into t->kb (capacity fused_kcap bytes; complete
@@ -1079,6 +1104,9 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     swap_buf(t->pfx, *pkbuf);
     ++t->pfx_gen;
     t->keyset = next_keyset();
+    t->kfp[0] = S.fp[0];
+    t->kfp[1] = S.fp[1];
+    t->kfp_ok = S.fp_ok;
     swap_buf(t->perm, *pmbuf);
     perm = t->perm.as<uint32_t>();
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
@@ -1422,6 +1450,9 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         dst->n = src->n;
         dst->nstore = src->nstore;
         dst->keyset = src->keyset;
+        dst->kfp[0] = src->kfp[0];
+        dst->kfp[1] = src->kfp[1];
+        dst->kfp_ok = src->kfp_ok;
         dst->kbytes = src->kbytes;
         dst->lev_cnt = src->lev_cnt;
         dst->lev_off = src->lev_off;
@@ -1603,6 +1634,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     swap_buf(t->pfx, t->m_pfx);
     ++t->pfx_gen;
     t->keyset = next_keyset();
+    t->kfp_ok = false;  // merged key set: no fingerprint
     swap_buf(t->perm, t->m_perm);
     swap_buf(t->nodes, t->m_nodes);
     t->kbytes = kbytes + kbn;
@@ -2548,7 +2580,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
     uint64_t m = 0;
     bool done = false;
     const uint64_t nwords = (A.n + 31) / 32;
-    if (!dev && A.n > 0 && same_plan(a, b) && !a->sharded && !b->sharded && a->lev_S.size() > 1 &&
+    if (!dev && A.n > 0 && same_plan(a, b) && !keysets_differ(a, b) && !a->sharded && !b->sharded && a->lev_S.size() > 1 &&
         ceil_div(nwords, 1024) <= 8192) {
         int fb = 0;
         mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);
@@ -2556,7 +2588,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
         if (l) return l;
         if (fb == 2) return keylist_from_refs(t, refs, m, A, B);
         m = 0;  // key sets differ (or the walk was abandoned): the merge-join below
-    } else if (A.n > 0 && same_plan(a, b)) {
+    } else if (A.n > 0 && same_plan(a, b) && !keysets_differ(a, b)) {
         // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
         size_t pd = prof_begin(t, "diff");
         const uint32_t *nbad = nullptr;
