@@ -584,18 +584,9 @@ void launch_clear_tomb(const uint8_t *tomb, const uint32_t *perm, uint64_t n, ui
     MKV_LAUNCH_CHECK();
 }
 
-// An empty launch in front of a window that opens on an idle stream: a marker recorded on an idle HIP
-// stream takes the completion time of the stream's last command, so the window would also count the host
-// time since then (the caller's own work between two API calls: ~0.13 ms per 100M diff call measured).
-__global__ void k_prof_anchor() {}
-
 size_t prof_begin(mkv_tree *t, const char *group, hipStream_t s = nullptr) {
     if (!t->prof) return SIZE_MAX;
     if (!s) s = t->st;
-    if (hipStreamQuery(s) == hipSuccess) {
-        hipLaunchKernelGGL(k_prof_anchor, dim3(1), dim3(64), 0, s);
-        MKV_LAUNCH_CHECK();
-    }
     if (t->evfree.empty()) {
         EvPair p;
         MKV_HIP(hipEventCreate(&p.a));
