@@ -21,6 +21,12 @@ MERGE_KERNELS = ("k_diff_partition", "k_diff_pass1", "k_diff_pass2")  # round 4:
 OUT = os.path.join(ROOT, "profiles")
 
 
+# FETCH_SIZE corrections (calibrated by scripts/pmc_calib.hip, profiles/pmc_incremental.json
+# "calibration"): a 16-B/lane streaming read is counted at half its bytes (128-B requests tallied as 64 B),
+# a random read of <= 64 B is one request counted exactly. Kernels whose reads are random probes:
+READ_FACTOR = {"k_diff_partition": 1.0, "k_dirty_climb": 1.0}
+
+
 def kname(s):
     m = re.search(r"(k_[a-z0-9_]+)", s)
     return m.group(1) if m else s.split("(")[0][:40]
@@ -49,7 +55,7 @@ def main():
             e[c + "@dur_us"] = sum(t for _, t in vals) / len(vals) / 1e3
         e["avg_duration_us"] = sum(t for vals in d.values() for _, t in vals) / sum(len(v) for v in d.values()) / 1e3
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
-            e["hbm_bytes_corrected"] = (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
+            e["hbm_bytes_corrected"] = (READ_FACTOR.get(k, 2.0) * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024
         if "GRBM_GUI_ACTIVE" in e:
             gdur = e["GRBM_GUI_ACTIVE@dur_us"]
             e["eff_clock_ghz"] = e["GRBM_GUI_ACTIVE"] / 8 / (gdur * 1e-6) / 1e9
@@ -79,8 +85,9 @@ def main():
         per = {k: summary[k]["hbm_bytes_corrected"] for k in MERGE_KERNELS}
         json.dump({"union_keys": n, "hbm_bytes_per_diff": sum(per.values()), "per_kernel": per,
                    "source": f"{tag}_pmc.json", "algorithmic_bytes_per_diff": 80 * n,
-                   "note": "FETCH_SIZE x2 (gfx950 wide-read under-count) + WRITE_SIZE, KB->bytes, summed over "
-                           "the merge-join kernels of one diff"},
+                   "note": "FETCH_SIZE x2 for the streaming passes (gfx950 wide-read under-count), x1 for the "
+                           "partition's random probes (calibration: scripts/pmc_calib.hip) + WRITE_SIZE, KB->bytes, "
+                           "summed over the merge-join kernels of one diff"},
                   open(os.path.join(OUT, "pmc_diff_merge.json"), "w"), indent=1)
     for k in sorted(summary, key=lambda k: -summary[k].get("avg_duration_us", 0))[:8]:
         e = summary[k]
