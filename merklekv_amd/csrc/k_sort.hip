@@ -854,7 +854,10 @@ void exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, uint64_t 
 
 void launch_mark_ties(const uint64_t *pfx, uint64_t n, uint8_t *tie, uint32_t *count, uint32_t *heads,
                       hipStream_t st, int shift, uint32_t *zero, uint32_t nzero) {
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n + 1, (uint64_t)MT_THREADS * 4), 512);
+    // 128 workgroups: the tie marker runs beside the VALU-bound leaf hash of a build, and every resident
+    // wave of it takes issue slots from the hash (10M build: 512 -> 128 workgroups, 2.25 -> 2.18 ms/step;
+    // 2,048 / 8,192: 2.76 / 3.02; 64 equal, 32 slower: the marker then outlasts the hash)
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n + 1, (uint64_t)MT_THREADS * 4), 128);
     hipLaunchKernelGGL(k_mark_ties, dim3(blocks), dim3(MT_THREADS), 0, st, pfx, n, shift, tie, count, heads, zero,
                        zero ? nzero : 0u);
     MKV_LAUNCH_CHECK();
@@ -883,7 +886,8 @@ void launch_prefix_hist(const uint8_t *kb, const uint64_t *koff, uint64_t n, uin
         if (zero2) MKV_HIP(hipMemsetAsync(zero2, 0, 48, st));
         return;
     }
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 2048);
+    // 256 workgroups for the same reason as the tie marker (beside the leaf hash: 2.18 -> 2.16 ms/step at 10M)
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(ceil_div(n, RS_THREADS * 8), 256);
     hipLaunchKernelGGL(k_prefix_hist, dim3(blocks), dim3(RS_THREADS), 0, st, kb, koff, n, off, lcp, pfx,
                        counts, zero2);
     MKV_LAUNCH_CHECK();
