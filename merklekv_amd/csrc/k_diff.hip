@@ -1112,6 +1112,15 @@ void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, c
     MKV_LAUNCH_CHECK();
 }
 
+__global__ void k_fill_stride_u64(uint64_t *__restrict__ off, uint64_t m, uint64_t stride) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k <= m) off[k] = k * stride;
+}
+void launch_fill_stride_u64(uint64_t *off, uint64_t m, uint64_t stride, hipStream_t st) {
+    hipLaunchKernelGGL(k_fill_stride_u64, grid1d(m + 1), dim3(256), 0, st, off, m, stride);
+    MKV_LAUNCH_CHECK();
+}
+
 void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
                          hipStream_t st) {
     if (!m) return;

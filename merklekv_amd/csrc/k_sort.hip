@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256) void k_prefix64(const uint8_t *__restrict__ kb
 // onesweep control words the radix passes never touch (they use 8 * 256 + 0..31): the longest key length
 // (PH_MAXLEN_WORD) and, with `lcp`, the complement of the shortest zero-padded common prefix of any key
 // with key 0 (PH_NLCP_WORD; bounded by the longer of the two keys, capped at PH_LCP_CAP) and key 0's
-// first 8 bytes (PH_K0_WORD, PH_K0_WORD + 1: high, low half).
+// first 8 bytes (PH_K0_WORD, PH_K0_WORD + 1: high, low half); the complement of the shortest key length
+// (PH_NMINLEN_WORD).
 constexpr uint64_t PH_LCP_CAP = 1u << 16;
 // zero2 (optional): eight counter words zeroed for the tie marker and refinement that follow. (No "last workgroup hands
 // the words to the host" tail: its per-workgroup agent-scope fence + same-address arrival atomic made
@@ -67,11 +68,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
     sort_prio();
     if (zero2 && blockIdx.x == 0 && threadIdx.x < 12) zero2[threadIdx.x] = 0;
     __shared__ uint32_t h[8][256];
-    __shared__ uint32_t lmax, lmin;
+    __shared__ uint32_t lmax, lmin, lshort;
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) (&h[0][0])[i] = 0;
     if (threadIdx.x == 0) {
         lmax = 0;
         lmin = 0xFFFFFFFFu;
+        lshort = 0xFFFFFFFFu;
     }
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * RS_THREADS;
@@ -81,11 +83,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
     // one go (independent loads, one memory latency) instead of one dependent chunk per iteration
     const uint64_t k01 = lcp ? key_chunk(kb + a0, l0, 8) : 0, k02 = lcp ? key_chunk(kb + a0, l0, 16) : 0;
     const uint64_t k03 = lcp ? key_chunk(kb + a0, l0, 24) : 0;
-    uint64_t mx = 0, mn = PH_LCP_CAP;
+    uint64_t mx = 0, mn = PH_LCP_CAP, sh = 0xFFFFFFFFull;
     for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
         const uint64_t a = koff[i], b = koff[i + 1], len = b - a;
         const uint64_t k = key_chunk(kb + a, len, off);
         mx = len > mx ? len : mx;
+        sh = len < sh ? len : sh;
         pfx[i] = k;
 #pragma unroll
         for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
@@ -117,6 +120,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
         }
     }
     atomicMax(&lmax, (uint32_t)(mx > 0xFFFFFFFFull ? 0xFFFFFFFFull : mx));
+    atomicMin(&lshort, (uint32_t)sh);
     if (lcp) atomicMin(&lmin, (uint32_t)mn);
     __syncthreads();
     for (int i = threadIdx.x; i < 8 * 256; i += RS_THREADS) {
@@ -125,6 +129,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
     }
     if (threadIdx.x == 0) {
         if (lmax) atomicMax(&counts[PH_MAXLEN_WORD], lmax);
+        atomicMax(&counts[PH_NMINLEN_WORD], ~lshort);  // max of ~x = min of x
         if (lcp) atomicMax(&counts[PH_NLCP_WORD], ~lmin);  // the words start at 0: max of ~x = min of x
         if (lcp && blockIdx.x == 0) {
             counts[PH_K0_WORD] = (uint32_t)(k0w >> 32);

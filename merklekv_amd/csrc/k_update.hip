@@ -175,6 +175,89 @@ __global__ __launch_bounds__(256) void k_locate(const uint8_t *__restrict__ kb, 
     if ((threadIdx.x & 63) == 0 && nmiss) atomicAdd(missing, nmiss);
 }
 
+// ---- hash index (round 5): batch key -> sorted position in ~1.5 table probes + one full-key check ----
+// The sample search above costs ~20 fabric requests per key at 125M leaves (PMC: 17M TCC_EA0_RDREQ for
+// 875K keys, 0.34 ms): ~11 sample probes beyond L2 plus the prefix window and the key check. The index
+// is keyed by a hash of the whole key, so keys sharing long prefixes spread like any others; a found
+// entry is always confirmed on the tree's own key bytes, so a tag collision can never locate the wrong
+// leaf, and a key that is not a leaf meets an empty slot (or the probe bound: then it counts as missing
+// and the batch takes the exact merge path).
+__device__ __forceinline__ uint64_t hix_mix(uint64_t z) {
+    z ^= z >> 31;
+    z *= 0x7FB5D329728EA185ull;
+    z ^= z >> 27;
+    z *= 0x81DADEF4BC2DD44Dull;
+    z ^= z >> 33;
+    return z;
+}
+__device__ __forceinline__ uint64_t hix_hash(const uint8_t *k, uint64_t len, uint64_t c0) {
+    uint64_t h = hix_mix(c0 ^ (len * 0x9E3779B97F4A7C15ull));
+    for (uint64_t off = 8; off < len; off += 8) h = hix_mix(h ^ key_chunk(k, len, off));
+    return h;
+}
+constexpr uint32_t HIX_MAX_PROBES = 4096;
+
+__global__ __launch_bounds__(256) void k_hix_build(DiffSide T, unsigned long long *__restrict__ tab, uint64_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < T.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t len;
+        const uint8_t *k = tree_key(T, i, &len);
+        const uint64_t h = hix_hash(k, len, key_chunk(k, len, 0));
+        const unsigned long long e = ((h >> 32) | 1ull) << 32 | i;
+        uint64_t s = h & mask;
+        for (uint32_t q = 0; q <= mask; ++q) {  // the table has >= 2n slots: an empty one is always found
+            if (atomicCAS(&tab[s], 0ull, e) == 0ull) break;
+            s = (s + 1) & mask;
+        }
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void locate_hix(const uint8_t *const kp[K], const uint64_t len[K], const bool v[K],
+                                           const DiffSide &T, const uint64_t *__restrict__ tab, uint64_t mask,
+                                           uint64_t found[K]) {
+    uint64_t c0[K], slot[K], tag[K];
+    bool live[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        c0[j] = v[j] ? key_chunk(kp[j], len[j], 0) : 0;
+        const uint64_t h = v[j] ? hix_hash(kp[j], len[j], c0[j]) : 0;
+        slot[j] = h & mask;
+        tag[j] = (h >> 32) | 1ull;
+        live[j] = v[j];
+        found[j] = UINT64_MAX;
+    }
+    for (uint32_t q = 0; q < HIX_MAX_PROBES; ++q) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < K; ++j) any |= live[j];
+        if (!any) break;
+        uint64_t e[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) e[j] = live[j] ? tab[slot[j]] : 0;  // the K probes in flight together
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            if (!live[j]) continue;
+            if (e[j] == 0) {  // empty slot: not a leaf
+                live[j] = false;
+                continue;
+            }
+            if ((e[j] >> 32) == tag[j]) {
+                const uint64_t p = e[j] & 0xFFFFFFFFull;
+                if (T.pfx[p] == c0[j]) {
+                    uint64_t tl;
+                    const uint8_t *tk = tree_key(T, p, &tl);
+                    if (key_cmp(kp[j], len[j], c0[j], tk, tl, c0[j]) == 0) {
+                        found[j] = p;
+                        live[j] = false;
+                        continue;
+                    }
+                }
+            }
+            slot[j] = (slot[j] + 1) & mask;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti L, int pbits,
                                                       uint64_t *__restrict__ pos, uint32_t *__restrict__ idx) {
     const uint32_t t = blockIdx.y;
@@ -191,7 +274,8 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
         kp[j] = B.kb[t] + a;
         len[j] = v[j] ? B.koff[t][i + 1] - a : 0;
     }
-    locate_k<LOCATE_ILP>(kp, len, v, L.T[t], L.ps[t], L.ns[t], found);
+    if (L.hix[t]) locate_hix<LOCATE_ILP>(kp, len, v, L.T[t], L.hix[t], L.hmask[t], found);  // uniform per tree
+    else locate_k<LOCATE_ILP>(kp, len, v, L.T[t], L.ps[t], L.ns[t], found);
     uint32_t nmiss = 0;
 #pragma unroll
     for (int j = 0; j < LOCATE_ILP; ++j) {
@@ -674,6 +758,13 @@ void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k,
     if (!k || !mmax) return;
     hipLaunchKernelGGL(k_locate_multi, dim3((uint32_t)ceil_div(mmax, 256 * LOCATE_ILP), k), dim3(256), 0, st, B, L, pbits,
                        pos, idx);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_hix_build(const DiffSide &T, uint64_t *tab, uint64_t mask, hipStream_t st) {
+    if (!T.n) return;
+    hipLaunchKernelGGL(k_hix_build, dim3((uint32_t)std::min<uint64_t>(ceil_div(T.n, 256), 65536)), dim3(256), 0, st, T,
+                       reinterpret_cast<unsigned long long *>(tab), mask);
     MKV_LAUNCH_CHECK();
 }
 

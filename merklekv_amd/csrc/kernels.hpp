@@ -78,6 +78,7 @@ void radix_prefix_hist(const uint64_t *k, uint64_t n, void *scratch, hipStream_t
 constexpr uint32_t PH_MAXLEN_WORD = 8 * 256 + 63;
 constexpr uint32_t PH_NLCP_WORD = 8 * 256 + 62;
 constexpr uint32_t PH_K0_WORD = 8 * 256 + 60;
+constexpr uint32_t PH_NMINLEN_WORD = 8 * 256 + 58;  // ~(shortest key length)
 constexpr uint32_t SORT_CTL_WORDS = 8 * 256 + 64;
 void launch_pfx_from_window(uint64_t *pk, uint64_t n, uint64_t shared, uint32_t win, hipStream_t st);
 // lcp: also measure the shared prefix with key 0 (PH_NLCP_WORD) and key 0's first bytes (PH_K0_WORD),
@@ -225,6 +226,8 @@ void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, c
                            uint32_t *nbad, hipStream_t st);
 void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t *lens,
                          hipStream_t st);
+// off[k] = k * stride, k <= m (key-list offsets of keys of one fixed length).
+void launch_fill_stride_u64(uint64_t *off, uint64_t m, uint64_t stride, hipStream_t st);
 void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,
                       uint8_t *out, hipStream_t st);
 // One-wait tail of the unsharded top-down pair diff: k_td_gate after the landing on level 4 (screen word
@@ -286,7 +289,12 @@ struct LocateMulti {
     const uint64_t *ps[LEAF_MULTI_MAX];  // locate samples of T[b] (launch_locate_samples)
     uint64_t ns[LEAF_MULTI_MAX];
     uint32_t *missing[LEAF_MULTI_MAX];
+    const uint64_t *hix[LEAF_MULTI_MAX];  // hash index of T[b] (launch_hix_build) or null: the sample search
+    uint64_t hmask[LEAF_MULTI_MAX];
 };
+// Hash index of a tree's sorted keys: open addressing (linear probing) over cap = 2^k >= 2n slots, entry =
+// (tag << 32 | sorted position), 0 = empty; tab zeroed by the caller.
+void launch_hix_build(const DiffSide &T, uint64_t *tab, uint64_t mask, hipStream_t st);
 void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
                          uint64_t *pos, uint32_t *idx, hipStream_t st);
 constexpr int DIRTY_MAX_TREES = 16;

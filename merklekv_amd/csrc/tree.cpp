@@ -237,6 +237,8 @@ struct mkv_tree {
     DevBuf kb, koff, perm, pfx, nodes;
     uint64_t sort_win_hint = 0;            // shared key prefix length found by the last sort (sort_unique)
     DevBuf pfx_s;                          // locate samples of pfx (every LOC_STRIDE-th), built on demand
+    DevBuf hix;                            // hash index of the sorted keys (locate_index_of), built on demand
+    uint64_t hix_gen = 0, hix_mask = 0;
     uint64_t pfx_gen = 1, pfx_s_gen = 0;   // pfx_s is current while pfx_s_gen == pfx_gen
     uint64_t keyset = next_keyset();       // key-set identity (see next_keyset)
     // Key-set fingerprint of the last sort (sum and xor of the sorted key prefixes, k_mark_ties): two trees
@@ -245,6 +247,7 @@ struct mkv_tree {
     // walk's own key-set screen and leaf-key checks decide as before. Cleared by key-set changes.
     uint64_t kfp[2] = {0, 0};
     bool kfp_ok = false;
+    uint64_t klen_fixed = 0;               // every key has this length (0: unknown / mixed): key lists skip the length scan
     std::vector<uint64_t> lev_cnt, lev_off, lev_base, lev_S;  // per level: owned count, node offset, base, global size
     bool has_root = false;
     uint8_t root[32] = {0};
@@ -327,6 +330,11 @@ uint64_t mkv::tree_global_n(const mkv_tree *t) { return t->sharded ? t->gN : t->
 // Same key-set id => same sorted keys. The id is a correctness input (the batched dirty path locates a
 // replica's batch in another tree, the walks skip the leaf-key check), so the cheap host-side facts that
 // must agree are checked every time: a mismatch means some key-changing path kept a stale id.
+// Both trees' keys all have one length: key lists need no length gather (0 otherwise).
+static uint64_t pair_klen(const mkv_tree *a, const mkv_tree *b) {
+    return a->klen_fixed && a->klen_fixed == b->klen_fixed ? a->klen_fixed : 0;
+}
+
 // Different key-set fingerprints (see mkv_tree::kfp): the key sets differ for certain.
 static bool keysets_differ(const mkv_tree *a, const mkv_tree *b) {
     return a->kfp_ok && b->kfp_ok && (a->kfp[0] != b->kfp[0] || a->kfp[1] != b->kfp[1]);
@@ -952,6 +960,7 @@ struct SortedSet {
     uint64_t n;
     uint64_t fp[2];  // key-set fingerprint (sum, xor of the sort keys); valid when fp_ok
     bool fp_ok;
+    uint64_t klen;   // every key has this length (0: lengths differ, or no keys)
 };
 // kbytes_out (optional): koff[n_in], read back with the sort's own counts (one host round trip).
 SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint64_t n_in, const uint8_t *tomb,
@@ -990,6 +999,7 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
     uint32_t digits = 0xFF;
     uint64_t win = hint;    // byte offset of the sort window
     uint64_t shared8 = 0;   // the first min(win, 8) bytes every key shares, big-endian at the top
+    uint64_t klen_all = 0;  // every key has this length (from the histogram pass), else 0
     if (n_in > 1) {
         wait_stream(t, st);
         // Bytes every key shares carry no order: move the window past them ("tenant/0001/object/..."
@@ -997,6 +1007,7 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         // refinement). One more histogram pass when the shared length the first pass measured is not
         // the window it used.
         const uint64_t maxlen = t->h_counts[PH_MAXLEN_WORD];
+        klen_all = n_in && (uint32_t)~t->h_counts[PH_NMINLEN_WORD] == maxlen ? maxlen : 0;
         const uint64_t lcp = (uint32_t)~t->h_counts[PH_NLCP_WORD];
         const uint64_t k0w = ((uint64_t)t->h_counts[PH_K0_WORD] << 32) | t->h_counts[PH_K0_WORD + 1];
         const uint64_t want = lcp > 0 && lcp < maxlen ? lcp : 0;
@@ -1073,7 +1084,7 @@ SortedSet sort_unique(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uint
         launch_pfx_from_window(pkbuf->as<uint64_t>(), n, shared8, (uint32_t)std::min<uint64_t>(win, 8), st);
         prof_end(t, pf);
     }
-    return SortedSet{pkbuf, pmbuf, n, {fp0, fp1}, dups == 0 && n == n_in};
+    return SortedSet{pkbuf, pmbuf, n, {fp0, fp1}, dups == 0 && n == n_in, n ? klen_all : 0};
 }
 
 // fused_kcap: the leaf kernels copied the borrowed keys into t->kb (capacity fused_kcap bytes; complete
@@ -1098,6 +1109,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     t->kfp[0] = S.fp[0];
     t->kfp[1] = S.fp[1];
     t->kfp_ok = S.fp_ok;
+    t->klen_fixed = S.klen;
     swap_buf(t->perm, *pmbuf);
     perm = t->perm.as<uint32_t>();
     // key-byte count of borrowed inputs, read while st is still busy hashing (never after the join:
@@ -1444,6 +1456,7 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         dst->kfp[0] = src->kfp[0];
         dst->kfp[1] = src->kfp[1];
         dst->kfp_ok = src->kfp_ok;
+        dst->klen_fixed = src->klen_fixed;
         dst->kbytes = src->kbytes;
         dst->lev_cnt = src->lev_cnt;
         dst->lev_off = src->lev_off;
@@ -1626,6 +1639,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     ++t->pfx_gen;
     t->keyset = next_keyset();
     t->kfp_ok = false;  // merged key set: no fingerprint
+    t->klen_fixed = t->klen_fixed && B.klen == t->klen_fixed ? t->klen_fixed : 0;
     swap_buf(t->perm, t->m_perm);
     swap_buf(t->nodes, t->m_nodes);
     t->kbytes = kbytes + kbn;
@@ -1683,6 +1697,27 @@ struct DirtyBatch {
 
 // The tree's locate samples (every LOC_STRIDE-th sorted prefix), rebuilt on stream st when the prefixes
 // changed since the last call (builds, merges, clones); value-only updates keep them.
+// The hash index of t's sorted keys for the dirty path's locate (k_update.hip locate_hix), built on first
+// use after every key-set change (pfx_gen): 2 x n slots of 8 B (2 GiB at 125M keys). Small trees keep the
+// sample search.
+constexpr uint64_t HIX_MIN_KEYS = 1ull << 20;
+static const uint64_t *locate_index_of(mkv_tree *t, hipStream_t st, uint64_t *mask) {
+    *mask = 0;
+    if (t->n < HIX_MIN_KEYS || t->n >= (1ull << 32) - 2) return nullptr;
+    uint64_t cap = 1;
+    while (cap < 2 * t->n) cap <<= 1;
+    const bool fresh = t->hix_gen != t->pfx_gen || t->hix_mask != cap - 1 || t->hix.cap < cap * 8;
+    uint64_t *tab = ens<uint64_t>(t->hix, cap);
+    if (fresh) {
+        MKV_HIP(hipMemsetAsync(tab, 0, cap * 8, st));
+        launch_hix_build(side_of(t), tab, cap - 1, st);
+        t->hix_gen = t->pfx_gen;
+        t->hix_mask = cap - 1;
+    }
+    *mask = cap - 1;
+    return tab;
+}
+
 static const uint64_t *locate_samples_of(mkv_tree *t, hipStream_t st, uint64_t *ns) {
     *ns = locate_samples(t->n);
     uint64_t *ps = ens<uint64_t>(t->pfx_s, *ns + 1);
@@ -1771,7 +1806,8 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             // for the caches and the TLB instead of k copies of the same data)
             mkv_tree *lt = same_keyset(t, t0) ? t0 : t;
             LM.T[q] = side_of(lt);
-            LM.ps[q] = locate_samples_of(lt, st, &LM.ns[q]);
+            LM.hix[q] = locate_index_of(lt, st, &LM.hmask[q]);
+            LM.ps[q] = LM.hix[q] ? nullptr : locate_samples_of(lt, st, &LM.ns[q]);
             LM.missing[q] = cnt + L + 1;
             CA.nodes[q] = t->nodes.as<uint8_t>();
             CA.missing[q] = cnt + L + 1;
@@ -2441,10 +2477,19 @@ static DiffSide side_of(const mkv_tree *t) {
 // Key list of the refs (bit 63 = side B) gathered on the device and copied to the host. `reject`
 // (optional device u32) is read back together with the byte count: nonzero -> nullptr, nothing copied.
 static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A,
-                                      const DiffSide &B, const uint32_t *reject = nullptr) {
+                                      const DiffSide &B, const uint32_t *reject = nullptr, uint64_t klen = 0) {
     auto *l = new mkv_keylist();
     try {
-        if (m) {
+        if (m && klen && !reject) {
+            // every key of both trees has length klen: offsets k * klen, no length gather / scan / readback
+            uint64_t *off = ens<uint64_t>(t->d_outoff, m + 1);
+            uint8_t *ob = ens<uint8_t>(t->d_out, m * klen + 16);
+            launch_fill_stride_u64(off, m, klen, t->st);
+            launch_diff_keys(refs, m, A, B, off, ob, t->st);
+            HTRACE("keys-queued");
+            keylist_fill(t, l, off, ob, m, m * klen);
+            HTRACE("copies-queued");
+        } else if (m) {
             size_t pk = prof_begin(t, "diff");
             uint64_t *lens = ens<uint64_t>(t->s_lens, m + 1);
             uint64_t *off = ens<uint64_t>(t->d_outoff, m + 1);
@@ -2518,21 +2563,27 @@ static bool keys_from_refs_dev(mkv_tree *t, const uint64_t *refs, uint64_t m, co
 // runs on st3 and the call returns without waiting for it; mkv_keylist_get waits when the bytes are
 // first read. The caller's next work (the next step's updates) overlaps the copy.
 static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A,
-                                            const DiffSide &B) {
+                                            const DiffSide &B, uint64_t klen = 0) {
     auto *l = new mkv_keylist();
     try {
         if (m) {
             if (t->a_ev) MKV_HIP(hipStreamWaitEvent(t->st, t->a_ev->e, 0));  // the last copy read a_out*
             size_t pk = prof_begin(t, "diff");
-            uint64_t *lens = ens<uint64_t>(t->a_lens, m + 1);
             uint64_t *off = ens<uint64_t>(t->a_outoff, m + 1);
-            void *scr = t->d_diffscr.ensure(scan_scratch_bytes(m + 1));
-            launch_diff_keylens(refs, m, A, B, lens, t->st);
-            exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
-            prof_end(t, pk);
-            small_d2h(t, t->h_small, off + m, 8, t->st);
-            wait_stream(t, t->st);
-            const uint64_t bytes = t->h_small[0];
+            uint64_t bytes = m * klen;
+            if (klen) {  // fixed-length keys: offsets k * klen, no length gather / scan / readback
+                launch_fill_stride_u64(off, m, klen, t->st);
+                prof_end(t, pk);
+            } else {
+                uint64_t *lens = ens<uint64_t>(t->a_lens, m + 1);
+                void *scr = t->d_diffscr.ensure(scan_scratch_bytes(m + 1));
+                launch_diff_keylens(refs, m, A, B, lens, t->st);
+                exclusive_scan_u64(lens, off, m, off + m, scr, t->st);
+                prof_end(t, pk);
+                small_d2h(t, t->h_small, off + m, 8, t->st);
+                wait_stream(t, t->st);
+                bytes = t->h_small[0];
+            }
             uint8_t *ob = ens<uint8_t>(t->a_out, bytes + 16);
             launch_diff_keys(refs, m, A, B, off, ob, t->st);
             l->n = m;
@@ -2579,7 +2630,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
         mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);
         HTRACE("topdown-done");
         if (l) return l;
-        if (fb == 2) return keylist_from_refs(t, refs, m, A, B);
+        if (fb == 2) return keylist_from_refs(t, refs, m, A, B, nullptr, pair_klen(a, b));
         m = 0;  // key sets differ (or the walk was abandoned): the merge-join below
     } else if (A.n > 0 && same_plan(a, b) && !keysets_differ(a, b)) {
         // Top-down: identical level plans, so node (l, j) covers the same leaf positions in both trees.
@@ -2620,7 +2671,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
         keys_from_refs_dev(t, refs, m, A, B, nullptr, dev);
         return nullptr;
     }
-    return keylist_from_refs(t, refs, m, A, B);
+    return keylist_from_refs(t, refs, m, A, B, nullptr, pair_klen(a, b));
 }
 
 // One top-down walk of base `a` against every variant in vs (same level plan, key sets screened
@@ -2712,7 +2763,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
         small_d2h(t, hb, nbad, 2 * k * 4, t->st);
     }
-    mkv_keylist *all = keylist_from_refs_async(t, refs, m, A, A);  // waits for st: hb is valid after this
+    mkv_keylist *all = keylist_from_refs_async(t, refs, m, A, A, a->klen_fixed);  // waits for st: hb valid after
     // segment starts -> per-variant counts (variants appear in ascending order)
     std::vector<uint64_t> cntv(k, 0);
     if (m) {
@@ -2893,7 +2944,7 @@ mkv_status mkv_tree_keys_at(const mkv_tree *tc, const uint64_t *pos, uint64_t m,
         uint64_t *refs = ens<uint64_t>(t->x_idx, m + 1);
         if (m) MKV_HIP(hipMemcpyAsync(refs, pos, m * 8, hipMemcpyHostToDevice, t->st));
         const DiffSide A = side_of(t);
-        *out = keylist_from_refs(t, refs, m, A, A);
+        *out = keylist_from_refs(t, refs, m, A, A, nullptr, t->klen_fixed);
     });
 }
 

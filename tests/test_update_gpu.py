@@ -576,3 +576,31 @@ def test_dirty_climb_passes_and_rendezvous_vs_oracle(n, dens):
         assert trees[r].get_root_hash() == expect[r].root(), r
         assert _levels(trees[r]) == _oracle_levels(expect[r]), r
         assert sum(trees[r].update_counts()) > 0  # the dirty path ran (no fallback to the batch merge)
+
+
+def test_hash_index_locate_shared_prefixes_and_missing_keys():
+    """Trees of >= 2^20 keys locate batch keys through the hash index (k_update.hip locate_hix): keys that
+    share a 19-byte prefix (the sample search's worst case, the index's hash covers the whole key), batch
+    keys at both ends and repeated, then a batch with a key that is not a leaf (empty slot: counted
+    missing, the exact merge path runs). Roots vs the oracle's insert-then-rebuild (merkle.rs:52-56)."""
+    n = (1 << 20) + 4097
+    keys = [b"tenant/0001/object/%010d" % (7 * i) for i in range(n)]
+    vals = [b"v%d" % i for i in range(n)]
+    kb, ko = pack(keys)
+    vb, vo = pack(vals)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    rng = np.random.default_rng(20)
+    idx = list(rng.integers(0, n, size=5000)) + [0, n - 1, n - 1, 1, n - 2]
+    ks, vs = _batch(keys, idx, "hix")
+    t.upsert(ks, vs)
+    o2 = o.upsert(*pack(ks), *pack(vs))
+    assert t.get_root_hash() == o2.root()
+    assert t.update_counts()[0] == len(set(int(i) for i in idx))  # every key located: the dirty path ran
+    ks3 = [keys[3], b"tenant/0001/object/0000000001", keys[n - 1]]  # 1 is no multiple of 7: not a leaf
+    vs3 = [b"a", b"b", b"c"]
+    t.upsert(ks3, vs3)
+    o3 = o2.upsert(*pack(ks3), *pack(vs3))
+    assert t.get_root_hash() == o3.root()
+    assert len(t) == n + 1  # the new key was inserted by the merge path
