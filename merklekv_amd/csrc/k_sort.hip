@@ -84,39 +84,59 @@ __global__ __launch_bounds__(RS_THREADS) void k_prefix_hist(const uint8_t *__res
     const uint64_t k01 = lcp ? key_chunk(kb + a0, l0, 8) : 0, k02 = lcp ? key_chunk(kb + a0, l0, 16) : 0;
     const uint64_t k03 = lcp ? key_chunk(kb + a0, l0, 24) : 0;
     uint64_t mx = 0, mn = PH_LCP_CAP, sh = 0xFFFFFFFFull;
-    for (uint64_t i = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += stride) {
-        const uint64_t a = koff[i], b = koff[i + 1], len = b - a;
-        const uint64_t k = key_chunk(kb + a, len, off);
-        mx = len > mx ? len : mx;
-        sh = len < sh ? len : sh;
-        pfx[i] = k;
+    // PH_ILP keys per thread and iteration, their offsets and first chunks loaded together: the pass runs
+    // on a few workgroups beside the leaf hash, so each iteration is a chain of dependent memory round
+    // trips (offsets -> key chunk), and ragged keys made it the build's critical path (10M: 673 us)
+    constexpr int PH_ILP = 4;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * RS_THREADS + threadIdx.x; i0 < n; i0 += PH_ILP * stride) {
+        uint64_t ka[PH_ILP], kl[PH_ILP], kc[PH_ILP];
 #pragma unroll
-        for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
-        if (lcp && mn) {  // common prefix with key 0, from the key's first chunk
-            uint64_t lim = len > l0 ? len : l0;
-            lim = lim < PH_LCP_CAP ? lim : PH_LCP_CAP;
-            uint64_t L = 0, x = (off == 0 ? k : key_chunk(kb + a, len, 0)) ^ k0w;
-            if (x == 0 && 8 < lim) {
-                const uint64_t x1 = key_chunk(kb + a, len, 8) ^ k01, x2 = key_chunk(kb + a, len, 16) ^ k02;
-                const uint64_t x3 = key_chunk(kb + a, len, 24) ^ k03;
-                L = 8;
-                x = x1;
-                if (x == 0 && L + 8 < lim) {
-                    L = 16;
-                    x = x2;
+        for (int j = 0; j < PH_ILP; ++j) {
+            const uint64_t i = i0 + (uint64_t)j * stride;
+            const bool v = i < n;
+            const uint64_t a = v ? koff[i] : 0, b = v ? koff[i + 1] : 0;
+            ka[j] = a;
+            kl[j] = b - a;
+        }
+#pragma unroll
+        for (int j = 0; j < PH_ILP; ++j) kc[j] = i0 + (uint64_t)j * stride < n ? key_chunk(kb + ka[j], kl[j], off) : 0;
+#pragma unroll
+        for (int j = 0; j < PH_ILP; ++j) {
+            const uint64_t i = i0 + (uint64_t)j * stride;
+            if (i >= n) break;
+            const uint64_t a = ka[j], len = kl[j];
+            const uint64_t k = kc[j];
+            mx = len > mx ? len : mx;
+            sh = len < sh ? len : sh;
+            pfx[i] = k;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) atomicAdd(&h[p][(uint32_t)(k >> (8 * p)) & 255u], 1u);
+            if (lcp && mn) {  // common prefix with key 0, from the key's first chunk
+                uint64_t lim = len > l0 ? len : l0;
+                lim = lim < PH_LCP_CAP ? lim : PH_LCP_CAP;
+                uint64_t L = 0, x = (off == 0 ? k : key_chunk(kb + a, len, 0)) ^ k0w;
+                if (x == 0 && 8 < lim) {
+                    const uint64_t x1 = key_chunk(kb + a, len, 8) ^ k01, x2 = key_chunk(kb + a, len, 16) ^ k02;
+                    const uint64_t x3 = key_chunk(kb + a, len, 24) ^ k03;
+                    L = 8;
+                    x = x1;
                     if (x == 0 && L + 8 < lim) {
-                        L = 24;
-                        x = x3;
+                        L = 16;
+                        x = x2;
+                        if (x == 0 && L + 8 < lim) {
+                            L = 24;
+                            x = x3;
+                        }
                     }
                 }
+                while (x == 0 && L + 8 < lim) {
+                    L += 8;
+                    x = key_chunk(kb + a, len, L) ^ key_chunk(kb + a0, l0, L);
+                }
+                L += x ? (uint64_t)(__builtin_clzll(x) >> 3) : 8;
+                L = L < lim ? L : lim;
+                mn = L < mn ? L : mn;
             }
-            while (x == 0 && L + 8 < lim) {
-                L += 8;
-                x = key_chunk(kb + a, len, L) ^ key_chunk(kb + a0, l0, L);
-            }
-            L += x ? (uint64_t)(__builtin_clzll(x) >> 3) : 8;
-            L = L < lim ? L : lim;
-            mn = L < mn ? L : mn;
         }
     }
     atomicMax(&lmax, (uint32_t)(mx > 0xFFFFFFFFull ? 0xFFFFFFFFull : mx));
