@@ -1146,13 +1146,26 @@ void launch_td_gate(uint32_t *cnt, uint32_t word, uint32_t level, uint64_t level
     MKV_LAUNCH_CHECK();
 }
 
+// off[k] = min(k, *mdev) x klen for k <= cap (fixed-length keys: the tail's offsets without a scan).
+__global__ void k_fill_stride_dev(uint64_t *__restrict__ off, const uint32_t *__restrict__ mdev, uint64_t cap,
+                                  uint64_t klen) {
+    const uint64_t m = *mdev;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= cap; k += (uint64_t)gridDim.x * blockDim.x)
+        off[k] = (k < m ? k : m) * klen;
+}
+
 void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
-                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st) {
+                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen) {
     const dim3 g((uint32_t)std::min<uint64_t>(ceil_div(cap_m, 256), 2048));
     if (check) hipLaunchKernelGGL(k_td_check_dev, g, dim3(256), 0, st, refs, mdev, A, B, nbad);
-    hipLaunchKernelGGL(k_keylens_dev, g, dim3(256), 0, st, refs, mdev, cap_m, A, lens);
-    exclusive_scan_u64(lens, off, cap_m, off + cap_m, scan_scr, st);
+    if (klen) {  // every key of both trees has length klen
+        hipLaunchKernelGGL(k_fill_stride_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)), dim3(256),
+                           0, st, off, mdev, cap_m, klen);
+    } else {
+        hipLaunchKernelGGL(k_keylens_dev, g, dim3(256), 0, st, refs, mdev, cap_m, A, lens);
+        exclusive_scan_u64(lens, off, cap_m, off + cap_m, scan_scr, st);
+    }
     hipLaunchKernelGGL(k_keys_dev, g, dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, off, kout);
     const uint64_t cb = std::min<uint64_t>(ceil_div(std::max(8 * (cap_m + 1), cap_b) / 16 + 1, 256), 2048);
     hipLaunchKernelGGL(k_tail_copy_dev, dim3((uint32_t)cb), dim3(256), 0, st, off, kout, mdev, cap_m, cap_b, doff, dkeys);

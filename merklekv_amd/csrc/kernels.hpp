@@ -238,7 +238,7 @@ void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const
 void launch_td_gate(uint32_t *cnt, uint32_t word, uint32_t level, uint64_t level_count, hipStream_t st);
 void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
-                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st);
+                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen = 0);
 // Batched top-down walk (one base vs up to TD_MAX_VARIANTS trees with the same level plan).
 constexpr int TD_MAX_VARIANTS = 64;
 struct TdVariants {

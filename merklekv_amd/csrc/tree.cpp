@@ -2412,7 +2412,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     positions_sorted_bitmap_dev(fin, cnt, n, bm, bc, refs, t->st);  // side-A refs = sorted positions
     t->td_bm_words = words;
     launch_diff_tail_dev(refs, cnt, A, B, !same_keyset(a, b), cnt + L + 1, cap_m, cap_b, lens, off, scr, kout, blk->dp,
-                         blk->dp + kpos, t->st);
+                         blk->dp + kpos, t->st, pair_klen(a, b));
     small_d2h(t, t->h_small, cnt, 4, t->st);                // divergent positions
     small_d2h(t, t->h_small + 1, cnt + L + 1, 4, t->st);    // screen / abort / leaf-key mismatches
     small_d2h(t, t->h_small + 2, off + cap_m, 8, t->st);    // key bytes (when m <= cap_m)
