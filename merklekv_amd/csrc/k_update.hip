@@ -38,6 +38,10 @@ __device__ __forceinline__ const uint8_t *tree_key(const DiffSide &T, uint64_t i
 __device__ __forceinline__ uint64_t locate_run(const uint8_t *k, uint64_t len, uint64_t c0, const DiffSide &T,
                                                uint64_t lo);
 constexpr int LOCATE_ILP = 2;  // batch keys per lane in k_locate / k_locate_multi
+#ifndef MKV_LOCATE_BLOCKS
+#define MKV_LOCATE_BLOCKS 128
+#endif
+constexpr uint64_t LOCATE_MAX_BLOCKS = MKV_LOCATE_BLOCKS;  // per tree (k_locate_multi grid.x)
 
 // Sorted positions of K batch keys in tree T (found[j] = UINT64_MAX when key j is not a leaf), K keys per
 // lane. ps[j] = T.pfx[LOC_STRIDE * j] (ns samples, a 1/64 copy that stays in the MALL / L2): the lower
@@ -262,7 +266,9 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
                                                       uint64_t *__restrict__ pos, uint32_t *__restrict__ idx) {
     const uint32_t t = blockIdx.y;
     const uint64_t m = B.m[t];
-    const uint64_t i0 = (uint64_t)blockIdx.x * (LOCATE_ILP * blockDim.x) + threadIdx.x;
+    uint32_t nmiss = 0;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * (LOCATE_ILP * blockDim.x) + threadIdx.x; i0 < m;
+         i0 += (uint64_t)gridDim.x * (LOCATE_ILP * blockDim.x)) {
     const uint8_t *kp[LOCATE_ILP];
     uint64_t len[LOCATE_ILP], found[LOCATE_ILP];
     bool v[LOCATE_ILP];
@@ -276,7 +282,6 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
     }
     if (L.hix[t]) locate_hix<LOCATE_ILP>(kp, len, v, L.T[t], L.hix[t], L.hmask[t], found);  // uniform per tree
     else locate_k<LOCATE_ILP>(kp, len, v, L.T[t], L.ps[t], L.ns[t], found);
-    uint32_t nmiss = 0;
 #pragma unroll
     for (int j = 0; j < LOCATE_ILP; ++j) {
         const uint64_t i = i0 + (uint64_t)j * blockDim.x;
@@ -287,6 +292,7 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
             idx[g] = (uint32_t)g;
         }
         nmiss += (uint32_t)__popcll(__ballot(miss));
+    }
     }
     if ((threadIdx.x & 63) == 0 && nmiss) atomicAdd(L.missing[t], nmiss);
 }
@@ -756,8 +762,12 @@ void launch_locate_samples(const uint64_t *pfx, uint64_t n, uint64_t *ps, hipStr
 void launch_locate_multi(const LeafBatches &B, const LocateMulti &L, uint32_t k, uint64_t mmax, int pbits,
                          uint64_t *pos, uint32_t *idx, hipStream_t st) {
     if (!k || !mmax) return;
-    hipLaunchKernelGGL(k_locate_multi, dim3((uint32_t)ceil_div(mmax, 256 * LOCATE_ILP), k), dim3(256), 0, st, B, L, pbits,
-                       pos, idx);
+    // A bounded grid (the blocks loop over their tree's keys): the locate's waves wait on memory most of
+    // the time, and a wave per 128 keys (6,860 at configs[4]) held the CUs' wave slots that the batch hash
+    // running beside it needs. configs[4] step per cap (interleaved A/B): 32 blocks per tree 1.98-2.06 ms,
+    // 64 1.87, 128 1.80-1.84, uncapped (245) 1.86-1.87; locate and hash serialised on one stream 1.91-1.98
+    const uint32_t gx = (uint32_t)std::min<uint64_t>(ceil_div(mmax, 256 * LOCATE_ILP), LOCATE_MAX_BLOCKS);
+    hipLaunchKernelGGL(k_locate_multi, dim3(gx, k), dim3(256), 0, st, B, L, pbits, pos, idx);
     MKV_LAUNCH_CHECK();
 }
 
