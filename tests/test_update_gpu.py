@@ -604,3 +604,39 @@ def test_hash_index_locate_shared_prefixes_and_missing_keys():
     o3 = o2.upsert(*pack(ks3), *pack(vs3))
     assert t.get_root_hash() == o3.root()
     assert len(t) == n + 1  # the new key was inserted by the merge path
+
+
+def test_fixed_length_key_lists_follow_key_length_changes():
+    """Key lists of trees whose keys all have one length skip the length gather (offsets k x len,
+    tree.cpp pair_klen); a merged batch with a key of another length must turn that off, and trees of
+    two different fixed lengths must not use it. Every list vs the oracle's R7 diff (merkle.rs:171-204)."""
+    n = 20000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    assert len(set(len(k) for k in keys)) == 1
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    ob = coracle.OracleTree.build(kb, ko, vb, vo)
+    t = base.clone()
+    t.upsert([keys[5], b"short", keys[n - 1]], [b"x", b"y", b"z"])  # a 5-byte key: merge path
+    o = ob.upsert(*pack([keys[5], b"short", keys[n - 1]]), *pack([b"x", b"y", b"z"]))
+    assert t.get_root_hash() == o.root()
+    assert base.diff_keys_bytes(t) == ob.diff(o)
+    assert t.diff_keys_bytes(base) == o.diff(ob)
+    # value-only update of the merged tree (dirty path keeps its key set), then diff again
+    t.upsert([b"short", keys[7]], [b"y2", b"w"])
+    o = o.upsert(*pack([b"short", keys[7]]), *pack([b"y2", b"w"]))
+    assert base.diff_keys_bytes(t) == ob.diff(o)
+    # two trees of different fixed lengths (every key of one tree is 2 bytes longer)
+    k2 = [k + b"zz" for k in keys[:n // 2]] + keys[n // 2:]
+    kb2, ko2 = pack(k2)
+    t2 = MerkleTree()
+    t2.build((kb2, ko2), (vb, vo))
+    o2 = coracle.OracleTree.build(kb2, ko2, vb, vo)
+    assert base.diff_keys_bytes(t2) == ob.diff(o2)
+    k3 = [k + b"zz" for k in keys]
+    kb3, ko3 = pack(k3)
+    t3 = MerkleTree()
+    t3.build((kb3, ko3), (vb, vo))
+    o3 = coracle.OracleTree.build(kb3, ko3, vb, vo)
+    assert base.diff_keys_bytes(t3) == ob.diff(o3)
