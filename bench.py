@@ -955,8 +955,7 @@ def configs4_measure(ctx, n, m, R, steps, warmup):
     inc = {"tree_keys": N, "batch_per_rank": m, "replicas": R,
            "update_device_ms_all_replicas": upd_ms, "diff_device_ms_per_pair": diff_ms,
            "climb_device_ms": climb_ms, "walk_device_ms_per_pair": walk_ms / (R - 1),
-           "keys_d2h_ms_per_pair": d2h_ms,
-           "diff_device_ms_per_pair_excl_d2h": diff_ms - d2h_ms,
+           "keys_d2h_ms_per_pair": d2h_ms,  # on the copy stream, beside the next step's update (not in diff_device)
            "diff_sizes_match_unique_updates": ok,
            "divergent_per_pair_rank0": [len(d) for d in diffs], "variant_roots": roots}
     out = {"workload": (f"configs[4]: {N} keys ({n} per rank), {R} replicas (base + {R - 1} variants), "
