@@ -2603,6 +2603,9 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
             t->a_ev = ev;
             l->offsets = reinterpret_cast<const uint64_t *>(l->blk->p);
             l->bytes = l->blk->p + kpos;
+            // the caller reads counters its own work on st wrote into pinned memory (topdown_batch: the
+            // per-variant check and segment words); the length path above waited already
+            if (klen) wait_stream(t, t->st);
         }
     } catch (...) {
         delete l;

@@ -640,3 +640,30 @@ def test_fixed_length_key_lists_follow_key_length_changes():
     t3.build((kb3, ko3), (vb, vo))
     o3 = coracle.OracleTree.build(kb3, ko3, vb, vo)
     assert base.diff_keys_bytes(t3) == ob.diff(o3)
+
+
+def test_batched_diff_per_variant_split_each_call():
+    """The batched 1-vs-k diff splits one shared key list into per-variant lists from counters the walk
+    writes into pinned memory; with fixed-length keys the key list needs no length readback, so the call
+    must still wait for those counters. Rounds of shrinking, uneven per-variant batches on fresh clones
+    (the pinned staging is reused, nothing else synchronises), every list vs the oracle's R7 diff."""
+    n = 200000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    base = MerkleTree()
+    base.build((kb, ko), (vb, vo))
+    ob = coracle.OracleTree.build(kb, ko, vb, vo)
+    rng = np.random.default_rng(77)
+    for rnd, scale in enumerate((3000, 1500, 700, 300)):
+        variants = [base.clone() for _ in range(4)]
+        expect = []
+        for i, v in enumerate(variants):
+            m = scale * (i + 1) // 2 + 7 * rnd
+            idx = rng.choice(n, size=m, replace=False)
+            ks, vs = _batch(keys, idx, "r%d-%d" % (rnd, i))
+            v.upsert(ks, vs)
+            expect.append(ob.diff(ob.upsert(*pack(ks), *pack(vs))))
+        got = base.diff_keys_many_packed(variants)
+        for i, (raw, offs) in enumerate(got):
+            b, o = raw.tobytes(), offs.tolist()
+            assert [b[o[j]:o[j + 1]] for j in range(len(o) - 1)] == expect[i], (rnd, i)
