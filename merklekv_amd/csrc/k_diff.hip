@@ -851,17 +851,87 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_level_batch(const uint8_
 // Sorted (variant, leaf position) entries: keys must be equal on both sides (else that variant's key
 // set differs there: nbad[v]); refs[k] = the base's sorted index; count[v] = first entry of variant v
 // (left untouched — the caller presets all-ones — when v has none).
+// mdev (optional): the entry count on the device (grid-stride; m is then only the grid's bound).
 __global__ void k_topdown_leaves_batch(const uint64_t *__restrict__ ent, uint64_t m, int pb, DiffSide A,
                                        const DiffSide *__restrict__ Bs, uint64_t check, uint64_t *__restrict__ refs,
-                                       uint32_t *__restrict__ nbad, uint32_t *__restrict__ count) {
-    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= m) return;
-    const uint64_t e = ent[k];  // (variant << pb) | position
-    const uint32_t v = (uint32_t)(e >> pb);
-    const uint64_t i = e & ((1ull << pb) - 1ull);
-    refs[k] = i;
-    if (k == 0 || (uint32_t)(ent[k - 1] >> pb) != v) count[v] = (uint32_t)k;  // segment start of variant v
-    if (((check >> v) & 1ull) && !key_eq_at(A, Bs[v], i)) atomicAdd(&nbad[v], 1u);
+                                       uint32_t *__restrict__ nbad, uint32_t *__restrict__ count,
+                                       const uint32_t *__restrict__ mdev) {
+    if (mdev) m = *mdev;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = ent[k];  // (variant << pb) | position
+        const uint32_t v = (uint32_t)(e >> pb);
+        const uint64_t i = e & ((1ull << pb) - 1ull);
+        refs[k] = i;
+        if (k == 0 || (uint32_t)(ent[k - 1] >> pb) != v) count[v] = (uint32_t)k;  // segment start of variant v
+        if (((check >> v) & 1ull) && !key_eq_at(A, Bs[v], i)) atomicAdd(&nbad[v], 1u);
+    }
+}
+
+// ---- batched walk: (variant, position) leaf entries in ascending order without a sort (round 5) ----
+// One bit per (variant, position) over k x n bits (all-zero between calls): set from the level-0 frontier
+// (device count), per-block popcounts, an exclusive scan of the block counts, then each block writes its
+// entries in order and clears its words. Replaces a host readback of the frontier size + a 5-launch
+// radix sort of the entries (configs[4]: ~0.15 ms per step).
+constexpr uint32_t VP_WORDS = 1024;  // bitmap words per block: 256 threads x 4
+__device__ __forceinline__ uint4 vp_words(const uint32_t *bm, uint64_t w0, uint64_t words) {
+    if (w0 + 3 < words) return *reinterpret_cast<const uint4 *>(bm + w0);
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (w0 < words) x.x = bm[w0];
+    if (w0 + 1 < words) x.y = bm[w0 + 1];
+    if (w0 + 2 < words) x.z = bm[w0 + 2];
+    return x;
+}
+__global__ void k_vpos_setbits(const uint64_t *__restrict__ f, const uint32_t *__restrict__ mdev, uint64_t n,
+                               uint32_t *__restrict__ bm) {
+    const uint64_t m = *mdev;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = f[i];  // (variant << 32) | position
+        const uint64_t g = (e >> 32) * n + (e & 0xFFFFFFFFull);
+        atomicOr(bm + (g >> 5), 1u << (g & 31));
+    }
+}
+__global__ __launch_bounds__(256) void k_vpos_count(const uint32_t *__restrict__ bm, uint64_t words,
+                                                    uint32_t *__restrict__ bc) {
+    __shared__ uint32_t red[4];
+    const uint64_t w0 = (uint64_t)blockIdx.x * VP_WORDS + 4 * threadIdx.x;
+    const uint4 x = vp_words(bm, w0, words);
+    uint32_t c = __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bc[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ __launch_bounds__(256) void k_vpos_emit(uint32_t *__restrict__ bm, uint64_t words,
+                                                   const uint32_t *__restrict__ boff, uint64_t n, int pb,
+                                                   uint64_t *__restrict__ out) {
+    if (boff[blockIdx.x + 1] == boff[blockIdx.x]) return;  // no entry in this block (its words are zero)
+    __shared__ uint32_t tot_w[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t w0 = (uint64_t)blockIdx.x * VP_WORDS + 4 * threadIdx.x;
+    const uint4 x = vp_words(bm, w0, words);
+    const uint32_t c = __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    const uint32_t v = wave_incl_scan<uint32_t>(c);
+    if (lane == 63) tot_w[wave] = v;
+    __syncthreads();
+    uint64_t o = boff[blockIdx.x] + (v - c);
+    for (uint32_t w = 0; w < wave; ++w) o += tot_w[w];
+    if (!c) return;
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        for (uint32_t b = xs[q]; b; b &= b - 1) {
+            const uint64_t g = (w0 + q) * 32 + (uint32_t)(__ffs(b) - 1);
+            const uint64_t vv = g / n;
+            out[o++] = (vv << pb) | (g - vv * n);
+        }
+    }
+    if (w0 + 3 < words) {
+        *reinterpret_cast<uint4 *>(bm + w0) = make_uint4(0, 0, 0, 0);
+    } else {
+        for (int q = 0; q < 4; ++q)
+            if (w0 + q < words) bm[w0 + q] = 0;
+    }
 }
 
 // Divergent leaf positions (sorted): refs of keys equal on both sides; counts positions whose keys
@@ -1033,9 +1103,25 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
 }
 
 void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs,
-                                 uint64_t check, uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st) {
+                                 uint64_t check, uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st,
+                                 const uint32_t *mdev) {
     if (!m) return;
-    hipLaunchKernelGGL(k_topdown_leaves_batch, grid1d(m), dim3(256), 0, st, ent, m, pb, A, Bs, check, refs, nbad, count);
+    const dim3 g = mdev ? dim3((uint32_t)std::min<uint64_t>(ceil_div(m, 256), 2048)) : grid1d(m);
+    hipLaunchKernelGGL(k_topdown_leaves_batch, g, dim3(256), 0, st, ent, m, pb, A, Bs, check, refs, nbad, count, mdev);
+    MKV_LAUNCH_CHECK();
+}
+
+uint64_t vpos_scratch_words(uint64_t bits) { return 2 * (ceil_div((bits + 31) / 32, VP_WORDS) + 2); }
+
+void launch_vpos_sorted_dev(const uint64_t *f, const uint32_t *mdev, uint64_t cap, uint64_t n, uint32_t k, int pb,
+                            uint32_t *bm, uint32_t *bc, void *scan_scr, uint64_t *out, hipStream_t st) {
+    const uint64_t words = ((uint64_t)k * n + 31) / 32, nb = ceil_div(words, VP_WORDS);
+    uint32_t *boff = bc + nb + 1;
+    hipLaunchKernelGGL(k_vpos_setbits, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap ? cap : 1, 256), 2048)), dim3(256),
+                       0, st, f, mdev, n, bm);
+    hipLaunchKernelGGL(k_vpos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
+    exclusive_scan_u32(bc, boff, nb, boff + nb, scan_scr, st);
+    hipLaunchKernelGGL(k_vpos_emit, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, boff, n, pb, out);
     MKV_LAUNCH_CHECK();
 }
 

@@ -258,7 +258,14 @@ void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t 
 // ent: sorted (variant << pb) | position.
 // check: bit v set = variant v's keys at its divergent positions are compared with the base's.
 void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs, uint64_t check,
-                                 uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st);
+                                 uint64_t *refs, uint32_t *nbad, uint32_t *count, hipStream_t st,
+                                 const uint32_t *mdev = nullptr);
+// Level-0 entries (variant << 32 | position; *mdev of them in f, at most cap) -> (variant << pb | position)
+// in ascending order in out, through a k x n-bit bitmap bm (all-zero before and after) and bc
+// (vpos_scratch_words(k x n) words).
+uint64_t vpos_scratch_words(uint64_t bits);
+void launch_vpos_sorted_dev(const uint64_t *f, const uint32_t *mdev, uint64_t cap, uint64_t n, uint32_t k, int pb,
+                            uint32_t *bm, uint32_t *bc, void *scan_scr, uint64_t *out, hipStream_t st);
 // key[k] = (variant << pb) | position of frontier entry (variant << 32) | position; val[k] = k.
 void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st);
 // Anti-entropy exchange: digests of level nodes by index (absent -> zeros); flags of indices whose local

@@ -286,6 +286,8 @@ struct mkv_tree {
     std::shared_ptr<PinnedBlock> tail_blk;      // its staging block (reused while no result holds it)
     uint64_t td_bm_words = 0;       // words of td_bm known to be zero
     DevBuf tb_f0, tb_f1, tb_sides, tb_screen;  // batched top-down walk
+    DevBuf tb_bm, tb_bc;            // its (variant, position) bitmap (all-zero between calls) + block counts
+    uint64_t tb_bm_words = 0;       // words of tb_bm known to be zero
     DevBuf x_idx, x_dig, x_flag;                // anti-entropy exchange requests
     DevBuf w_scan, w_gets, w_nl1, w_nl2, w_scr, w_ks, w_kl, w_vs, w_vl, w_found, w_rank;  // wire ingestion
     DevBuf d_seam, d_S, d_fr;
@@ -2563,7 +2565,7 @@ static bool keys_from_refs_dev(mkv_tree *t, const uint64_t *refs, uint64_t m, co
 // runs on st3 and the call returns without waiting for it; mkv_keylist_get waits when the bytes are
 // first read. The caller's next work (the next step's updates) overlaps the copy.
 static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, uint64_t m, const DiffSide &A,
-                                            const DiffSide &B, uint64_t klen = 0) {
+                                            const DiffSide &B, uint64_t klen = 0, bool wait_st = true) {
     auto *l = new mkv_keylist();
     try {
         if (m) {
@@ -2605,7 +2607,7 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
             l->bytes = l->blk->p + kpos;
             // the caller reads counters its own work on st wrote into pinned memory (topdown_batch: the
             // per-variant check and segment words); the length path above waited already
-            if (klen) wait_stream(t, t->st);
+            if (klen && wait_st) wait_stream(t, t->st);
         }
     } catch (...) {
         delete l;
@@ -2681,6 +2683,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
 // equal): frontier entries carry the variant id, so each level is one launch for all of them.
 // res[i] = keylist, or nullptr when variant i's key set turned out to differ (caller diffs it pairwise).
 // Returns false (nothing decided) when the level-4 frontier says the walk is not worth finishing.
+constexpr uint64_t VPOS_MAX_BITS = 1ull << 33;  // (variant, position) bitmap of the batched walk: <= 1 GiB
 static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<const mkv_tree *> &vs,
                           std::vector<mkv_keylist *> &res) {
     const uint32_t k = (uint32_t)vs.size();
@@ -2736,37 +2739,65 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         }
     }
     prof_end(t, pwalk);
-    const uint32_t *hc = d2h_u32s(t, cnt, (uint32_t)L + 2);
-    if (hc[L + 1] != 0) return false;  // the gate stopped the walk: not worth finishing
-    const uint64_t m = hc[0];
     uint32_t *nbad = cnt + L + 2, *vcount = nbad + k;
-    // per-variant key-check failures and segment starts come back through pinned memory with the
-    // key list's own wait (a pageable readback here would hold the host until the sort finishes)
+    // per-variant key-check failures and segment starts come back through pinned memory
     static_assert(2 * TD_MAX_VARIANTS * 4 <= 512, "h_small holds the batched-walk counters");
     uint32_t *hb = reinterpret_cast<uint32_t *>(t->h_small + 64);
     for (uint32_t i = 0; i < k; ++i) hb[i] = 0;
-    uint64_t *refs = ens<uint64_t>(t->d_refs, m + 1);
     const DiffSide A = side_of(a);
-    if (m) {
-        const int pb = std::max(1, bits_for(n));
-        const int vb = std::max(1, bits_for(k - 1));
-        uint64_t *k1 = ens<uint64_t>(t->td_k1, m + 1), *k2 = ens<uint64_t>(t->td_k2, m + 1);
-        uint32_t *v1 = ens<uint32_t>(t->td_v1, m + 1), *v2 = ens<uint32_t>(t->td_v2, m + 1);
-        void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
-        launch_pack_entries(fin, m, pb, k1, v1, t->st);
-        const bool sw = radix_sort_pairs(k1, v1, k2, v2, m, 0, pb + vb, radix, t->st);
-        std::vector<DiffSide> hs(k);
-        for (uint32_t i = 0; i < k; ++i) hs[i] = side_of(vs[i]);
-        DiffSide *ds = reinterpret_cast<DiffSide *>(t->tb_sides.ensure(k * sizeof(DiffSide)));
+    const int pb = std::max(1, bits_for(n));
+    std::vector<DiffSide> hs(k);
+    for (uint32_t i = 0; i < k; ++i) hs[i] = side_of(vs[i]);
+    DiffSide *ds = reinterpret_cast<DiffSide *>(t->tb_sides.ensure(k * sizeof(DiffSide)));
+    uint64_t check = 0;  // variants whose key set may differ from the base's
+    for (uint32_t i = 0; i < k; ++i)
+        if (!same_keyset(vs[i], a)) check |= 1ull << i;
+    const uint64_t bits = (uint64_t)k * n;
+    uint64_t m = 0;
+    uint64_t *refs = nullptr;
+    const bool bitmap = bits <= VPOS_MAX_BITS;
+    if (bitmap) {
+        // the level-0 entries ordered on the device from the device count (k_vpos_*), the leaf checks
+        // from the same count: one host wait for the count, the abort flag and the per-variant words
+        const uint64_t words = (bits + 31) / 32;
+        uint32_t *bm = ens<uint32_t>(t->tb_bm, words + 4);
+        if (t->tb_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
+        t->tb_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
+        const uint64_t sw = vpos_scratch_words(bits);
+        uint32_t *bc = ens<uint32_t>(t->tb_bc, sw);
+        void *scr = t->d_diffscr.ensure(scan_scratch_bytes(sw));
+        launch_vpos_sorted_dev(fin, cnt, cap, n, k, pb, bm, bc, scr, fout, t->st);
+        t->tb_bm_words = words;
         MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
         MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
-        uint64_t check = 0;  // variants whose key set may differ from the base's
-        for (uint32_t i = 0; i < k; ++i)
-            if (!same_keyset(vs[i], a)) check |= 1ull << i;
-        launch_topdown_leaves_batch(sw ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
+        refs = fin;  // the level-0 frontier is consumed: its buffer holds the refs
+        launch_topdown_leaves_batch(fout, cap, pb, A, ds, check, refs, nbad, vcount, t->st, cnt);
+        small_d2h(t, t->h_small, cnt, 4ull * (L + 2), t->st);
         small_d2h(t, hb, nbad, 2 * k * 4, t->st);
+        wait_stream(t, t->st);
+        const uint32_t *hc = reinterpret_cast<const uint32_t *>(t->h_small);
+        if (hc[L + 1] != 0) return false;  // the gate stopped the walk: not worth finishing
+        m = hc[0];
+    } else {
+        const uint32_t *hc = d2h_u32s(t, cnt, (uint32_t)L + 2);
+        if (hc[L + 1] != 0) return false;  // the gate stopped the walk: not worth finishing
+        m = hc[0];
+        refs = ens<uint64_t>(t->d_refs, m + 1);
+        if (m) {
+            const int vb = std::max(1, bits_for(k - 1));
+            uint64_t *k1 = ens<uint64_t>(t->td_k1, m + 1), *k2 = ens<uint64_t>(t->td_k2, m + 1);
+            uint32_t *v1 = ens<uint32_t>(t->td_v1, m + 1), *v2 = ens<uint32_t>(t->td_v2, m + 1);
+            void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
+            launch_pack_entries(fin, m, pb, k1, v1, t->st);
+            const bool swp = radix_sort_pairs(k1, v1, k2, v2, m, 0, pb + vb, radix, t->st);
+            MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
+            MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
+            launch_topdown_leaves_batch(swp ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
+            small_d2h(t, hb, nbad, 2 * k * 4, t->st);
+        }
     }
-    mkv_keylist *all = keylist_from_refs_async(t, refs, m, A, A, a->klen_fixed);  // waits for st: hb valid after
+    // waits for st (hb valid after) unless the bitmap path waited already
+    mkv_keylist *all = keylist_from_refs_async(t, refs, m, A, A, a->klen_fixed, !bitmap);
     // segment starts -> per-variant counts (variants appear in ascending order)
     std::vector<uint64_t> cntv(k, 0);
     if (m) {
