@@ -1240,19 +1240,50 @@ __global__ void k_fill_stride_dev(uint64_t *__restrict__ off, const uint32_t *__
         off[k] = (k < m ? k : m) * klen;
 }
 
+// Fixed-length keys (every key of both trees klen bytes): the leaf-key check (check), the offsets
+// min(k, *mdev) x klen for k <= cap_m and the key bytes at k x klen in one launch (the offsets are
+// known per position, so no thread waits for another's).
+__global__ void k_tail_fixed_dev(const uint64_t *__restrict__ refs, const uint32_t *__restrict__ mdev, uint64_t cap_m,
+                                 uint64_t cap_b, DiffSide A, DiffSide B, int check, uint32_t *__restrict__ nbad,
+                                 uint64_t klen, uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+    const uint64_t m = *mdev;
+    const bool fits = m <= cap_m && m * klen <= cap_b;
+    const uint64_t end = m > cap_m + 1 ? m : cap_m + 1;  // every divergent position is checked, even past cap_m
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < end; k += (uint64_t)gridDim.x * blockDim.x) {
+        if (k <= cap_m) off[k] = (k < m ? k : m) * klen;
+        if (k >= m) continue;
+        const uint64_t i = refs[k];
+        if (check && !key_eq_at(A, B, i)) atomicAdd(nbad, 1u);
+        if (!fits) continue;
+        uint64_t len;
+        const uint8_t *src = key_at(A, i, &len);
+        uint8_t *d = out + k * klen;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(d) | (uintptr_t)len;
+        if ((al & 15) == 0) {
+            for (uint64_t x = 0; x < len; x += 16)
+                *reinterpret_cast<uint4 *>(d + x) = *reinterpret_cast<const uint4 *>(src + x);
+        } else if ((al & 3) == 0) {
+            for (uint64_t x = 0; x < len; x += 4)
+                *reinterpret_cast<uint32_t *>(d + x) = *reinterpret_cast<const uint32_t *>(src + x);
+        } else {
+            for (uint64_t x = 0; x < len; ++x) d[x] = src[x];
+        }
+    }
+}
+
 void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
                           uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen) {
     const dim3 g((uint32_t)std::min<uint64_t>(ceil_div(cap_m, 256), 2048));
-    if (check) hipLaunchKernelGGL(k_td_check_dev, g, dim3(256), 0, st, refs, mdev, A, B, nbad);
-    if (klen) {  // every key of both trees has length klen
-        hipLaunchKernelGGL(k_fill_stride_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)), dim3(256),
-                           0, st, off, mdev, cap_m, klen);
+    if (klen) {  // every key of both trees has length klen: check, offsets and key bytes in one launch
+        hipLaunchKernelGGL(k_tail_fixed_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)), dim3(256),
+                           0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, klen, off, kout);
     } else {
+        if (check) hipLaunchKernelGGL(k_td_check_dev, g, dim3(256), 0, st, refs, mdev, A, B, nbad);
         hipLaunchKernelGGL(k_keylens_dev, g, dim3(256), 0, st, refs, mdev, cap_m, A, lens);
         exclusive_scan_u64(lens, off, cap_m, off + cap_m, scan_scr, st);
+        hipLaunchKernelGGL(k_keys_dev, g, dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, off, kout);
     }
-    hipLaunchKernelGGL(k_keys_dev, g, dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, off, kout);
     const uint64_t cb = std::min<uint64_t>(ceil_div(std::max(8 * (cap_m + 1), cap_b) / 16 + 1, 256), 2048);
     hipLaunchKernelGGL(k_tail_copy_dev, dim3((uint32_t)cb), dim3(256), 0, st, off, kout, mdev, cap_m, cap_b, doff, dkeys);
     MKV_LAUNCH_CHECK();
