@@ -667,3 +667,30 @@ def test_sort_window_hint_across_builds(oracle_lib):
             pairs = _shared_prefix_pairs(rng, shape, 20_000)
         t.build([k for k, _ in pairs], [v for _, v in pairs])
         assert_tree_equal(t, oracle_lib.OracleTree.from_pairs(pairs), check_levels=False)
+
+
+@pytest.mark.parametrize("layout", ["disjoint", "overlap_half", "interleaved", "reversed_disjoint"])
+def test_merge_join_partition_far_from_interpolation_vs_oracle(oracle_lib, layout):
+    """Equal leaf counts with different key sets (fingerprints differ: straight to the merge-join) whose
+    merge-path splits lie far from the |A| / (|A| + |B|) interpolation the partition's first, exponential
+    round probes around (k_diff.hip k_diff_partition): up to n/2 = 100K positions away, beyond its
+    +-65,535 reach, so the 33-ary rounds finish the search."""
+    n = 200_000
+    keys = sorted({b"%010d" % (i * 104729 % 1000000007) for i in range(2 * n + 10)})[: 2 * n]
+    if layout == "disjoint":
+        ka, kb = keys[:n], keys[n:]
+    elif layout == "reversed_disjoint":
+        ka, kb = keys[n:], keys[:n]
+    elif layout == "overlap_half":
+        ka, kb = keys[:n], keys[n // 2: n // 2 + n]
+    else:
+        ka, kb = keys[0::2], keys[1::2]
+    a_pairs = [(k, b"x") for k in ka]
+    b_pairs = [(k, b"x" if i % 11 else b"y") for i, k in enumerate(kb)]
+    a, b = MerkleTree(), MerkleTree()
+    a.build([k for k, _ in a_pairs], [v for _, v in a_pairs])
+    b.build([k for k, _ in b_pairs], [v for _, v in b_pairs])
+    oa = oracle_lib.OracleTree.from_pairs(a_pairs)
+    ob = oracle_lib.OracleTree.from_pairs(b_pairs)
+    assert a.diff_keys_bytes(b) == oa.diff(ob)
+    assert b.diff_keys_bytes(a) == ob.diff(oa)
