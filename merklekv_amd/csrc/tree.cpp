@@ -2281,6 +2281,9 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
+    t->walk_jumps.clear();  // mkv_tree_walk_stats describes this walk
+    t->walk_L = (uint32_t)L;
+    t->walk_k = 1;
     if (!a->sharded && !b->sharded && L > 1) {
         // Unsharded: seed with the root, then jump 4 levels per launch (landing on level 4 for the
         // key-shift check and on level 0).
@@ -2291,6 +2294,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
         for (size_t q = 1; q < T.size(); ++q) {
             const size_t l = T[q - 1], lt = T[q];
             const int k = (int)(l - lt);
+            t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
             launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
                                 cnt + lt, std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
             std::swap(fin, fout);
@@ -2304,6 +2308,7 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
         uint64_t r[2];
         level_roots(a, l - 1, r);
         const uint64_t a_par = l < L ? a->lev_base[l] : 0, max_par = l < L ? a->lev_cnt[l] : 0;
+        if (l < L) t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)(l - 1));  // (fringe-root seeds not counted)
         launch_topdown_level(na + 32 * a->lev_off[l - 1], nb + 32 * b->lev_off[l - 1], a->lev_cnt[l - 1], a_par,
                              a->lev_base[l - 1], r[0], r[1], fin, cnt + l, fout, cnt + (l - 1), max_par, t->st);
         std::swap(fin, fout);
