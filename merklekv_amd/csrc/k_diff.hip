@@ -793,6 +793,35 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump(const uint8_t *__re
     }
 }
 
+// Sharded form (a shard's owned ranges per level): entry p of level l is global node p + a_par, its
+// descendants at level l - k are global ((p + a_par) << k) + j, local minus a_desc (an owned node's leaves
+// are all owned, so they are too). After the frontier's descendants come the seeds: the fringe roots of
+// the levels this jump crosses, which no frontier entry covers, each as its span of descendants.
+__global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_sh(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
+                                                        uint64_t desc_count, int k, uint64_t a_par, uint64_t a_desc,
+                                                        TdSeeds S, const uint32_t *__restrict__ fin,
+                                                        const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
+                                                        uint32_t *__restrict__ nout) {
+    __shared__ uint32_t sapp[17];
+    const uint32_t cnt = *nin;
+    const uint64_t totf = (uint64_t)cnt << k, tot = totf + S.total;
+    const uint64_t mask = (1ull << k) - 1ull;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        bool d = false;
+        uint64_t c = UINT64_MAX;
+        if (t < totf) {
+            c = ((((uint64_t)fin[t >> k] + a_par) << k) | (t & mask)) - a_desc;
+        } else if (t < tot) {
+            uint32_t u = (uint32_t)(t - totf), i = 0;
+            while (i + 1 < S.n && u >= S.span[i]) u -= S.span[i++];
+            c = S.first[i] + u;
+        }
+        if (c < desc_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
+        block_append<uint32_t>(d, (uint32_t)c, fout, nout, sapp);
+    }
+}
+
 // Batched form: entries (variant << 32) | node.
 __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_batch(const uint8_t *__restrict__ ca, TdVariants V,
                                                            uint64_t desc_off, uint64_t desc_count, int k,
@@ -1144,6 +1173,14 @@ void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_cou
     const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
     hipLaunchKernelGGL(k_topdown_jump, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, desc_count, k, fin, nin, fout,
                        nout);
+    MKV_LAUNCH_CHECK();
+}
+void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, uint64_t a_par,
+                            uint64_t a_desc, const TdSeeds &S, const uint32_t *fin, const uint32_t *nin, uint32_t *fout,
+                            uint32_t *nout, uint64_t max_desc, hipStream_t st) {
+    const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc + S.total ? max_desc + S.total : 1, TD_THREADS), 2048);
+    hipLaunchKernelGGL(k_topdown_jump_sh, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, desc_count, k, a_par,
+                       a_desc, S, fin, nin, fout, nout);
     MKV_LAUNCH_CHECK();
 }
 void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,

@@ -252,6 +252,18 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
 // at the target level (desc_count nodes there). max_desc: upper bound on parents << k (grid sizing).
 void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st);
+// Sharded plans: the frontier holds local indices of level l (global = local + a_par), descendants are
+// addressed at level l - k as global - a_desc; seeds = a shard's fringe roots at levels lt..l (owned nodes
+// whose parent is not owned), each compared through its span of level-lt descendants starting at first[i].
+constexpr int TD_MAX_SEEDS = 12;
+struct TdSeeds {
+    uint32_t n, total;
+    uint32_t span[TD_MAX_SEEDS];
+    uint64_t first[TD_MAX_SEEDS];
+};
+void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, uint64_t a_par,
+                            uint64_t a_desc, const TdSeeds &S, const uint32_t *fin, const uint32_t *nin, uint32_t *fout,
+                            uint32_t *nout, uint64_t max_desc, hipStream_t st);
 void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
                                uint64_t max_desc, hipStream_t st);

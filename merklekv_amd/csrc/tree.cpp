@@ -2247,6 +2247,25 @@ static bool same_plan(const mkv_tree *a, const mkv_tree *b) {
 
 constexpr size_t TD_CHECK_LEVEL = 4;
 
+// Seeds of a sharded jump from level l to lt: the shard's fringe roots (owned nodes whose parent is not
+// owned, level_roots) of levels lt .. l - 1, and of l itself on the first jump (from the top, where the
+// frontier starts empty), each as its span of level-lt descendants. No frontier entry covers them.
+static TdSeeds fringe_seeds(const mkv_tree *a, size_t l, size_t lt, bool top) {
+    TdSeeds S{};
+    for (size_t j = lt; j < l || (top && j == l); ++j) {
+        uint64_t r[2];
+        level_roots(a, j, r);
+        for (int z = 0; z < 2; ++z) {
+            if (r[z] == UINT64_MAX) continue;
+            if (S.n >= (uint32_t)TD_MAX_SEEDS) throw Error(ST_ESTATE, "too many fringe roots in one jump");
+            S.first[S.n] = ((r[z] + a->lev_base[j]) << (j - lt)) - a->lev_base[lt];
+            S.span[S.n] = 1u << (j - lt);
+            S.total += S.span[S.n++];
+        }
+    }
+    return S;
+}
+
 // Levels the jumping walk lands on: the top level, then every multiple of 4 below it down to 0.
 // fine: below level 8 every multiple of 2 instead. A jump of k levels reads 2^k digests per frontier
 // node; near the leaves of a dense diff the frontier holds about one node per divergent leaf, so
@@ -2303,23 +2322,30 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
                 if (h[L + 1] != 0 || 2 * (uint64_t)h[lt] > a->lev_cnt[lt]) return false;
             }
         }
-    } else
-    for (size_t l = L; l >= 1; --l) {  // parents at level l (none at l == L) -> children at level l-1
-        uint64_t r[2];
-        level_roots(a, l - 1, r);
-        const uint64_t a_par = l < L ? a->lev_base[l] : 0, max_par = l < L ? a->lev_cnt[l] : 0;
-        if (l < L) t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)(l - 1));  // (fringe-root seeds not counted)
-        launch_topdown_level(na + 32 * a->lev_off[l - 1], nb + 32 * b->lev_off[l - 1], a->lev_cnt[l - 1], a_par,
-                             a->lev_base[l - 1], r[0], r[1], fin, cnt + l, fout, cnt + (l - 1), max_par, t->st);
-        std::swap(fin, fout);
-        // Inserted/deleted keys shift every later leaf position, so nearly every node below the first
-        // shift diverges. One readback at level 4 (16-leaf nodes: a 0.1 % value-only divergence marks
-        // ~1.6 % of them) stops such a walk before the expensive bottom levels; the merge-join is exact
-        // for any key sets.
-        if (l - 1 == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
-            const uint32_t *h = d2h_u32s(t, cnt, (uint32_t)L + 2);
-            if (h[L + 1] != 0 || 2 * (uint64_t)h[l - 1] > a->lev_cnt[l - 1]) return false;
+    } else if (L > 1) {
+        // Sharded: the same jumps from an empty top frontier, the shard's fringe roots seeded into the jump
+        // whose levels they sit on (fringe_seeds). Inserted/deleted keys shift every later leaf position, so
+        // nearly every node below the first shift diverges: one readback at level 4 (16-leaf nodes: a 0.1 %
+        // value-only divergence marks ~1.6 % of them) stops such a walk before the expensive bottom levels;
+        // the merge-join is exact for any key sets.
+        const std::vector<size_t> T = jump_targets(L);
+        for (size_t q = 1; q < T.size(); ++q) {
+            const size_t l = T[q - 1], lt = T[q];
+            const int k = (int)(l - lt);
+            t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
+            launch_topdown_jump_sh(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, a->lev_base[l],
+                                   a->lev_base[lt], fringe_seeds(a, l, lt, q == 1), fin, cnt + l, fout, cnt + lt,
+                                   std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
+            std::swap(fin, fout);
+            if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2) {
+                const uint32_t *h = d2h_u32s(t, cnt, (uint32_t)L + 2);
+                if (h[L + 1] != 0 || 2 * (uint64_t)h[lt] > a->lev_cnt[lt]) return false;
+            }
         }
+    } else {  // a one-leaf plan: the leaf is the shard's only root
+        launch_topdown_jump_sh(na, nb, a->lev_cnt[0], 0, 0, a->lev_base[0], fringe_seeds(a, 0, 0, true), fin, cnt + 1,
+                               fout, cnt, 0, t->st);
+        std::swap(fin, fout);
     }
     const uint32_t *h = d2h_u32s(t, cnt, (uint32_t)L + 2);
     if (h[L + 1] != 0) return false;  // key sets differ (screen): the merge-join is exact
@@ -2398,9 +2424,12 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
-    launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin, cnt + L,
-                         fout, cnt + (L - 1), 0, t->st);
-    std::swap(fin, fout);
+    const bool sh = a->sharded;  // same plan: b is sharded the same way
+    if (!sh) {
+        launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
+                             cnt + L, fout, cnt + (L - 1), 0, t->st);
+        std::swap(fin, fout);
+    }  // sharded: the frontier at the top level starts empty (cnt[L - 1] = 0); the roots come in as seeds
     const std::vector<size_t> T = jump_targets(L);
     t->walk_jumps.clear();  // mkv_tree_walk_stats describes this walk (one variant)
     t->walk_L = (uint32_t)L;
@@ -2409,8 +2438,15 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         const size_t l = T[q - 1], lt = T[q];
         const int k = (int)(l - lt);
         t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
-        launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
-                            cnt + lt, std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40), t->st);
+        const uint64_t maxd = std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40);
+        if (!sh) {
+            launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
+                                cnt + lt, maxd, t->st);
+        } else {
+            launch_topdown_jump_sh(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, a->lev_base[l],
+                                   a->lev_base[lt], fringe_seeds(a, l, lt, q == 1), fin, cnt + l, fout, cnt + lt, maxd,
+                                   t->st);
+        }
         std::swap(fin, fout);
         if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2)
             launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)lt, a->lev_cnt[lt], t->st);
@@ -2645,7 +2681,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
     uint64_t m = 0;
     bool done = false;
     const uint64_t nwords = (A.n + 31) / 32;
-    if (!dev && A.n > 0 && same_plan(a, b) && !keysets_differ(a, b) && !a->sharded && !b->sharded && a->lev_S.size() > 1 &&
+    if (!dev && A.n > 0 && same_plan(a, b) && !keysets_differ(a, b) && a->sharded == b->sharded && a->lev_S.size() > 1 &&
         ceil_div(nwords, 1024) <= 8192) {
         int fb = 0;
         mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);

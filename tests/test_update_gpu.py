@@ -183,7 +183,8 @@ def _recombine(trees, N):
     return [t.shard_combine(fr, len(trees), N) for t in trees]
 
 
-@pytest.mark.parametrize("n,cuts", [(1001, (333, 700)), (40000, (1, 16384, 16385, 39999)), (7, (3,))])
+@pytest.mark.parametrize("n,cuts", [(1001, (333, 700)), (40000, (1, 16384, 16385, 39999)), (7, (3,)),
+                                    (200003, (1, 2, 77777, 131072, 131073, 199999, 200002))])
 def test_sharded_dirty_update_and_topdown_diff(n, cuts):
     kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
     trees, ks, bounds, roots = _shard_trees(kb, ko, vb, vo, cuts)
