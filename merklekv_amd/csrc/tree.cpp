@@ -2279,8 +2279,8 @@ static std::vector<size_t> jump_targets(size_t L, bool fine = false) {
 
 // Top-down diff of two trees with identical level plans (equal leaf counts, and for shards the same
 // global offset and size): node (l, j) covers the same leaf positions in both. Equal digests prune
-// whole subtrees; only the divergent frontier is expanded, level by level, starting from the local
-// roots (the root, or a shard's fringe roots). Returns false (caller falls back to the merge-join)
+// whole subtrees; only the divergent frontier is expanded, up to 4 levels per launch, starting from the
+// local roots (the root, or a shard's fringe roots seeded into the jumps). Returns false (caller falls back to the merge-join)
 // when a divergent leaf position holds different keys, i.e. the key sets differ there.
 static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, const DiffSide &A, const DiffSide &B,
                          uint64_t *refs, uint64_t *m_out, const uint32_t **nbad_out) {
@@ -2380,7 +2380,8 @@ static bool topdown_diff(mkv_tree *t, const mkv_tree *a, const mkv_tree *b, cons
     return true;
 }
 
-// Unsharded top-down pair diff queued whole before ONE host wait (round 3): the jumping walk, the level-4
+// Top-down pair diff queued whole before ONE host wait (round 3; shards too since round 5, their fringe
+// roots seeded into the jumps): the jumping walk, the level-4
 // abort test on the device (k_td_gate), the divergent positions (bitmap, device count) written straight
 // into refs, the leaf-key check, key lengths, scan, key gather and the copy into a mapped pinned block
 // sized from earlier calls. Returns the key list, or nullptr with *fallback = 1 (key sets differ or the
