@@ -775,12 +775,23 @@ __global__ __launch_bounds__(256) void k_sample_pfx(const uint64_t *__restrict__
 // level: R5 promotion keeps the implicit arrays aligned). Comparing those 2^k nodes directly — they are
 // contiguous, so the loads coalesce — replaces k dependent level launches: the walk is latency-bound,
 // and a descendant can only differ when its ancestors do. One thread per (parent, descendant).
+// gate != nullptr: the level-4 abort test of the one-wait pair diff, made by every workgroup before it
+// starts (the jump from level 4): the key-set screen word gate[word] set, or a frontier over half the level
+// (nin > level_count / 2) -> no descendant is compared and workgroup 0 sets bit 31 of the word (merge-join).
+// Every workgroup reaches the same verdict: nin is not written here, and the word is nonzero either way.
 __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump(const uint8_t *__restrict__ ca, const uint8_t *__restrict__ cb,
                                                      uint64_t desc_count, int k, const uint32_t *__restrict__ fin,
                                                      const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
-                                                     uint32_t *__restrict__ nout) {
+                                                     uint32_t *__restrict__ nout, uint32_t *__restrict__ gate,
+                                                     uint32_t word, uint64_t level_count) {
     __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
+    // (a plain uniform load: one scalar-cache read per wave; a per-lane coherent load of the one word
+    // from every wave of the grid serialises on its L2 channel, 27 -> 134 us for this launch)
+    if (gate && (gate[word] != 0 || 2ull * cnt > level_count)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(gate + word, 0x80000000u);
+        return;
+    }
     const uint64_t tot = (uint64_t)cnt << k;
     const uint64_t mask = (1ull << k) - 1ull;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
@@ -1169,10 +1180,11 @@ void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key,
 }
 
 void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
-                         const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st) {
+                         const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st,
+                         uint32_t *gate, uint32_t word, uint64_t level_count) {
     const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
     hipLaunchKernelGGL(k_topdown_jump, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, desc_count, k, fin, nin, fout,
-                       nout);
+                       nout, gate, word, level_count);
     MKV_LAUNCH_CHECK();
 }
 void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, uint64_t a_par,

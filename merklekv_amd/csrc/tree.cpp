@@ -2440,17 +2440,18 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         const int k = (int)(l - lt);
         t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
         const uint64_t maxd = std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40);
+        // the level-4 abort test rides on the jump from level 4 (no launch of its own)
+        const bool gate = l == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2;
         if (!sh) {
             launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
-                                cnt + lt, maxd, t->st);
+                                cnt + lt, maxd, t->st, gate ? cnt : nullptr, (uint32_t)L + 1, a->lev_cnt[l]);
         } else {
+            if (gate) launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)l, a->lev_cnt[l], t->st);
             launch_topdown_jump_sh(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, a->lev_base[l],
                                    a->lev_base[lt], fringe_seeds(a, l, lt, q == 1), fin, cnt + l, fout, cnt + lt, maxd,
                                    t->st);
         }
         std::swap(fin, fout);
-        if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2)
-            launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)lt, a->lev_cnt[lt], t->st);
     }
     if (t->td_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
     t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
