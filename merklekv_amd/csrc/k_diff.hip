@@ -783,7 +783,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump(const uint8_t *__re
                                                      uint64_t desc_count, int k, const uint32_t *__restrict__ fin,
                                                      const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
                                                      uint32_t *__restrict__ nout, uint32_t *__restrict__ gate,
-                                                     uint32_t word, uint64_t level_count) {
+                                                     uint32_t word, uint64_t level_count, uint32_t *__restrict__ bm) {
     __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
     // (a plain uniform load: one scalar-cache read per wave; a per-lane coherent load of the one word
@@ -800,6 +800,7 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump(const uint8_t *__re
         uint64_t c = UINT64_MAX;
         if (t < tot) c = ((uint64_t)fin[t >> k] << k) | (t & mask);
         if (c < desc_count) d = !digest_eq(ca + 32ull * c, cb + 32ull * c);
+        if (bm && d) atomicOr(bm + (c >> 5), 1u << (c & 31));  // landing on the leaves: the position bitmap
         block_append<uint32_t>(d, (uint32_t)c, fout, nout, sapp);
     }
 }
@@ -1181,10 +1182,10 @@ void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key,
 
 void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st,
-                         uint32_t *gate, uint32_t word, uint64_t level_count) {
+                         uint32_t *gate, uint32_t word, uint64_t level_count, uint32_t *bm) {
     const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
     hipLaunchKernelGGL(k_topdown_jump, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, desc_count, k, fin, nin, fout,
-                       nout, gate, word, level_count);
+                       nout, gate, word, level_count, bm);
     MKV_LAUNCH_CHECK();
 }
 void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, uint64_t a_par,

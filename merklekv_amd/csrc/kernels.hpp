@@ -251,10 +251,11 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
 // Jump k levels down from divergent parents (unsharded plans): fout gets every divergent descendant
 // at the target level (desc_count nodes there). max_desc: upper bound on parents << k (grid sizing).
 // gate: the one-wait pair diff's level-4 abort test folded into the jump from level 4 (k_td_gate's rule on
-// gate[word] and *nin against level_count); nullptr = none.
+// gate[word] and *nin against level_count); nullptr = none. bm: a jump landing on the leaves also sets each
+// divergent position's bit there (zeroed bitmap; positions_sorted_bitmap_dev then skips its set pass).
 void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st,
-                         uint32_t *gate = nullptr, uint32_t word = 0, uint64_t level_count = 0);
+                         uint32_t *gate = nullptr, uint32_t word = 0, uint64_t level_count = 0, uint32_t *bm = nullptr);
 // Sharded plans: the frontier holds local indices of level l (global = local + a_par), descendants are
 // addressed at level l - k as global - a_desc; seeds = a shard's fringe roots at levels lt..l (owned nodes
 // whose parent is not owned), each compared through its span of level-lt descendants starting at first[i].

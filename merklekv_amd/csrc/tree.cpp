@@ -563,10 +563,10 @@ bool positions_sorted_bitmap(const uint32_t *f, uint64_t m, uint64_t n, uint32_t
 
 // The same from a device count (*mdev entries of f), positions into out (room for every position < n).
 bool positions_sorted_bitmap_dev(const uint32_t *f, const uint32_t *mdev, uint64_t n, uint32_t *bm, uint32_t *bc,
-                                 uint64_t *out, hipStream_t st) {
+                                 uint64_t *out, hipStream_t st, bool bits_set) {
     const uint64_t words = (n + 31) / 32, nb = ceil_div(words, POS_BLOCK_WORDS);
     if (nb > POS_MAX_BLOCKS) return false;
-    hipLaunchKernelGGL(k_pos_setbits_dev, dim3(1024), dim3(256), 0, st, f, mdev, bm);
+    if (!bits_set) hipLaunchKernelGGL(k_pos_setbits_dev, dim3(1024), dim3(256), 0, st, f, mdev, bm);
     hipLaunchKernelGGL(k_pos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
     hipLaunchKernelGGL(k_pos_emit, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc, out);
     MKV_LAUNCH_CHECK();
@@ -2426,6 +2426,10 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
     const bool sh = a->sharded;  // same plan: b is sharded the same way
+    // the position bitmap is all-zero between calls; zeroed here (grown) before the jump that lands on the
+    // leaves sets its bits
+    if (t->td_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
+    t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
     if (!sh) {
         launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
                              cnt + L, fout, cnt + (L - 1), 0, t->st);
@@ -2444,7 +2448,8 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         const bool gate = l == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2;
         if (!sh) {
             launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
-                                cnt + lt, maxd, t->st, gate ? cnt : nullptr, (uint32_t)L + 1, a->lev_cnt[l]);
+                                cnt + lt, maxd, t->st, gate ? cnt : nullptr, (uint32_t)L + 1, a->lev_cnt[l],
+                                lt == 0 ? bm : nullptr);
         } else {
             if (gate) launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)l, a->lev_cnt[l], t->st);
             launch_topdown_jump_sh(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, a->lev_base[l],
@@ -2453,9 +2458,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         }
         std::swap(fin, fout);
     }
-    if (t->td_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
-    t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
-    positions_sorted_bitmap_dev(fin, cnt, n, bm, bc, refs, t->st);  // side-A refs = sorted positions
+    positions_sorted_bitmap_dev(fin, cnt, n, bm, bc, refs, t->st, !sh);  // side-A refs = sorted positions
     t->td_bm_words = words;
     launch_diff_tail_dev(refs, cnt, A, B, !same_keyset(a, b), cnt + L + 1, cap_m, cap_b, lens, off, scr, kout, blk->dp,
                          blk->dp + kpos, t->st, pair_klen(a, b));
