@@ -1043,7 +1043,8 @@ __global__ void k_keys_dev(const uint64_t *__restrict__ refs, const uint32_t *__
 // Offsets (m + 1) and key bytes into the mapped pinned block (16-B stores), unless over capacity.
 __global__ __launch_bounds__(256) void k_tail_copy_dev(const uint64_t *__restrict__ off, const uint8_t *__restrict__ kout,
                                                        const uint32_t *__restrict__ mdev, uint64_t cap_m, uint64_t cap_b,
-                                                       uint8_t *__restrict__ doff, uint8_t *__restrict__ dkeys) {
+                                                       uint8_t *__restrict__ doff, uint8_t *__restrict__ dkeys,
+                                                       int copy_offsets) {
     const uint64_t m = *mdev;
     if (m > cap_m) return;
     const uint64_t bytes = off[cap_m];
@@ -1051,9 +1052,11 @@ __global__ __launch_bounds__(256) void k_tail_copy_dev(const uint64_t *__restric
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t no = 8 * (m + 1), nvo = no / 16;
     const uint8_t *so = reinterpret_cast<const uint8_t *>(off);
-    for (uint64_t v = t; v < nvo; v += stride)
-        reinterpret_cast<uint4 *>(doff)[v] = reinterpret_cast<const uint4 *>(so)[v];
-    if (t < no - nvo * 16) doff[nvo * 16 + t] = so[nvo * 16 + t];
+    if (copy_offsets) {
+        for (uint64_t v = t; v < nvo; v += stride)
+            reinterpret_cast<uint4 *>(doff)[v] = reinterpret_cast<const uint4 *>(so)[v];
+        if (t < no - nvo * 16) doff[nvo * 16 + t] = so[nvo * 16 + t];
+    }
     const uint64_t nvk = bytes / 16;
     for (uint64_t v = t; v < nvk; v += stride)
         reinterpret_cast<uint4 *>(dkeys)[v] = reinterpret_cast<const uint4 *>(kout)[v];
@@ -1323,7 +1326,8 @@ __global__ void k_tail_fixed_dev(const uint64_t *__restrict__ refs, const uint32
 
 void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
-                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen) {
+                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen,
+                          bool host_offsets) {
     const dim3 g((uint32_t)std::min<uint64_t>(ceil_div(cap_m, 256), 2048));
     if (klen) {  // every key of both trees has length klen: check, offsets and key bytes in one launch
         hipLaunchKernelGGL(k_tail_fixed_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)), dim3(256),
@@ -1335,7 +1339,8 @@ void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const Diff
         hipLaunchKernelGGL(k_keys_dev, g, dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, off, kout);
     }
     const uint64_t cb = std::min<uint64_t>(ceil_div(std::max(8 * (cap_m + 1), cap_b) / 16 + 1, 256), 2048);
-    hipLaunchKernelGGL(k_tail_copy_dev, dim3((uint32_t)cb), dim3(256), 0, st, off, kout, mdev, cap_m, cap_b, doff, dkeys);
+    hipLaunchKernelGGL(k_tail_copy_dev, dim3((uint32_t)cb), dim3(256), 0, st, off, kout, mdev, cap_m, cap_b, doff, dkeys,
+                       (int)!(klen && host_offsets));
     MKV_LAUNCH_CHECK();
 }
 

@@ -234,11 +234,14 @@ void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const
 // cnt[word] != 0 or a frontier over half the level: bit 31 set there, frontier emptied); then from the
 // sorted side-A refs (count *mdev on the device): leaf-key check (nbad), key lengths padded to cap_m,
 // scan (total at off[cap_m]), key bytes (cap_b) and their copy into the mapped pinned views doff / dkeys
-// -- skipped when the list outgrows the capacity (the host then copies it from the refs).
+// -- skipped when the list outgrows the capacity (the host then copies it from the refs). host_offsets
+// (fixed-length keys): the host writes the offsets k x klen into doff's block itself; only the key bytes
+// cross PCIe.
 void launch_td_gate(uint32_t *cnt, uint32_t word, uint32_t level, uint64_t level_count, hipStream_t st);
 void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
-                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen = 0);
+                          uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen = 0,
+                          bool host_offsets = false);
 // Batched top-down walk (one base vs up to TD_MAX_VARIANTS trees with the same level plan).
 constexpr int TD_MAX_VARIANTS = 64;
 struct TdVariants {

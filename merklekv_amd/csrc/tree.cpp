@@ -69,7 +69,14 @@ struct EvPair {
 // (mkv_pool_stats) let a caller see whether a slow call paid for page pinning.
 namespace {
 std::mutex g_pool_mu;
-std::vector<std::pair<uint8_t *, size_t>> g_pool;  // free pinned blocks
+// a free pinned block; fill_klen / fill_n: its first fill_n u64 words hold k x fill_klen (the offsets of a
+// fixed-length key list, written by the host once and kept while the block cycles through the pool)
+struct PoolEnt {
+    uint8_t *first;
+    size_t second;
+    uint64_t fill_klen, fill_n;
+};
+std::vector<PoolEnt> g_pool;  // free pinned blocks
 size_t g_pool_bytes = 0;
 std::atomic<uint64_t> g_pin_allocs{0}, g_pin_frees{0}, g_pin_alloc_bytes{0};
 std::atomic<uint64_t> g_pin_ns{0};  // host time spent in hipHostMalloc / hipHostFree
@@ -102,7 +109,10 @@ struct PinnedBlock {
     uint8_t *p = nullptr;
     uint8_t *dp = nullptr;  // the same memory as the device sees it (written by k_copy_to_host)
     size_t cap = 0;
-    explicit PinnedBlock(size_t bytes) {
+    // words [0, fill_n) hold k x fill_klen. Kept through the pool only for an owner that asks for it
+    // (keep_fill) and writes that range through fill_offsets alone; every other acquisition clears it.
+    uint64_t fill_klen = 0, fill_n = 0;
+    explicit PinnedBlock(size_t bytes, bool keep_fill = false) {
         {
             std::lock_guard<std::mutex> lk(g_pool_mu);
             const size_t limit = std::max<size_t>(4 * bytes, 1 << 20);
@@ -114,6 +124,10 @@ struct PinnedBlock {
             if (best != SIZE_MAX) {
                 p = g_pool[best].first;
                 cap = g_pool[best].second;
+                if (keep_fill) {
+                    fill_klen = g_pool[best].fill_klen;
+                    fill_n = g_pool[best].fill_n;
+                }
                 g_pool_bytes -= cap;
                 g_pool.erase(g_pool.begin() + (long)best);
                 map_device();
@@ -127,6 +141,14 @@ struct PinnedBlock {
         g_pin_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         ++g_pin_allocs;
         g_pin_alloc_bytes += cap;
+    }
+    // words [0, n) = k x klen, writing only what an earlier fill of this memory did not leave there
+    void fill_offsets(uint64_t klen, uint64_t n) {
+        uint64_t *o = reinterpret_cast<uint64_t *>(p);
+        const uint64_t from = fill_klen == klen ? std::min(fill_n, n) : 0;
+        for (uint64_t k = from; k < n; ++k) o[k] = k * klen;
+        fill_klen = klen;
+        fill_n = n;
     }
     void map_device() {
         void *d = nullptr;
@@ -157,7 +179,7 @@ struct PinnedBlock {
             pin_free(g_pool[small].first);
             g_pool.erase(g_pool.begin() + (long)small);
         }
-        g_pool.emplace_back(p, cap);
+        g_pool.push_back({p, cap, fill_klen, fill_n});
         g_pool_bytes += cap;
     }
 };
@@ -2417,8 +2439,13 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     const uint64_t kpos = (8 * (cap_m + 1) + 15) & ~uint64_t(15);
     // the staging block is the tree's own, reused call to call unless an earlier result still holds it
     if (!t->tail_blk || t->tail_blk.use_count() > 1 || t->tail_blk->cap < kpos + cap_b + 16)
-        t->tail_blk = std::make_shared<PinnedBlock>(kpos + cap_b + 16);
+        t->tail_blk = std::make_shared<PinnedBlock>(kpos + cap_b + 16, true);
     std::shared_ptr<PinnedBlock> blk = t->tail_blk;
+    const uint64_t klen = pair_klen(a, b);
+    // fixed-length keys: the list's offsets k x klen are written by the host into the staging block (once
+    // per block: they stay there while it cycles through the pool), not copied over PCIe
+    if (!klen) blk->fill_n = 0;  // the device writes the offsets region
+    blk->fill_n = std::min<uint64_t>(blk->fill_n, cap_m + 1);  // the key bytes start at kpos
     const size_t pd = prof_begin(t, "diff");  // the queued device work (the wait excluded)
     MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
     // (one 1,024-thread workgroup zeroing and sampling in a single launch measured slower: 0.238 vs 0.231 ms)
@@ -2461,7 +2488,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     positions_sorted_bitmap_dev(fin, cnt, n, bm, bc, refs, t->st, !sh);  // side-A refs = sorted positions
     t->td_bm_words = words;
     launch_diff_tail_dev(refs, cnt, A, B, !same_keyset(a, b), cnt + L + 1, cap_m, cap_b, lens, off, scr, kout, blk->dp,
-                         blk->dp + kpos, t->st, pair_klen(a, b));
+                         blk->dp + kpos, t->st, klen, klen != 0);
     {  // one launch: divergent positions, screen / abort / leaf-key mismatches, key bytes (when m <= cap_m)
         SmallCopies SC{};
         const uint8_t *srcs[3] = {reinterpret_cast<const uint8_t *>(cnt), reinterpret_cast<const uint8_t *>(cnt + L + 1),
@@ -2477,6 +2504,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     }
     prof_end(t, pd);
     HTRACE("onewait-queued");
+    if (klen) blk->fill_offsets(klen, cap_m + 1);  // while the device works
     sync(t);
     const uint64_t m = (uint32_t)t->h_small[0];
     const uint32_t word = (uint32_t)t->h_small[1];

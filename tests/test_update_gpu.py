@@ -643,6 +643,37 @@ def test_fixed_length_key_lists_follow_key_length_changes():
     assert base.diff_keys_bytes(t3) == ob.diff(o3)
 
 
+def test_fixed_length_offsets_written_by_host_across_pool_cycles():
+    """The one-wait diff of fixed-length keys has the host write the list's offsets k x len into the
+    pinned staging block and keeps them while the block cycles through the pinned pool
+    (tree.cpp PinnedBlock::fill_offsets; only the key bytes cross PCIe). Results of growing and shrinking
+    size and of a second key length, some kept alive across calls so the blocks change hands, must all
+    carry exact offsets and keys (R7, merkle.rs:171-204: the changed keys, sorted)."""
+    n = 60000
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    k2 = [k + b"zz" for k in keys]
+    kb2, ko2 = pack(k2)
+    b1, b2 = MerkleTree(), MerkleTree()
+    b1.build((kb, ko), (vb, vo))
+    b2.build((kb2, ko2), (vb, vo))
+    rng = np.random.default_rng(11)
+    held = []
+    for rnd, m in enumerate([10, 3000, 50, 20000, 5, 8000, 1, 12000]):
+        for bt, ks in ((b1, keys), (b2, k2)):
+            t = bt.clone()
+            idx = sorted(int(i) for i in rng.choice(n, m, replace=False))
+            t.upsert([ks[i] for i in idx], [b"new-%d" % rnd] * m)
+            d = bt.diff_keys_view(t)
+            L = len(ks[0])
+            assert len(d) == m
+            assert np.array_equal(d.offs, np.arange(m + 1, dtype=np.uint64) * np.uint64(L))
+            raw = d.raw.tobytes()
+            assert [raw[i * L:(i + 1) * L] for i in range(m)] == sorted(ks[i] for i in idx)
+            held.append(d)
+        held = held[-3:]
+
+
 def test_batched_diff_per_variant_split_each_call():
     """The batched 1-vs-k diff splits one shared key list into per-variant lists from counters the walk
     writes into pinned memory; with fixed-length keys the key list needs no length readback, so the call
