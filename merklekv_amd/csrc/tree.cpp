@@ -2675,15 +2675,18 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
             launch_diff_keys(refs, m, A, B, off, ob, t->st);
             l->n = m;
             const uint64_t kpos = (8 * (m + 1) + 15) & ~uint64_t(15);
-            l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
+            l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16, klen != 0);
             MKV_HIP(hipEventRecord(t->ev_a, t->st));
             MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_a, 0));
             const size_t ph = prof_begin(t, "d2h", t->st3);
             // DMA engine, not a copy kernel: beside the next update, a kernel's PCIe writes into pinned
-            // memory slowed the update's random-read locate 2x (configs[4] step 2.83 -> 2.37-2.43 ms)
-            MKV_HIP(hipMemcpyAsync(l->blk->p, off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st3));
+            // memory slowed the update's random-read locate 2x (configs[4] step 2.83 -> 2.37-2.43 ms).
+            // Fixed-length keys: only the key bytes cross PCIe, the host writes the offsets k x klen (once
+            // per pinned block: they stay there while it cycles through the pool; 7 MB of 35 at configs[4])
+            if (!klen) MKV_HIP(hipMemcpyAsync(l->blk->p, off, (m + 1) * 8, hipMemcpyDeviceToHost, t->st3));
             MKV_HIP(hipMemcpyAsync(l->blk->p + kpos, ob, bytes, hipMemcpyDeviceToHost, t->st3));
             prof_end(t, ph);
+            if (klen) l->blk->fill_offsets(klen, m + 1);
             auto ev = std::make_shared<KeyEvent>();
             MKV_HIP(hipEventRecord(ev->e, t->st3));
             l->ready = ev;

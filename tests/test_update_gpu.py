@@ -648,7 +648,8 @@ def test_fixed_length_offsets_written_by_host_across_pool_cycles():
     pinned staging block and keeps them while the block cycles through the pinned pool
     (tree.cpp PinnedBlock::fill_offsets; only the key bytes cross PCIe). Results of growing and shrinking
     size and of a second key length, some kept alive across calls so the blocks change hands, must all
-    carry exact offsets and keys (R7, merkle.rs:171-204: the changed keys, sorted)."""
+    carry exact offsets and keys (R7, merkle.rs:171-204: the changed keys, sorted); the same for the
+    batched 1-vs-k list (keylist_from_refs_async) and its per-variant views."""
     n = 60000
     kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
     keys = split_blob(kb, ko)
@@ -672,6 +673,23 @@ def test_fixed_length_offsets_written_by_host_across_pool_cycles():
             assert [raw[i * L:(i + 1) * L] for i in range(m)] == sorted(ks[i] for i in idx)
             held.append(d)
         held = held[-3:]
+        # the batched 1-vs-k walk's shared list (host-written offsets too), split per variant
+        for bt, ks in ((b1, keys), (b2, k2)):
+            vs, want = [], []
+            for v in range(3):
+                t = bt.clone()
+                idx = sorted(int(i) for i in rng.choice(n, m // (v + 1) + 1, replace=False))
+                t.upsert([ks[i] for i in idx], [b"b-%d-%d" % (rnd, v)] * len(idx))
+                vs.append(t)
+                want.append(sorted(ks[i] for i in idx))
+            L = len(ks[0])
+            for d, w in zip(bt.diff_keys_many_view(vs), want):
+                assert len(d) == len(w)
+                assert np.array_equal(d.offs, np.arange(len(w) + 1, dtype=np.uint64) * np.uint64(L))
+                raw = d.raw.tobytes()
+                assert [raw[i * L:(i + 1) * L] for i in range(len(w))] == w
+                held.append(d)
+            held = held[-4:]
 
 
 def test_batched_diff_per_variant_split_each_call():
