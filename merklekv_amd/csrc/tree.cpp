@@ -2203,18 +2203,21 @@ mkv_status mkv_tree_level(const mkv_tree *t, uint32_t level, uint64_t *count, ui
 }
 
 // Fill a key list from device offsets (m+1, starting at 0) and key bytes.
+// klen != 0 (every key klen bytes): the host writes the offsets k x klen (PinnedBlock::fill_offsets) and
+// only the key bytes are copied.
 static void keylist_fill(mkv_tree *t, mkv_keylist *l, const uint64_t *d_off, const uint8_t *d_bytes, uint64_t m,
-                         uint64_t bytes) {
+                         uint64_t bytes, uint64_t klen = 0) {
     l->n = m;
     if (!m) return;
     const uint64_t kpos = (8 * (m + 1) + 15) & ~uint64_t(15);  // key bytes 16-B aligned in the block
-    l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
+    l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16, klen != 0);
     uint64_t *ho = reinterpret_cast<uint64_t *>(l->blk->p);
     uint8_t *hb = l->blk->p + kpos;
     const size_t ph = prof_begin(t, "d2h", t->st);  // the PCIe part of a key list (profiling only)
-    copy_to_host(d_off, l->blk->dp, (m + 1) * 8, t->st);
+    if (!klen) copy_to_host(d_off, l->blk->dp, (m + 1) * 8, t->st);
     copy_to_host(d_bytes, l->blk->dp + kpos, bytes, t->st);
     prof_end(t, ph);
+    if (klen) l->blk->fill_offsets(klen, m + 1);
     l->offsets = ho;
     l->bytes = hb;
 }
@@ -2574,7 +2577,7 @@ static mkv_keylist *keylist_from_refs(mkv_tree *t, const uint64_t *refs, uint64_
             launch_fill_stride_u64(off, m, klen, t->st);
             launch_diff_keys(refs, m, A, B, off, ob, t->st);
             HTRACE("keys-queued");
-            keylist_fill(t, l, off, ob, m, m * klen);
+            keylist_fill(t, l, off, ob, m, m * klen, klen);
             HTRACE("copies-queued");
         } else if (m) {
             size_t pk = prof_begin(t, "diff");
