@@ -32,6 +32,10 @@ constexpr int WTILE = 64 * DI;  // merged outputs per wave tile
 // Sorted key i of a side: storage record perm[i].
 __device__ __forceinline__ const uint8_t *key_at(const DiffSide &S, uint64_t i, uint64_t *len) {
     const uint32_t o = S.perm[i];
+    if (S.klen) {  // fixed-length keys: the offset is arithmetic (koff[0] is one uniform read)
+        *len = S.klen;
+        return S.kb + S.koff[0] + (uint64_t)o * S.klen;
+    }
     const uint64_t a = S.koff[o];
     *len = S.koff[o + 1] - a;
     return S.kb + a;
@@ -52,7 +56,18 @@ __device__ __forceinline__ int cmp_ab(const DiffSide &A, uint64_t i, uint64_t pa
 __device__ __forceinline__ bool key_eq_at(const DiffSide &A, const DiffSide &B, uint64_t i) {
     const uint64_t pa = A.pfx[i], pb = B.pfx[i];
     const uint32_t oa = A.perm[i], ob = B.perm[i];
-    const uint64_t a0 = A.koff[oa], a1 = A.koff[oa + 1], b0 = B.koff[ob], b1 = B.koff[ob + 1];
+    uint64_t a0, a1, b0, b1;
+    if (A.klen && B.klen) {  // fixed-length keys: arithmetic offsets
+        a0 = A.koff[0] + (uint64_t)oa * A.klen;
+        a1 = a0 + A.klen;
+        b0 = B.koff[0] + (uint64_t)ob * B.klen;
+        b1 = b0 + B.klen;
+    } else {
+        a0 = A.koff[oa];
+        a1 = A.koff[oa + 1];
+        b0 = B.koff[ob];
+        b1 = B.koff[ob + 1];
+    }
     const uint64_t len = a1 - a0;
     if (pa != pb || len != b1 - b0) return false;
     if (len <= 8) return true;

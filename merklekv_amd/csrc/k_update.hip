@@ -30,6 +30,10 @@ namespace {
 
 __device__ __forceinline__ const uint8_t *tree_key(const DiffSide &T, uint64_t i, uint64_t *len) {
     const uint32_t o = T.perm[i];
+    if (T.klen) {  // fixed-length keys: arithmetic offsets (koff[0] is one uniform read)
+        *len = T.klen;
+        return T.kb + T.koff[0] + (uint64_t)o * T.klen;
+    }
     const uint64_t a = T.koff[o];
     *len = T.koff[o + 1] - a;
     return T.kb + a;
@@ -102,8 +106,13 @@ __device__ __forceinline__ void locate_k(const uint8_t *const kp[K], const uint6
     uint64_t ka[K], kl[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        ka[j] = hit[j] && !run[j] ? T.koff[o[j]] : 0;
-        kl[j] = hit[j] && !run[j] ? T.koff[o[j] + 1] - ka[j] : 0;
+        if (T.klen) {
+            ka[j] = T.koff[0] + (uint64_t)o[j] * T.klen;
+            kl[j] = T.klen;
+        } else {
+            ka[j] = hit[j] && !run[j] ? T.koff[o[j]] : 0;
+            kl[j] = hit[j] && !run[j] ? T.koff[o[j] + 1] - ka[j] : 0;
+        }
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -245,16 +254,14 @@ __device__ __forceinline__ void locate_hix(const uint8_t *const kp[K], const uin
                 live[j] = false;
                 continue;
             }
-            if ((e[j] >> 32) == tag[j]) {
-                const uint64_t p = e[j] & 0xFFFFFFFFull;
-                if (T.pfx[p] == c0[j]) {
-                    uint64_t tl;
-                    const uint8_t *tk = tree_key(T, p, &tl);
-                    if (key_cmp(kp[j], len[j], c0[j], tk, tl, c0[j]) == 0) {
-                        found[j] = p;
-                        live[j] = false;
-                        continue;
-                    }
+            if ((e[j] >> 32) == tag[j]) {  // a 32-bit tag match: confirm on the tree's key bytes (no
+                const uint64_t p = e[j] & 0xFFFFFFFFull;  // prefix pre-check: one dependent read fewer)
+                uint64_t tl;
+                const uint8_t *tk = tree_key(T, p, &tl);
+                if (tl == len[j] && key_cmp(kp[j], len[j], c0[j], tk, tl, key_chunk(tk, tl, 0)) == 0) {
+                    found[j] = p;
+                    live[j] = false;
+                    continue;
                 }
             }
             slot[j] = (slot[j] + 1) & mask;

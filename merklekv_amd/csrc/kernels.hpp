@@ -202,6 +202,9 @@ struct DiffSide {
     const uint64_t *pfx;
     const uint8_t *dig;
     uint64_t n;
+    // every key of the tree is klen bytes (tree klen_fixed): key s sits at kb + koff[0] + s * klen, one
+    // dependent random read (perm) instead of two (perm, koff); 0 = variable lengths
+    uint64_t klen;
 };
 constexpr int DIFF_ITEMS = 8;     // merged outputs per thread
 constexpr int DIFF_THREADS = 256;

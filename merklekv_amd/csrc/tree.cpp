@@ -1631,13 +1631,14 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     MKV_HIP(hipEventRecord(t->ev_join, t->st2));
     MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
     const DiffSide A = side_of(t);
-    DiffSide Bs;
+    DiffSide Bs{};
     Bs.kb = t->u_kb.as<uint8_t>();
     Bs.koff = t->u_koff.as<uint64_t>();
     Bs.perm = B.pm->as<uint32_t>();
     Bs.pfx = B.pk->as<uint64_t>();
     Bs.dig = bdig;
     Bs.n = B.n;
+    Bs.klen = B.klen;  // the batch's own key length when all its keys share one (its offsets are then arithmetic)
     const uint64_t M = A.n + Bs.n;
     if (t->nstore + nb >= 0xFFFFFFF0ull) throw Error(ST_EINVAL, "too many stored key records");
     uint64_t *npfx = ens<uint64_t>(t->m_pfx, M + 1);
@@ -2554,13 +2555,14 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
 }
 
 static DiffSide side_of(const mkv_tree *t) {
-    DiffSide s;
+    DiffSide s{};
     s.kb = t->kb.as<uint8_t>();
     s.koff = t->koff.as<uint64_t>();
     s.perm = t->perm.as<uint32_t>();
     s.pfx = t->pfx.as<uint64_t>();
     s.dig = t->nodes.as<uint8_t>();
     s.n = t->n;
+    s.klen = t->klen_fixed;
     return s;
 }
 
