@@ -328,6 +328,10 @@ struct mkv_tree {
     // batch merge (key-set changes): batch tombstones, merged prefixes / permutation / levels, count
     DevBuf u_tomb, m_pfx, m_perm, m_nodes, m_cnt;
     uint64_t bf_words = 0;  // words of u_bf known to be zero (every climb leaves them all-zero)
+    // words of u_cnt known to be zero: the end-of-update readback copies the counters to h_small + UCNT_HOST
+    // and zeroes them, so the next update needs no zeroing launch (one at the start of the update ran beside
+    // the previous step's key-list DMA, which stretched it from ~4 to 50-240 us)
+    uint64_t ucnt_zero_words = 0;
     uint64_t *h_small = nullptr;  // pinned host scalars (1 KB: bytes [512, 1024) = batched-walk counters)
     uint8_t *h_small_dev = nullptr;  // h_small as the device sees it (readbacks are kernel stores)
     uint32_t *h_counts = nullptr;  // pinned host copy of the prefix digit histograms (8 x 256)
@@ -418,11 +422,18 @@ struct SmallCopies {
     const uint8_t *src[32];
     uint8_t *dst[32];
     uint32_t bytes[32];
+    uint32_t zero;  // bit c: copy c also zeroes its source (a counter array read back and reset in one launch)
 };
 __global__ __launch_bounds__(64) void k_copy_small_many(SmallCopies C) {
     const uint32_t c = blockIdx.x;
-    for (uint32_t b = threadIdx.x; b < C.bytes[c]; b += 64) C.dst[c][b] = C.src[c][b];
+    const bool z = (C.zero >> c) & 1u;
+    for (uint32_t b = threadIdx.x; b < C.bytes[c]; b += 64) {
+        const uint8_t v = C.src[c][b];
+        C.dst[c][b] = v;
+        if (z) const_cast<uint8_t *>(C.src[c])[b] = 0;
+    }
 }
+constexpr size_t UCNT_HOST = 256;  // byte offset in h_small of the last update's counters (L + 2 words)
 
 // Zero-fill of up to 32 device ranges in one launch (grid.y = range): a multi-replica update clears
 // every replica's dirty bitmap and level counters with one launch instead of one memset call each
@@ -1823,9 +1834,14 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             B.base[q] = M;
             M += b.m;
             mmax = std::max(mmax, b.m);
+            const void *old_cnt = t->u_cnt.p;
             uint32_t *cnt = ens<uint32_t>(t->u_cnt, L + 2);  // cnt[l] < L: dirty nodes per level; cnt[L+1]: missing
-            Z.p[nz] = reinterpret_cast<uint8_t *>(cnt);
-            Z.bytes[nz++] = (L + 2) * 4;
+            if (cnt != old_cnt) t->ucnt_zero_words = 0;
+            if (t->ucnt_zero_words < L + 2) {  // first update (or the last one did not finish): zero them here
+                Z.p[nz] = reinterpret_cast<uint8_t *>(cnt);
+                Z.bytes[nz++] = (L + 2) * 4;
+            }
+            t->ucnt_zero_words = 0;  // until the end-of-update readback has reset them
             // replicas sharing t0's key-set id hold the same sorted keys, so their batches are located
             // in t0: one tree's prefix / permutation / key arrays serve all lookups (a 1/k working set
             // for the caches and the TLB instead of k copies of the same data)
@@ -1894,14 +1910,16 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         if (dense_top) run_reduce(t0, t0->nodes.as<uint8_t>(), nullptr, nullptr, (size_t)lstop, CA.ztab, k2);
         for (size_t q = 0; q < g.size(); ++q) ts[g[q]]->upd_dense_from = dense_top ? lstop : -1;
         prof_end(t0, pclimb);
-        // every tree's missing-key count and root, read back by one launch
+        // every tree's counters (dirty nodes per level, missing keys) and root, read back by one launch that
+        // also zeroes the counters for the next update (mkv_tree_update_counts reads the host copy)
         SmallCopies SC{};
         uint32_t nc = 0;
         for (size_t q = 0; q < g.size(); ++q) {
             mkv_tree *t = ts[g[q]];
-            SC.src[nc] = reinterpret_cast<const uint8_t *>(CA.missing[q]);
-            SC.dst[nc] = t->h_small_dev;
-            SC.bytes[nc++] = sizeof(uint32_t);
+            SC.src[nc] = reinterpret_cast<const uint8_t *>(CA.cnt[q]);
+            SC.dst[nc] = t->h_small_dev + UCNT_HOST;
+            SC.zero |= 1u << nc;
+            SC.bytes[nc++] = (uint32_t)((L + 2) * sizeof(uint32_t));
             if (!t->sharded) {
                 SC.src[nc] = t->nodes.as<uint8_t>() + 32 * t->lev_off[L - 1];
                 SC.dst[nc] = t->h_small_dev + 16 * sizeof(uint64_t);
@@ -1914,6 +1932,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
         }
         hipLaunchKernelGGL(k_copy_small_many, dim3(nc), dim3(64), 0, st, SC);
         MKV_LAUNCH_CHECK();
+        for (size_t q = 0; q < g.size(); ++q) ts[g[q]]->ucnt_zero_words = L + 2;
         HTRACE("climb-queued");
         for (size_t q = 0; q < g.size(); ++q) prof_end(ts[g[q]], prof[q]);
         for (size_t q = 0; q < g.size(); ++q) {
@@ -1923,7 +1942,7 @@ static void dirty_update_many(mkv_tree *const *ts, const DirtyBatch *bs, uint32_
             // later query of that stream ~15 µs), and their profiling pairs were recorded on st
             if (q == 0) sync(t);
             else prof_collect(t);
-            ok[g[q]] = reinterpret_cast<volatile uint32_t *>(t->h_small)[0] == 0;
+            ok[g[q]] = reinterpret_cast<volatile uint32_t *>(reinterpret_cast<uint8_t *>(t->h_small) + UCNT_HOST)[L + 1] == 0;
             if (ok[g[q]] && !t->sharded) std::memcpy(t->root, t->h_small + 16, 32);
             if (!ok[g[q]]) {  // tree untouched (the rehash above the climb rewrote the same digests)
                 t->upd_dense_from = -1;
@@ -3562,9 +3581,9 @@ mkv_status mkv_tree_update_counts(const mkv_tree *t, uint64_t *out, uint32_t cap
             return MKV_OK;
         }
         DevGuard g(t->dev);
-        std::vector<uint32_t> h(L);
         MKV_HIP(hipStreamSynchronize(t->st));
-        MKV_HIP(hipMemcpy(h.data(), t->u_cnt.p, 4ull * L, hipMemcpyDeviceToHost));
+        // the last update's counters, copied to the host (and reset on the device) when it ended
+        const uint32_t *h = reinterpret_cast<const uint32_t *>(reinterpret_cast<const uint8_t *>(t->h_small) + UCNT_HOST);
         for (uint32_t l = 0; l < L && l < cap; ++l)  // levels above the climb: rehashed whole
             out[l] = (t->upd_dense_from >= 0 && (int)l > t->upd_dense_from) ? t->lev_cnt[l] : h[l];
     });
