@@ -854,7 +854,8 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_batch(const uint8_t
                                                            uint64_t desc_off, uint64_t desc_count, int k,
                                                            const uint64_t *__restrict__ fin,
                                                            const uint32_t *__restrict__ nin,
-                                                           uint64_t *__restrict__ fout, uint32_t *__restrict__ nout) {
+                                                           uint64_t *__restrict__ fout, uint32_t *__restrict__ nout,
+                                                           uint32_t *__restrict__ bm, uint64_t bn) {
     __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
     const uint64_t tot = (uint64_t)cnt << k;
@@ -870,6 +871,10 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_batch(const uint8_t
             c = ((e & 0xFFFFFFFFull) << k) | (t & mask);
         }
         if (c < desc_count) d = !digest_eq(ca + 32ull * c, V.nodes[v] + desc_off + 32ull * c);
+        if (bm && d) {  // landing on the leaves: the (variant, position) bit of k_vpos_* directly
+            const uint64_t g = (uint64_t)v * bn + c;
+            atomicOr(bm + (g >> 5), 1u << (g & 31));
+        }
         block_append<uint64_t>(d, ((uint64_t)v << 32) | c, fout, nout, sapp);
     }
 }
@@ -1173,10 +1178,10 @@ void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const 
 uint64_t vpos_scratch_words(uint64_t bits) { return 2 * (ceil_div((bits + 31) / 32, VP_WORDS) + 2); }
 
 void launch_vpos_sorted_dev(const uint64_t *f, const uint32_t *mdev, uint64_t cap, uint64_t n, uint32_t k, int pb,
-                            uint32_t *bm, uint32_t *bc, void *scan_scr, uint64_t *out, hipStream_t st) {
+                            uint32_t *bm, uint32_t *bc, void *scan_scr, uint64_t *out, hipStream_t st, bool bits_set) {
     const uint64_t words = ((uint64_t)k * n + 31) / 32, nb = ceil_div(words, VP_WORDS);
     uint32_t *boff = bc + nb + 1;
-    hipLaunchKernelGGL(k_vpos_setbits, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap ? cap : 1, 256), 2048)), dim3(256),
+    if (!bits_set) hipLaunchKernelGGL(k_vpos_setbits, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap ? cap : 1, 256), 2048)), dim3(256),
                        0, st, f, mdev, n, bm);
     hipLaunchKernelGGL(k_vpos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
     exclusive_scan_u32(bc, boff, nb, boff + nb, scan_scr, st);
@@ -1216,10 +1221,10 @@ void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_
 }
 void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
-                               uint64_t max_desc, hipStream_t st) {
+                               uint64_t max_desc, hipStream_t st, uint32_t *bm, uint64_t bn) {
     const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
     hipLaunchKernelGGL(k_topdown_jump_batch, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, V, desc_off, desc_count, k,
-                       fin, nin, fout, nout);
+                       fin, nin, fout, nout, bm, bn);
     MKV_LAUNCH_CHECK();
 }
 

@@ -276,7 +276,8 @@ void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_
                             uint32_t *nout, uint64_t max_desc, hipStream_t st);
 void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
-                               uint64_t max_desc, hipStream_t st);
+                               uint64_t max_desc, hipStream_t st, uint32_t *bm = nullptr,
+                               uint64_t bn = 0);
 // ent: sorted (variant << pb) | position.
 // check: bit v set = variant v's keys at its divergent positions are compared with the base's.
 void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs, uint64_t check,
@@ -287,7 +288,7 @@ void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const 
 // (vpos_scratch_words(k x n) words).
 uint64_t vpos_scratch_words(uint64_t bits);
 void launch_vpos_sorted_dev(const uint64_t *f, const uint32_t *mdev, uint64_t cap, uint64_t n, uint32_t k, int pb,
-                            uint32_t *bm, uint32_t *bc, void *scan_scr, uint64_t *out, hipStream_t st);
+                            uint32_t *bm, uint32_t *bc, void *scan_scr, uint64_t *out, hipStream_t st, bool bits_set = false);
 // key[k] = (variant << pb) | position of frontier entry (variant << 32) | position; val[k] = k.
 void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key, uint32_t *val, hipStream_t st);
 // Anti-entropy exchange: digests of level nodes by index (absent -> zeros); flags of indices whose local

@@ -2814,6 +2814,17 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     t->walk_jumps.clear();
     t->walk_L = (uint32_t)L;
     t->walk_k = k;
+    // the (variant, position) bitmap that orders the level-0 entries (all-zero between calls; zeroed here
+    // when grown): the jump that lands on the leaves sets its bits itself
+    const uint64_t bits = (uint64_t)k * n, words = (bits + 31) / 32;
+    const bool bitmap = bits <= VPOS_MAX_BITS;
+    uint32_t *bm = nullptr;
+    bool bits_set = false;
+    if (bitmap) {
+        bm = ens<uint32_t>(t->tb_bm, words + 4);
+        if (t->tb_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
+        t->tb_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
+    }
     const size_t pwalk = prof_begin(t, "walk");
     if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
         launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
@@ -2824,8 +2835,11 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
             const size_t l = T[q - 1], lt = T[q];
             const int kk = (int)(l - lt);
             t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
+            const bool land = bitmap && lt == 0;
             launch_topdown_jump_batch(na + 32 * a->lev_off[lt], V, 32 * a->lev_off[lt], a->lev_cnt[lt], kk, fin, cnt + l,
-                                      fout, cnt + lt, std::min<uint64_t>(k * (a->lev_cnt[l] << kk), 1ull << 40), t->st);
+                                      fout, cnt + lt, std::min<uint64_t>(k * (a->lev_cnt[l] << kk), 1ull << 40), t->st,
+                                      land ? bm : nullptr, n);
+            bits_set |= land;
             std::swap(fin, fout);
             // the level-4 abort test on the device (k_td_gate: frontier over half the level -> emptied,
             // bit 31 in cnt[L + 1]), read back with the leaf count: no host round trip inside the walk
@@ -2864,21 +2878,15 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     uint64_t check = 0;  // variants whose key set may differ from the base's
     for (uint32_t i = 0; i < k; ++i)
         if (!same_keyset(vs[i], a)) check |= 1ull << i;
-    const uint64_t bits = (uint64_t)k * n;
     uint64_t m = 0;
     uint64_t *refs = nullptr;
-    const bool bitmap = bits <= VPOS_MAX_BITS;
     if (bitmap) {
         // the level-0 entries ordered on the device from the device count (k_vpos_*), the leaf checks
         // from the same count: one host wait for the count, the abort flag and the per-variant words
-        const uint64_t words = (bits + 31) / 32;
-        uint32_t *bm = ens<uint32_t>(t->tb_bm, words + 4);
-        if (t->tb_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
-        t->tb_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
         const uint64_t sw = vpos_scratch_words(bits);
         uint32_t *bc = ens<uint32_t>(t->tb_bc, sw);
         void *scr = t->d_diffscr.ensure(scan_scratch_bytes(sw));
-        launch_vpos_sorted_dev(fin, cnt, cap, n, k, pb, bm, bc, scr, fout, t->st);
+        launch_vpos_sorted_dev(fin, cnt, cap, n, k, pb, bm, bc, scr, fout, t->st, bits_set);
         t->tb_bm_words = words;
         MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
         MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
