@@ -110,6 +110,44 @@ def test_upsert_device_dirty_and_fallback():
     assert _levels(t) == _oracle_levels(o)
 
 
+@pytest.mark.parametrize("base_off", [1000, 4, 3])
+def test_fixed_length_keys_at_offset_base(base_off):
+    """Trees whose keys all have one length address them arithmetically (kb + koff[0] + s x len,
+    DiffSide::klen). Device inputs whose offsets start at base_off (a slice of a larger buffer; 3 leaves
+    the key bytes unaligned) over 2^20 + 100 keys (so the update locates through the hash index): root,
+    value-only update (locate + dirty climb), merge of a new key, diffs — all vs the oracle
+    (merkle.rs:52-56, :73-121, :171-204)."""
+    import torch
+    n = (1 << 20) + 100
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    dk = torch.zeros(base_off + len(kb) + 16, dtype=torch.uint8)
+    dk[base_off:base_off + len(kb)] = torch.from_numpy(kb)
+    dk = dk.cuda()
+    dko = torch.from_numpy(ko.astype(np.int64) + base_off).cuda()
+    dv = torch.from_numpy(vb.copy()).cuda()
+    dvo = torch.from_numpy(vo.astype(np.int64)).cuda()
+    torch.cuda.synchronize()
+    t = MerkleTree()
+    t.build_device(dk.data_ptr(), dko.data_ptr(), dv.data_ptr(), dvo.data_ptr(), n)
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    assert t.get_root_hash() == o.root()
+    base, ob = t.clone(), o
+    rng = np.random.default_rng(base_off)
+    idx = sorted(int(i) for i in rng.choice(n, 5000, replace=False))
+    uk, uv = [keys[i] for i in idx], [b"u-%d" % i for i in idx]
+    t.upsert(uk, uv)  # value-only: hash-index locate + dirty climb
+    o = o.upsert(*pack(uk), *pack(uv))
+    assert t.get_root_hash() == o.root()
+    assert base.diff_keys_bytes(t) == ob.diff(o) == sorted(uk)
+    assert t.diff_keys_bytes(base) == o.diff(ob)
+    nk = keys[7][:-1] + b"#"  # one new key of the same length: merge path, the tree stays fixed-length
+    t.upsert([nk], [b"new"])
+    o = o.upsert(*pack([nk]), *pack([b"new"]))
+    assert t.get_root_hash() == o.root()
+    assert base.diff_keys_bytes(t) == ob.diff(o)
+
+
 @pytest.mark.parametrize("n,m", [(20000, 300), (70001, 9000)])
 def test_upsert_device_many_matches_separate_calls(n, m):
     """Batched dirty climb of several replicas (shared level plan) + a replica of another size (own
