@@ -855,9 +855,15 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_batch(const uint8_t
                                                            const uint64_t *__restrict__ fin,
                                                            const uint32_t *__restrict__ nin,
                                                            uint64_t *__restrict__ fout, uint32_t *__restrict__ nout,
-                                                           uint32_t *__restrict__ bm, uint64_t bn) {
+                                                           uint32_t *__restrict__ bm, uint64_t bn,
+                                                           uint32_t *__restrict__ gate, uint32_t word,
+                                                           uint64_t level_count) {
     __shared__ uint32_t sapp[17];
     const uint32_t cnt = *nin;
+    if (gate && (gate[word] != 0 || 2ull * cnt > level_count)) {  // the level-4 abort test (k_topdown_jump)
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(gate + word, 0x80000000u);
+        return;
+    }
     const uint64_t tot = (uint64_t)cnt << k;
     const uint64_t mask = (1ull << k) - 1ull;
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < tot; base += (uint64_t)gridDim.x * blockDim.x) {
@@ -1221,10 +1227,11 @@ void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_
 }
 void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
-                               uint64_t max_desc, hipStream_t st, uint32_t *bm, uint64_t bn) {
+                               uint64_t max_desc, hipStream_t st, uint32_t *bm, uint64_t bn, uint32_t *gate,
+                               uint32_t word, uint64_t level_count) {
     const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, TD_THREADS), 2048);
     hipLaunchKernelGGL(k_topdown_jump_batch, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, V, desc_off, desc_count, k,
-                       fin, nin, fout, nout, bm, bn);
+                       fin, nin, fout, nout, bm, bn, gate, word, level_count);
     MKV_LAUNCH_CHECK();
 }
 

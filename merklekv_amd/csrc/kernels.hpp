@@ -277,7 +277,7 @@ void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_
 void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t desc_off, uint64_t desc_count, int k,
                                const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
                                uint64_t max_desc, hipStream_t st, uint32_t *bm = nullptr,
-                               uint64_t bn = 0);
+                               uint64_t bn = 0, uint32_t *gate = nullptr, uint32_t word = 0, uint64_t level_count = 0);
 // ent: sorted (variant << pb) | position.
 // check: bit v set = variant v's keys at its divergent positions are compared with the base's.
 void launch_topdown_leaves_batch(const uint64_t *ent, uint64_t m, int pb, const DiffSide &A, const DiffSide *Bs, uint64_t check,

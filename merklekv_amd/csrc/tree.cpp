@@ -2836,15 +2836,14 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
             const int kk = (int)(l - lt);
             t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
             const bool land = bitmap && lt == 0;
+            // the level-4 abort test rides on the jump from level 4 (frontier over half the level: nothing
+            // compared, bit 31 in cnt[L + 1]), read back with the leaf count: no host round trip in the walk
+            const bool gate = l == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2;
             launch_topdown_jump_batch(na + 32 * a->lev_off[lt], V, 32 * a->lev_off[lt], a->lev_cnt[lt], kk, fin, cnt + l,
                                       fout, cnt + lt, std::min<uint64_t>(k * (a->lev_cnt[l] << kk), 1ull << 40), t->st,
-                                      land ? bm : nullptr, n);
+                                      land ? bm : nullptr, n, gate ? cnt : nullptr, (uint32_t)L + 1, k * a->lev_cnt[l]);
             bits_set |= land;
             std::swap(fin, fout);
-            // the level-4 abort test on the device (k_td_gate: frontier over half the level -> emptied,
-            // bit 31 in cnt[L + 1]), read back with the leaf count: no host round trip inside the walk
-            if (lt == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2)
-                launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)lt, k * a->lev_cnt[lt], t->st);
         }
     } else
     for (size_t l = L; l >= 1; --l) {
