@@ -284,7 +284,7 @@ mkv_status mkv_prof_read(const mkv_tree *t, const char *group, double *total_ms,
  * kb >= n*klen, vb >= n*vlen, koff/voff n+1 entries. Synchronous. */
 /* Introspection (benches / tests): per-level dirty entry counts of the tree's last dirty-path update
  * (level 0 = changed leaves, level l > 0 = rehashed nodes), and the last top-down walk this tree ran as
- * the base (a batched walk of mkv_tree_diff_many or an unsharded pair walk of mkv_tree_diff):
+ * the base (a batched walk of mkv_tree_diff_many or a pair walk of mkv_tree_diff, sharded or not):
  * out[0] = frontier entries expanded, out[1] = digest bytes the walk compared, out[2] = divergent leaf
  * positions, out[3] = launches. Both synchronise the tree's stream. */
 mkv_status mkv_tree_update_counts(const mkv_tree *t, uint64_t *out, uint32_t cap, uint32_t *nlevels);
