@@ -189,7 +189,11 @@ mkv_status mkv_shard_combine_device(mkv_tree *t, const uint8_t *dfringes, uint32
  * Failure: every operation's first collective carries each rank's status word, and so does every later
  * collective of it, so when one rank's local step fails (bad blob, out of memory) EVERY rank returns an
  * error from the same call (the failing rank its own, the others that rank's code) — no rank is left
- * waiting in a collective. (A rank that never calls the operation at all still blocks the others.)
+ * waiting in a collective. Staging buffers that must grow are allocated before a 32-B status round on
+ * buffers reserved at creation, so an allocation failure after the meta all-gather reaches every rank too.
+ * Every wait on a collective is bounded (MKV_WAIT_TIMEOUT_S, default 120 s): a rank whose peers never join
+ * (a rank that never calls the operation, a dead link) aborts the RCCL communicator (ncclCommAbort) and
+ * returns MKV_EHIP; later calls on that communicator return MKV_ESTATE.
  *   host: mkv_comm_create_host with the caller's all-gather (gloo, MPI, a test harness): fn gathers
  *     `bytes` from every rank into recv in rank order (host memory) and returns 0.
  * Replaces: the host-side count / fringe / key-list exchanges a caller had to write around
@@ -201,6 +205,11 @@ mkv_status mkv_comm_unique_id(uint8_t id[MKV_COMM_ID_BYTES]);
 mkv_status mkv_comm_init_rank(const uint8_t id[MKV_COMM_ID_BYTES], int rank, int world, int hip_device, mkv_comm **out);
 mkv_status mkv_comm_create_host(int rank, int world, mkv_allgather_fn fn, void *ctx, mkv_comm **out);
 mkv_status mkv_comm_rank(const mkv_comm *c, int *rank, int *world);
+/* Test hook (no reference counterpart): the next local step of this rank between an operation's meta
+ * all-gather and its block all-gather fails with MKV_ENOMEM, as a failed staging allocation would; every
+ * rank must then return an error from that call. where = 0 clears it. */
+#define MKV_FAULT_AFTER_META 1
+mkv_status mkv_comm_inject_fault(mkv_comm *c, int where);
 /* All-gather of `bytes` host bytes per rank through the communicator (recv: world x bytes, rank order);
  * what the sharded entry points use for their metadata. Collective; needs no GPU in the host form. */
 mkv_status mkv_comm_all_gather(mkv_comm *c, const void *send, void *recv, uint64_t bytes);
@@ -209,7 +218,7 @@ mkv_status mkv_comm_all_gather(mkv_comm *c, const void *send, void *recv, uint64
 #define MKV_COLL_COUNTS 0 /* leaf counts (8 B) */
 #define MKV_COLL_RANGE 1  /* range check: first / last key per shard */
 #define MKV_COLL_FRINGE 2 /* seam fringes (k x MKV_FRINGE_BYTES) */
-#define MKV_COLL_DIFF 3   /* divergent keys: (count, bytes) meta + padded blocks, or the local slice's counts */
+#define MKV_COLL_DIFF 3   /* divergent keys: (count, bytes) meta + per-rank blocks, or the local slice's counts */
 #define MKV_COLL_USER 4   /* mkv_comm_all_gather: the caller's own bytes */
 #define MKV_COLL_KINDS 5
 mkv_status mkv_comm_stats(mkv_comm *c, double secs[MKV_COLL_KINDS], uint64_t calls[MKV_COLL_KINDS],
@@ -236,7 +245,9 @@ mkv_status mkv_sharded_root(mkv_tree *t, mkv_comm *c, uint8_t out32[32], int *ha
 mkv_status mkv_sharded_root_many(mkv_tree *const *ts, uint32_t k, mkv_comm *c, uint8_t *roots, int *has_root);
 /* diff_keys (merkle.rs:171-196) of two sharded trees over the same partition, as ONE sorted list on every
  * rank — what SyncManager::sync_once consumes (sync.rs:67): local device diff, all-gather of (count,
- * bytes), all-gather of [u32 lengths | key bytes] blocks. Rank order is key order. */
+ * bytes), then the lists themselves: RCCL form an all-gather-v (grouped send / receive) of device blocks
+ * sized by each rank's own list, host form one all-gather of blocks padded to the largest rank's. Rank
+ * order is key order. */
 mkv_status mkv_sharded_diff(const mkv_tree *a, const mkv_tree *b, mkv_comm *c, mkv_keylist **out);
 /* This rank's slice of that global list: the sorted divergent keys of its own key range (one device ->
  * host copy) and their position in the global list — the sum of the lower ranks' counts, from ONE 32-B

@@ -34,7 +34,7 @@ EXPORTS = [
     "mkv_route_sample", "mkv_route_splitters", "mkv_route_plan", "mkv_route_pack", "mkv_route_offsets",
     "mkv_comm_unique_id", "mkv_comm_init_rank", "mkv_comm_create_host", "mkv_comm_rank", "mkv_comm_destroy",
     "mkv_comm_stats", "mkv_comm_all_gather", "mkv_sharded_build", "mkv_sharded_root", "mkv_sharded_root_many", "mkv_sharded_diff",
-    "mkv_sharded_diff_local", "mkv_comm_traffic",
+    "mkv_sharded_diff_local", "mkv_comm_traffic", "mkv_comm_inject_fault",
 ]
 
 COMM_ID_BYTES = 128
@@ -132,6 +132,7 @@ def lib():
         "mkv_sharded_diff": ([vp, vp, vp, P(vp)], i32),
         "mkv_sharded_diff_local": ([vp, vp, vp, P(vp), P(u64), P(u64)], i32),
         "mkv_comm_traffic": ([vp, vp, vp], i32),
+        "mkv_comm_inject_fault": ([vp, i32], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

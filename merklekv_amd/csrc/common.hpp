@@ -89,6 +89,9 @@ struct DevKeys {
 DevKeys tree_diff_device(const mkv_tree *a, const mkv_tree *b);
 DevKeys tree_keys_at_device(const mkv_tree *t, const uint64_t *pos, uint64_t m);
 hipStream_t tree_stream(const mkv_tree *t);
+// The library's bounded wait for a stream (poll, then yield, then sleep; MKV_EHIP after
+// MKV_WAIT_TIMEOUT_S instead of blocking forever).
+void wait_bounded(hipStream_t s);
 int tree_device(const mkv_tree *t);
 uint64_t tree_len(const mkv_tree *t);
 mkv_keylist *keylist_from_device(const uint64_t *d_off, const uint8_t *d_kb, uint64_t n, uint64_t bytes, hipStream_t st);

@@ -52,6 +52,7 @@ constexpr uint32_t RG_INV = 0xFFFFFFFFu;
 #endif
 
 typedef uint32_t rg4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t rg3 __attribute__((ext_vector_type(3), aligned(4)));
 
 // 17 dwords at base + a (base and a 4-B aligned; gfx950 serves 16-B loads at 4-B alignment). Addresses
 // stay pointer arithmetic on the kernel's blob arguments so the loads are global_load, not flat_load
@@ -87,10 +88,11 @@ struct RgRec {
 
 // kmis / vmis: byte misalignment of the key / value blob pointers (the bases are the blobs rounded down to
 // a dword); klo .. vhi: the blobs' dword ranges as offsets from those bases.
-__device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint64_t k1, uint64_t v0, uint64_t v1, uint32_t r,
+// k1, v1: the low words of the record's end offsets (a record is shorter than 4 GiB).
+__device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint32_t k1, uint64_t v0, uint32_t v1, uint32_t r,
                                         uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi, int64_t vlo,
                                         int64_t vhi) {
-    const uint32_t k = (uint32_t)(k1 - k0), v = (uint32_t)(v1 - v0);
+    const uint32_t k = k1 - (uint32_t)k0, v = v1 - (uint32_t)v0;
     const uint32_t c4 = k & 3;
     R.k = k;
     R.L = 8 + k + v;
@@ -120,7 +122,7 @@ __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint64_t k1, uint
 // A record whose source dwords would reach outside the blobs (within ~128 B of a blob's ends; every record
 // of a blob of empty or tiny keys) goes to k_leaf_edges instead: no bounds checks in this kernel's loads
 // (the checked form cost ~70 VGPRs).
-__device__ __forceinline__ void rg_take_or_leave(RgRec &R, uint64_t k0, uint64_t k1, uint64_t v0, uint64_t v1,
+__device__ __forceinline__ void rg_take_or_leave(RgRec &R, uint64_t k0, uint32_t k1, uint64_t v0, uint32_t v1,
                                                  uint32_t r, uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi,
                                                  int64_t vlo, int64_t vhi, uint32_t *ctr) {
 
@@ -234,7 +236,8 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     Q.qpos = 0;
 
     // next record of this lane (offsets in flight one step ahead)
-    uint64_t nk0 = 0, nk1 = 0, nv0 = 0, nv1 = 0;
+    uint64_t nk0 = 0, nv0 = 0;
+    uint32_t nk1 = 0, nv1 = 0;  // low words of koff[rec + 1] / voff[rec + 1]
     uint32_t nrec = 0;
     bool nok = false;
     auto refill = [&](bool need) {
@@ -248,17 +251,16 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
             nok = ch != RG_INV && rec < n;
             if (nok) {
                 nrec = (uint32_t)rec;
-                const rg4 *kq = reinterpret_cast<const rg4 *>(koff + rec);  // koff[rec], koff[rec + 1]
-                const rg4 *vq = reinterpret_cast<const rg4 *>(voff + rec);
-                const rg4 a = *kq, b = *vq;
+                // koff[rec] and the low word of koff[rec + 1] (lengths are < 4 GiB): 12-B loads, so no
+                // loaded dword is dead — a dead destination register gets reused as a temporary, and the
+                // write-after-write wait on it would stall the step on these loads
+                const rg3 *kq = reinterpret_cast<const rg3 *>(koff + rec);
+                const rg3 *vq = reinterpret_cast<const rg3 *>(voff + rec);
+                const rg3 a = *kq, b = *vq;
                 nk0 = ((uint64_t)a.y << 32) | a.x;
-                nk1 = ((uint64_t)a.w << 32) | a.z;
+                nk1 = a.z;
                 nv0 = ((uint64_t)b.y << 32) | b.x;
-                nv1 = ((uint64_t)b.w << 32) | b.z;
-                if (KO.odst) {  // key ownership: every record of a ragged chunk passes here (leaf.hpp)
-                    KO.odst[rec] = nk0;
-                    if (rec + 1 == n) KO.odst[n] = nk1;
-                }
+                nv1 = b.z;
             }
         }
         if (Q.qc != RG_INV) {
@@ -276,8 +278,18 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     R.k = R.L = R.b1 = R.b3 = R.nb = R.blk = R.r = 0;
     R.ka = R.va = 0;
     R.ksel = R.vsel = R.hc = R.vhl = R.vtl = R.he = R.term = 0;
+    // key ownership: every record of a ragged chunk is taken exactly once (leaf.hpp); its offsets are
+    // stored then, from registers that were loaded a step earlier (a store in the refill itself would wait
+    // for the offsets it just requested)
+    auto take = [&]() {
+        rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, ctr);
+        if (KO.odst) {
+            KO.odst[nrec] = nk0;
+            if ((uint64_t)nrec + 1 == n) KO.odst[n] = koff[n];
+        }
+    };
     refill(true);
-    if (nok) rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, ctr);
+    if (nok) take();
     nok = false;
     refill(true);
 
@@ -289,6 +301,10 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     sha_init(st);
 
     while (__any(R.live || nok)) {
+        // Every load of the previous step (source dwords, next offsets) lands here, on every path: the
+        // compiler's own waits sit inside the lane-conditional assembly branches, so on a path that skipped
+        // them it waited again in the middle of the step, in front of the new loads.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
         // ---- assemble this step's block in the lane's LDS slot ----
         uint32_t w[16];
         {
@@ -340,12 +356,14 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
         if (R.live && !fin) {
             ++R.blk;
         } else {
-            if (nok) rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, ctr);
+            if (nok) take();
             else R.live = false;
             nok = false;
         }
+        // both in flight during the rounds: the block's source dwords first, then the next record's offsets
+        // (fetching after the refill made every step wait for the offsets before its source loads issued)
+        rg_fetch(R, kbase, vbase, dk, dv);
         refill(!nok);
-        rg_fetch(R, kbase, vbase, dk, dv);  // in flight during the rounds
         // ---- compress ----
         sha_compress<SHORT>(st, w);
         if (fin) store_digest(out + 32 * (uint64_t)rfin, st);

@@ -3713,6 +3713,7 @@ DevKeys tree_keys_at_device(const mkv_tree *tc, const uint64_t *pos, uint64_t m)
     return d;
 }
 hipStream_t tree_stream(const mkv_tree *t) { return t->st; }
+void wait_bounded(hipStream_t s) { wait_idle(s); }
 int tree_device(const mkv_tree *t) { return t->dev; }
 uint64_t tree_len(const mkv_tree *t) { return t->n; }
 // One copy of a device key list (offsets[0..n], offsets[0] == 0, then the bytes) into a pinned block on
@@ -3725,7 +3726,7 @@ mkv_keylist *keylist_from_device(const uint64_t *d_off, const uint8_t *d_kb, uin
         l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16);
         MKV_HIP(hipMemcpyAsync(l->blk->p, d_off, (n + 1) * 8, hipMemcpyDeviceToHost, st));
         if (bytes) MKV_HIP(hipMemcpyAsync(l->blk->p + kpos, d_kb, bytes, hipMemcpyDeviceToHost, st));
-        MKV_HIP(hipStreamSynchronize(st));
+        wait_idle(st);
         l->offsets = reinterpret_cast<const uint64_t *>(l->blk->p);
         l->bytes = l->blk->p + kpos;
         l->n = n;

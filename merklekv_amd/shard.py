@@ -197,6 +197,90 @@ def sequential_root(tree, shard_blobs, global_n: int):
     return tree.shard_combine(b"".join(fringes), len(fringes), global_n), counts
 
 
+def sequential_diff(ta, tb, shard_pairs, global_na: int, global_nb: int):
+    """diff_keys of two key-range-sharded replicas (configs[2] x configs[3]: two 1B-key trees) on ONE GPU,
+    shard after shard — what 8 ranks do in parallel, each with its own range (sync.rs:67-83 consumes the
+    global list). Per shard g in key order: shard_prepare + shard_reduce of both replicas at their global
+    offsets (A: o_g inside a tree of global_na leaves, B likewise; offsets are the leaf counts of the
+    shards before g), both fringes kept, then the shard-local diff_keys (merkle.rs:171-196): the top-down
+    walk from the fringe roots when the two shard plans match, the merge-join otherwise. Ranges are
+    ordered, so the per-shard lists concatenate into the global sorted list at the offsets given by their
+    counts. shard_pairs yields ((kb, koff, vb, voff, n) of A, same of B) device blobs, possibly generated
+    lazily into reused buffers (the trees own copies of their keys).
+    Returns (root_a, root_b, [(raw, offs) per shard], [global offset per shard], [diff ms per shard])."""
+    import time
+    fa, fb, lists, offs, ms = [], [], [], [], []
+    oa = ob = at = 0
+    for blob_a, blob_b in shard_pairs:
+        na = ta.shard_prepare(blob_a, None, on_device=True)
+        ta.shard_reduce(oa, global_na)
+        fa.append(ta.shard_fringe())
+        nb = tb.shard_prepare(blob_b, None, on_device=True)
+        tb.shard_reduce(ob, global_nb)
+        fb.append(tb.shard_fringe())
+        t0 = time.perf_counter()
+        raw, o = ta.diff_keys_packed(tb)
+        ms.append((time.perf_counter() - t0) * 1e3)
+        lists.append((raw, o))
+        offs.append(at)
+        at += len(o) - 1
+        oa += na
+        ob += nb
+    if oa != global_na or ob != global_nb:
+        raise ValueError(f"shards hold {oa} / {ob} leaves, not {global_na} / {global_nb}")
+    ra = ta.shard_combine(b"".join(fa), len(fa), global_na)
+    rb = tb.shard_combine(b"".join(fb), len(fb), global_nb)
+    return ra, rb, lists, offs, ms
+
+
+def sequential_incremental(shards, global_n: int, replicas: int, warmup: bool = True, device: int = 0):
+    """configs[4] at its full size on ONE GPU: a 1B-key tree as key-range shards, base + (replicas - 1)
+    variants, each variant applying its own value batch in every shard (1M keys per variant over 8 shards
+    of 125K), shard after shard — the 8-rank form runs the shards in parallel. Per shard g: the base shard
+    built at its global offset (shard_prepare + shard_reduce), cloned per variant; a STEP = every variant's
+    batch through one upsert_device_many (dirty path: merkle.rs:52-56 then the climb) + the base diffed
+    against all variants in one shared walk (diff_keys_many, merkle.rs:171-196); the first step is a warm-up
+    when `warmup` (the same batches applied again leave the trees and the diffs unchanged); then every
+    replica's fringe is kept. After the last shard, each replica's global root is the seam combine of its
+    fringes (the recombine the ranks do over RCCL). shards yields ((kb, koff, vb, voff, n) base blob,
+    [(kb, koff, vb, voff, m) batch per variant]) device tensors.
+    Returns (roots [base, variants...], per-variant [(raw, offs) per shard], [step ms per shard])."""
+    import time
+
+    from .merkle import MerkleTree
+    fr = [[] for _ in range(replicas)]
+    lists = [[] for _ in range(replicas - 1)]
+    ms = []
+    off = 0
+    for blob, batches in shards:
+        base = MerkleTree(device)
+        n_g = base.shard_prepare(blob, None, on_device=True)
+        base.shard_reduce(off, global_n)
+        variants = [base.clone() for _ in range(replicas - 1)]
+        ptrs = [tuple(x.data_ptr() if hasattr(x, "data_ptr") else x for x in b) for b in batches]
+
+        def step():
+            MerkleTree.upsert_device_many(variants, ptrs)
+            return base.diff_keys_many_packed(variants)
+
+        if warmup:
+            step()
+        t0 = time.perf_counter()
+        diffs = step()
+        ms.append((time.perf_counter() - t0) * 1e3)
+        for i, d in enumerate(diffs):
+            lists[i].append(d)
+        for i, t in enumerate([base] + variants):
+            fr[i].append(t.shard_fringe())
+        off += n_g
+        del base, variants
+    if off != global_n:
+        raise ValueError(f"shards hold {off} leaves, not global_n = {global_n}")
+    holder = MerkleTree(device)
+    roots = [holder.shard_combine(b"".join(f), len(f), global_n) for f in fr]
+    return roots, lists, ms
+
+
 def shard_recombine_many(trees, dist, total: int, device="cpu", group=None) -> list:
     """Fringe all-gather + seam combine for k trees (replicas of one key range) in ONE collective:
     after in-place updates (MerkleTree.upsert / upsert_device of keys in the rank's range: the dirty

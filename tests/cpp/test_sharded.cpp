@@ -8,10 +8,13 @@
 //      rank's global root equals the unsharded root, the gathered divergent-key list is the whole sorted
 //      diff on every rank, the local slices sit at their global offsets, in-range updates +
 //      mkv_sharded_root_many track the new root, overlapping ranges are rejected (MKV_EINVAL) on every
-//      rank, and an invalid blob on ONE rank makes every rank's call fail (status words) without a hang.
+//      rank, an invalid blob on ONE rank makes every rank's call fail (status words) without a hang, and so
+//      does a failure injected on one rank AFTER the meta all-gather (mkv_comm_inject_fault: block header
+//      and status-round paths).
 // Built by __graft_entry__.build_cpp_tests(); run by tests/test_cpp_ports_gpu.py.
 #include <openssl/evp.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -137,6 +140,10 @@ static void test_rccl_world1(int dev) {
     mkv_comm *c = nullptr;
     OK(mkv_comm_init_rank(id, 0, 1, dev, &c));
     if (!c) return;
+    auto step = [](const char *what) {
+        std::printf("  rccl world 1: %s\n", what);
+        std::fflush(stdout);
+    };
     int rank = -1, world = -1;
     OK(mkv_comm_rank(c, &rank, &world));
     CHECK(rank == 0 && world == 1);
@@ -151,6 +158,7 @@ static void test_rccl_world1(int dev) {
     OK(mkv_tree_create(dev, &u));
     uint64_t counts[1] = {0};
     OK(mkv_sharded_build(a, c, ka.blob(), va.blob(), 0, 1, counts));
+    step("built a");
     CHECK(counts[0] == ra.size());
     OK(mkv_sharded_build(b, c, kb.blob(), vb.blob(), 0, 0, nullptr));
     OK(mkv_sharded_build(a2, c, ka.blob(), va.blob(), 0, 1, nullptr));
@@ -170,9 +178,11 @@ static void test_rccl_world1(int dev) {
     CHECK(std::string(reinterpret_cast<char *>(roots), 32) == want);
     CHECK(std::string(reinterpret_cast<char *>(roots + 32), 32) == model_root(rb));
     CHECK(std::string(reinterpret_cast<char *>(roots + 64), 32) == want);
+    step("roots");
     mkv_keylist *l = nullptr;
     OK(mkv_sharded_diff(a, b, c, &l));
     if (l) CHECK(keylist(l) == model_diff(ra, rb));
+    step("diff");
     // this rank's slice and its place in the global list (world 1: the whole list at offset 0)
     mkv_keylist *ls = nullptr;
     uint64_t goff = 99, gtot = 0;
@@ -184,10 +194,12 @@ static void test_rccl_world1(int dev) {
     uint64_t calls[MKV_COLL_KINDS], bytes[MKV_COLL_KINDS], staged[MKV_COLL_KINDS], meta[MKV_COLL_KINDS];
     OK(mkv_comm_traffic(c, staged, meta));
     OK(mkv_comm_stats(c, secs, calls, bytes, 1));
-    // one meta gather per build (3), 5 fringe gathers, the diff's meta + block gathers, the slice's meta
-    CHECK(calls[MKV_COLL_COUNTS] == 3 && calls[MKV_COLL_FRINGE] == 5 && calls[MKV_COLL_DIFF] == 3);
-    CHECK(calls[MKV_COLL_RANGE] == 2);  // one boundary-key gather per range-checked build
-    CHECK(bytes[MKV_COLL_FRINGE] == 7ull * MKV_FRINGE_BYTES + 5 * 32);  // 1 + 1 + 1 + 1 + 3 trees + headers
+    // one meta gather per build (3); 5 fringe gathers + 2 status rounds (the fringe staging grew for 1 and
+    // for 3 trees); the diff's meta + block gathers (+ a status round if its staging grew), the slice's meta
+    CHECK(calls[MKV_COLL_COUNTS] == 3 && calls[MKV_COLL_FRINGE] == 7);
+    CHECK(calls[MKV_COLL_DIFF] == 3 || calls[MKV_COLL_DIFF] == 4);
+    CHECK(calls[MKV_COLL_RANGE] == 3);  // one boundary-key gather per range-checked build + the first's status round
+    CHECK(bytes[MKV_COLL_FRINGE] == 7ull * MKV_FRINGE_BYTES + 7 * 32);  // 1 + 1 + 1 + 1 + 3 trees, 5 headers, 2 rounds
     // RCCL form: no payload byte crossed between host and device; only status / count words came back
     for (int k = 0; k < MKV_COLL_KINDS; ++k) CHECK(staged[k] == 0);
     CHECK(meta[MKV_COLL_COUNTS] == 3 * 32 && meta[MKV_COLL_DIFF] > 0);
@@ -195,6 +207,20 @@ static void test_rccl_world1(int dev) {
     mkv_blob bad_v = va.blob();
     bad_v.n = bad_v.n - 1;
     CHECK(mkv_sharded_build(b, c, ka.blob(), bad_v, 0, 1, nullptr) == MKV_EINVAL);
+    OK(mkv_sharded_build(b, c, kb.blob(), vb.blob(), 0, 1, nullptr));
+    CHECK(root_of(b) == model_root(rb));
+    // a local step failing AFTER the meta all-gather (test hook: as a failed staging allocation): within the
+    // staging plan the status rides on the block header, beyond it on a status round; either way the call
+    // returns the error and the communicator stays usable
+    step("stats");
+    OK(mkv_comm_inject_fault(c, MKV_FAULT_AFTER_META));
+    l = nullptr;
+    CHECK(mkv_sharded_diff(a, b, c, &l) == MKV_ENOMEM && l == nullptr);
+    step("fault diff");
+    OK(mkv_sharded_diff(a, b, c, &l));  // the plan was reset: the staging regrows behind a status round
+    if (l) CHECK(keylist(l) == want_d);
+    OK(mkv_comm_inject_fault(c, MKV_FAULT_AFTER_META));
+    CHECK(mkv_sharded_build(b, c, kb.blob(), vb.blob(), 0, 1, nullptr) == MKV_ENOMEM);
     OK(mkv_sharded_build(b, c, kb.blob(), vb.blob(), 0, 1, nullptr));
     CHECK(root_of(b) == model_root(rb));
     for (mkv_tree *t : {a, b, a2, u}) mkv_tree_destroy(t);
@@ -220,24 +246,39 @@ static int thread_all_gather(void *ctx, const void *send, void *recv, uint64_t b
     RankCtx *rc = static_cast<RankCtx *>(ctx);
     ThreadGather &g = *rc->g;
     std::unique_lock<std::mutex> lk(g.mu);
-    g.cv.wait(lk, [&] { return g.departed == 0; });  // the previous round has drained
+    // bounded waits: a protocol bug (ranks in different collectives) fails the test instead of hanging it
+    const auto limit = std::chrono::seconds(60);
+    if (!g.cv.wait_for(lk, limit, [&] { return g.departed == 0; })) {  // the previous round has drained
+        std::printf("  FAIL rank %d: all-gather of %llu B: previous round never drained\n", rc->rank,
+                    (unsigned long long)bytes);
+        std::fflush(stdout);
+        std::_Exit(3);
+    }
     const uint64_t my = g.gen;
     g.slots[rc->rank].assign(static_cast<const char *>(send), bytes);
     if (++g.arrived == g.world) {
         ++g.gen;
         g.cv.notify_all();
-    } else {
-        g.cv.wait(lk, [&] { return g.gen != my; });
+    } else if (!g.cv.wait_for(lk, limit, [&] { return g.gen != my; })) {
+        std::printf("  FAIL rank %d: all-gather of %llu B: peers never arrived\n", rc->rank, (unsigned long long)bytes);
+        std::fflush(stdout);
+        std::_Exit(3);
     }
+    bool same = true;
     for (int r = 0; r < g.world; ++r) {
-        if (g.slots[r].size() != bytes) return 1;
-        std::memcpy(static_cast<char *>(recv) + bytes * r, g.slots[r].data(), bytes);
+        if (g.slots[r].size() != bytes) same = false;
+        else std::memcpy(static_cast<char *>(recv) + bytes * r, g.slots[r].data(), bytes);
+    }
+    if (!same) {
+        std::printf("  FAIL rank %d: all-gather sizes differ across ranks (%llu B here)\n", rc->rank,
+                    (unsigned long long)bytes);
+        std::fflush(stdout);
     }
     if (++g.departed == g.world) {
         g.arrived = g.departed = 0;
         g.cv.notify_all();
     }
-    return 0;
+    return same ? 0 : 1;
 }
 
 static void test_host_world3(int dev) {
@@ -259,7 +300,9 @@ static void test_host_world3(int dev) {
     const Digest want_upd = model_root(upd);
     std::vector<std::string> got_a(world), got_b(world), got_upd(world);
     std::vector<std::vector<std::string>> got_diff(world);
-    std::vector<int> bad_status(world, -1), fail_status(world, -1);
+    std::vector<int> bad_status(world, -1), fail_status(world, -1), fault_diff(world, -1), fault_build(world, -1),
+        fault_root(world, -1);
+    std::vector<std::vector<std::string>> got_diff2(world);
     std::vector<std::vector<std::string>> got_slice(world);
     std::vector<uint64_t> got_off(world), got_tot(world);
     std::vector<std::thread> th;
@@ -298,6 +341,29 @@ static void test_host_world3(int dev) {
                 fail_status[r] = mkv_sharded_build(b, c, bk.blob(), vbl, 0, 1, nullptr);
                 OK(mkv_sharded_build(b, c, bk.blob(), bv.blob(), 0, 1, nullptr));  // back in step
             }
+            // rank 1 fails AFTER the meta all-gather (test hook): (1) a diff whose staging fits the plan (the
+            // status rides on the block header), (2) the same diff again succeeds (the staging regrows behind a
+            // status round), (3) a range-checked build right after another failure (plan reset: the failure
+            // is reported by the status round before the boundary-key gather), (4) a root recombine; every
+            // rank returns MKV_ENOMEM from each failing call, nobody hangs
+            if (r == 1) OK(mkv_comm_inject_fault(c, MKV_FAULT_AFTER_META));
+            mkv_keylist *lf = nullptr;
+            fault_diff[r] = mkv_sharded_diff(a, b, c, &lf);
+            if (lf) mkv_keylist_free(lf);
+            lf = nullptr;
+            OK(mkv_sharded_diff(a, b, c, &lf));
+            if (lf) got_diff2[r] = keylist(lf);
+            {
+                Packed bk, bv;
+                pack(sb[r], bk, bv);
+                if (r == 1) OK(mkv_comm_inject_fault(c, MKV_FAULT_AFTER_META));
+                fault_build[r] = mkv_sharded_build(b, c, bk.blob(), bv.blob(), 0, 1, nullptr);
+                OK(mkv_sharded_build(b, c, bk.blob(), bv.blob(), 0, 1, nullptr));
+                uint8_t rr[32];
+                int hh = 0;
+                if (r == 1) OK(mkv_comm_inject_fault(c, MKV_FAULT_AFTER_META));
+                fault_root[r] = mkv_sharded_root(b, c, rr, &hh);
+            }
             // in-range update of this shard, then the global root of both replicas in one all-gather
             Packed uk, uv;
             uk.add(sa[r].begin()->first);
@@ -325,6 +391,8 @@ static void test_host_world3(int dev) {
         CHECK(got_upd[r] == want_upd);
         CHECK(bad_status[r] == MKV_EINVAL);
         CHECK(fail_status[r] == MKV_EINVAL);
+        CHECK(fault_diff[r] == MKV_ENOMEM && fault_build[r] == MKV_ENOMEM && fault_root[r] == MKV_ENOMEM);
+        CHECK(got_diff2[r] == want_diff);
         // the slices are the global list cut at the global offsets (ranges ordered by rank)
         CHECK(got_tot[r] == want_diff.size());
         CHECK(got_off[r] + got_slice[r].size() <= want_diff.size());

@@ -245,3 +245,164 @@ def test_configs3_1b_root_sequential_shards_vs_golden():
     assert counts == [ng] * nsh
     assert root == _golden_root(nsh, ng)
     del t, kb, vb, ko, vo
+
+
+def _sorted_rows(a):
+    return a[np.lexsort(a.T[::-1])] if len(a) else a
+
+
+def _b_shard(torch, g, ng, kv, ko, vv, vo, mode):
+    """Replica B of shard g (0.1 % of the records): value_only flips a byte of every 1000th value (rows
+    3 + g mod 1000); mixed removes every tenth of those rows and inserts as many new keys of the same key
+    range, so both replicas keep n_g leaves per shard (equal global offsets, different key sets -> the
+    merge-join). Returns (B blob, expected divergent keys of the shard, sorted)."""
+    from merklekv_amd.merkle import gen_records_device
+    rows = torch.arange(3 + g, ng, 1000, device="cuda")
+    k2, v2 = kv[: ng * K].view(ng, K), vv[: ng * V].view(ng, V).clone()
+    if mode == "value_only":
+        v2[rows, 9] ^= 4
+        torch.cuda.synchronize()
+        return (kv, ko, v2.view(-1), vo, ng), _sorted_rows(k2[rows].cpu().numpy())
+    rm = rows[(rows // 1000) % 10 == 0]
+    chg = rows[(rows // 1000) % 10 != 0]
+    v2[chg, 9] ^= 4
+    keep = torch.ones(ng, dtype=torch.bool, device="cuda")
+    keep[rm] = False
+    new = rm.numel()
+    nkb = torch.empty(new * K + 64, dtype=torch.uint8, device="cuda")
+    nvb = torch.empty(new * V + 64, dtype=torch.uint8, device="cuda")
+    nko = torch.empty(new + 1, dtype=torch.int64, device="cuda")
+    nvo = torch.empty(new + 1, dtype=torch.int64, device="cuda")
+    gen_records_device(0, DEFAULT_SEED, 10**12 + g * new, new, K, V, nkb.data_ptr(), nko.data_ptr(), nvb.data_ptr(),
+                       nvo.data_ptr(), shard=g, nshards=W)
+    torch.cuda.synchronize()
+    kB = torch.cat([k2[keep], nkb[: new * K].view(new, K)]).contiguous().view(-1)
+    vB = torch.cat([v2[keep], nvb[: new * V].view(new, V)]).contiguous().view(-1)
+    del v2
+    exp = torch.cat([k2[chg], k2[rm], nkb[: new * K].view(new, K)]).cpu().numpy()
+    offk = torch.arange(0, ng + 1, device="cuda", dtype=torch.int64) * K
+    offv = torch.arange(0, ng + 1, device="cuda", dtype=torch.int64) * V
+    torch.cuda.synchronize()
+    return (kB, offk, vB, offv, ng), _sorted_rows(exp)
+
+
+@pytest.mark.parametrize("mode", ["value_only", "mixed"])
+def test_configs3_1b_diff_sequential_vs_construction(mode):
+    """configs[2] x configs[3] at full size: the diff of two 1B-key replicas (8 key ranges x 125M, 0.1 %
+    divergence) on ONE GPU, shard after shard (shard.sequential_diff: both replicas' shards prepared and
+    reduced at their global offsets, the shard-local diff — top-down from the fringe roots for value-only
+    changes, merge-join for key-set changes — each list at its global offset from the counts). The
+    concatenated 1B diff equals the constructed divergent set and is globally sorted
+    (/root/reference/src/store/merkle.rs:171-196, consumed whole by sync.rs:67-83); replica A's global
+    root is the CPU oracle's golden 1B root (tests/golden/roots_sharded.json)."""
+    import torch
+
+    from merklekv_amd.merkle import gen_records_device
+    from merklekv_amd.shard import sequential_diff
+    ng, nsh = 125_000_000, W
+    kb = torch.empty(ng * K + 64, dtype=torch.uint8, device="cuda")
+    vb = torch.empty(ng * V + 64, dtype=torch.uint8, device="cuda")
+    ko = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    vo = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    exp = []
+
+    def pairs():
+        for g in range(nsh):
+            gen_records_device(0, DEFAULT_SEED, g * ng, ng, K, V, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
+                               vo.data_ptr(), shard=g, nshards=nsh)
+            torch.cuda.synchronize()
+            blob_b, e = _b_shard(torch, g, ng, kb, ko, vb, vo, mode)
+            exp.append(e)
+            yield (kb, ko, vb, vo, ng), blob_b
+            del blob_b
+
+    ta, tb = MerkleTree(), MerkleTree()
+    ra, rb, lists, offs, ms = sequential_diff(ta, tb, pairs(), ng * nsh, ng * nsh)
+    assert ra == _golden_root(nsh, ng)
+    assert rb is not None and rb != ra
+    got = np.concatenate([raw.reshape(-1, K) for raw, _ in lists])
+    want = np.concatenate(exp)  # ranges ordered by shard: the concatenation is the global order
+    assert offs == [sum(len(o) - 1 for _, o in lists[:g]) for g in range(nsh)]
+    assert len(got) == len(want) >= nsh * (ng // 1000)
+    assert np.array_equal(got, want), mode
+    assert (np.lexsort(got.T[::-1]) == np.arange(len(got))).all()  # globally sorted
+    del ta, tb, kb, vb, ko, vo
+
+
+def _c4_batches(torch, g, ng, kv, R, m):
+    """configs[4]'s batches of shard g: variant r writes m random values at m random positions
+    (duplicates: the last write wins), seeded by (r, g) so a second pass reproduces them."""
+    out = []
+    uko = torch.arange(0, m + 1, device="cuda", dtype=torch.int64) * K
+    uvo = torch.arange(0, m + 1, device="cuda", dtype=torch.int64) * V
+    for r in range(R - 1):
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(1000 * r + g)
+        sel = torch.randint(0, ng, (m,), device="cuda", generator=gen)
+        uvb = torch.randint(45, 122, (m, V), device="cuda", generator=gen, dtype=torch.uint8)
+        out.append((kv[: ng * K].view(ng, K)[sel].contiguous().view(-1), uko, uvb.contiguous().view(-1), uvo, m, sel))
+    return out
+
+
+def test_configs4_1b_incremental_sequential_vs_construction():
+    """configs[4] at full size on ONE GPU: a 1B-key tree as 8 key-range shards of 125M, base + 7 variants,
+    each variant applying 125K value updates per shard (1M per variant), shard after shard
+    (shard.sequential_incremental: dirty path for all 7 variants in one call, then the base diffed against
+    all 7 in one shared walk, every replica's fringe kept; per replica the global root from the seam
+    combine of its 8 fringes). Base root = the golden 1B root; each variant's concatenated diff = its
+    updated keys, globally sorted; variant 0's global root = a fresh sequential build of its updated
+    records (merkle.rs:52-56 and :73-121)."""
+    import torch
+
+    from merklekv_amd.merkle import gen_records_device
+    from merklekv_amd.shard import sequential_incremental, sequential_root
+    ng, nsh, R, m = 125_000_000, W, 8, 125_000
+    N = ng * nsh
+    kb = torch.empty(ng * K + 64, dtype=torch.uint8, device="cuda")
+    vb = torch.empty(ng * V + 64, dtype=torch.uint8, device="cuda")
+    ko = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    vo = torch.empty(ng + 1, dtype=torch.int64, device="cuda")
+    exp = [[] for _ in range(R - 1)]
+
+    def gen(g):
+        gen_records_device(0, DEFAULT_SEED, g * ng, ng, K, V, kb.data_ptr(), ko.data_ptr(), vb.data_ptr(),
+                           vo.data_ptr(), shard=g, nshards=nsh)
+        torch.cuda.synchronize()
+
+    def shards():
+        for g in range(nsh):
+            gen(g)
+            bs = _c4_batches(torch, g, ng, kb, R, m)
+            for r, b in enumerate(bs):
+                exp[r].append(_sorted_rows(kb[: ng * K].view(ng, K)[torch.unique(b[5])].cpu().numpy()))
+            yield (kb, ko, vb, vo, ng), [b[:5] for b in bs]
+            del bs
+
+    roots, lists, ms = sequential_incremental(shards(), N, R)
+    assert roots[0] == _golden_root(nsh, ng)
+    assert len(set(roots)) == R
+    for r in range(R - 1):
+        got = np.concatenate([raw.reshape(-1, K) for raw, _ in lists[r]])
+        want = np.concatenate(exp[r])
+        assert np.array_equal(got, want), r
+        assert (np.lexsort(got.T[::-1]) == np.arange(len(got))).all()
+    exp.clear()
+
+    def variant0():
+        for g in range(nsh):
+            gen(g)
+            ukb, uko, uvb, uvo, mm, sel = _c4_batches(torch, g, ng, kb, R, m)[0]
+            last = {}
+            for j, i in enumerate(sel.cpu().tolist()):
+                last[i] = j
+            idx = torch.tensor(list(last.keys()), device="cuda")
+            src = torch.tensor(list(last.values()), device="cuda")
+            vb[: ng * V].view(ng, V)[idx] = uvb.view(m, V)[src]
+            torch.cuda.synchronize()
+            yield (kb, ko, vb, vo, ng)
+
+    t = MerkleTree()
+    fresh, counts = sequential_root(t, variant0(), N)
+    assert counts == [ng] * nsh
+    assert fresh == roots[1]
+    del t, kb, vb, ko, vo
