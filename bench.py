@@ -15,8 +15,11 @@ keys on one GPU: the per-GPU anchor of the 125M-per-rank curve),
 config on the GPU), `configs4` (configs[4]: 125M keys x 8 replicas, 125K-key value batches per variant —
 the same measurement as `--workload incremental`, with the dirty climb's roofline), `configs3_1b_sequential`
 (configs[3]'s 1B keys on ONE GPU: 8 key-range shards resident in HBM, built shard after shard and combined,
-root checked against the CPU oracle's golden root) and the CPU baselines (cpu_ref: the reference's data
-structures, single thread; cpu_mt: all host cores).
+root checked against the CPU oracle's golden root), `configs3_1b_diff_sequential` (the diff of two 1B-key
+replicas on ONE GPU, shard after shard: value-only through the top-down walk, mixed through the merge-join,
+exact vs construction), `configs4_1b_sequential` (configs[4] at its full 1B keys on ONE GPU: 8 shards x
+(base + 7 variants), 125K-key batches per shard, replica roots from their fringes) and the CPU baselines
+(cpu_ref: the reference's data structures, single thread; cpu_mt: all host cores).
 
 Other BASELINE configs (run explicitly; their JSON lines are committed under profiles/):
   --workload diff         configs[2]: two 100M-key replicas, (a) 0.1 % value-only divergence (top-down
@@ -632,11 +635,14 @@ def wl_build(ctx, args):
         torch.cuda.empty_cache()
         if args.anchor_records:
             anchor = anchor_block(ctx, args.anchor_records)
-    c4 = c3seq = None
+    c4 = c3seq = c3diff = c4seq = None
     if not args.no_diff and ctx.world == 1 and not args.no_big:
-        # configs[4] (125M x 8 replicas, 125K-key batches) and configs[3] (1B keys, 8 shards in sequence)
+        # configs[4] (125M x 8 replicas, 125K-key batches) and configs[3] (1B keys, 8 shards in sequence):
+        # the 1B root, the 1B two-replica diff and the 1B incremental step on one GPU
         c4 = configs4_measure(ctx, 125_000_000, 125_000, 8, steps=10, warmup=3)
         c3seq = configs3_sequential_block(ctx)
+        c3diff = configs3_diff_sequential_block(ctx)
+        c4seq = configs4_sequential_block(ctx)
     c3 = None
     if not args.no_diff and ctx.dist is not None and args.anchor_records:
         c3 = sharded_anchor_block(ctx, args.anchor_records)
@@ -669,6 +675,8 @@ def wl_build(ctx, args):
         out["ragged_10m"] = ragged
         out["configs4"] = c4
         out["configs3_1b_sequential"] = c3seq
+        out["configs3_1b_diff_sequential"] = c3diff
+        out["configs4_1b_sequential"] = c4seq
         if ctx.dist is not None:
             out["diff_sharded"] = dN
             out["collectives_build"] = coll
@@ -1022,6 +1030,178 @@ def configs3_sequential_block(ctx, nshards=8, per_shard=125_000_000, steps=2, wa
            "note": "records resident in HBM before timing; per shard hash + sort + dedup + reduction at its "
                    "global offset + fringe readback (<= 6 KiB), then the seam combine: 1B-key root on one GPU"}
     del t, blobs
+    torch.cuda.empty_cache()
+    return out
+
+
+def _shard_blob(ctx, g, nshards, per_shard, bufs):
+    """Generate key range g of nshards (records [g * per_shard, (g + 1) * per_shard)) into bufs."""
+    from merklekv_amd.merkle import gen_records_device
+    kb, ko, vb, vo = bufs
+    gen_records_device(ctx.local, SEED, g * per_shard, per_shard, KLEN, VLEN, kb.data_ptr(), ko.data_ptr(),
+                       vb.data_ptr(), vo.data_ptr(), shard=g, nshards=nshards)
+    ctx.torch.cuda.synchronize()
+    return (kb, ko, vb, vo, per_shard)
+
+
+def configs3_diff_sequential_block(ctx, nshards=8, per_shard=125_000_000, steps=5, warmup=3):
+    """configs[2] x configs[3] at full size on ONE GPU: the diff of two 1B-key replicas (8 key ranges x 125M,
+    0.1 % divergence) shard after shard — what 8 ranks do in parallel. Per shard g: both replicas' shards
+    prepared and reduced at their global offsets (shard_prepare + shard_reduce), then the shard-local
+    diff_keys (value-only: top-down from the fringe roots; mixed, 90 % changed / 10 % replaced keys:
+    merge-join), warmed, then timed `steps` times (HIP-event-free, like the 100M lines); the per-shard lists
+    sit at the global offsets given by their counts. ms_per_1b_diff = the sum over the 8 shards of the mean
+    diff call (list host-visible on return). exact: every shard's list equals the constructed divergent set
+    (sorted), so the concatenation is the global list (merkle.rs:171-196, sync.rs:67-83)."""
+    torch = ctx.torch
+    import numpy as np
+    from merklekv_amd import MerkleTree
+    from merklekv_amd.merkle import gen_records_device
+    bufs = (torch.empty(per_shard * KLEN + 64, dtype=torch.uint8, device=ctx.dev),
+            torch.empty(per_shard + 1, dtype=torch.int64, device=ctx.dev),
+            torch.empty(per_shard * VLEN + 64, dtype=torch.uint8, device=ctx.dev),
+            torch.empty(per_shard + 1, dtype=torch.int64, device=ctx.dev))
+    N = nshards * per_shard
+    out = {"keys": N, "shards": nshards, "keys_per_shard": per_shard, "steps": steps}
+    for mode in ("value_only", "mixed"):
+        ta, tb = MerkleTree(ctx.local), MerkleTree(ctx.local)
+        per_ms, counts, exact, fa, fb = [], [], True, [], []
+        for g in range(nshards):
+            kb, ko, vb, vo, ng = _shard_blob(ctx, g, nshards, per_shard, bufs)
+            rows = torch.arange(3 + g, ng, 1000, device=ctx.dev)
+            kv, v2 = kb[: ng * KLEN].view(ng, KLEN), vb[: ng * VLEN].view(ng, VLEN).clone()
+            if mode == "value_only":
+                v2[rows, 9] ^= 4
+                blob_b = (kb, ko, v2.view(-1), vo, ng)
+                exp = kv[rows]
+            else:
+                rm, chg = rows[(rows // 1000) % 10 == 0], rows[(rows // 1000) % 10 != 0]
+                v2[chg, 9] ^= 4
+                keep = torch.ones(ng, dtype=torch.bool, device=ctx.dev)
+                keep[rm] = False
+                new = rm.numel()
+                nkb = torch.empty(new * KLEN + 64, dtype=torch.uint8, device=ctx.dev)
+                nvb = torch.empty(new * VLEN + 64, dtype=torch.uint8, device=ctx.dev)
+                nko = torch.empty(new + 1, dtype=torch.int64, device=ctx.dev)
+                nvo = torch.empty(new + 1, dtype=torch.int64, device=ctx.dev)
+                gen_records_device(ctx.local, SEED, 10**12 + g * new, new, KLEN, VLEN, nkb.data_ptr(), nko.data_ptr(),
+                                   nvb.data_ptr(), nvo.data_ptr(), shard=g, nshards=nshards)
+                torch.cuda.synchronize()
+                nk = nkb[: new * KLEN].view(new, KLEN)
+                kB = torch.cat([kv[keep], nk]).contiguous().view(-1)
+                vB = torch.cat([v2[keep], nvb[: new * VLEN].view(new, VLEN)]).contiguous().view(-1)
+                off = torch.arange(0, ng + 1, device=ctx.dev, dtype=torch.int64)
+                blob_b = (kB, off * KLEN, vB, off * VLEN, ng)
+                exp = torch.cat([kv[chg], kv[rm], nk])
+                del nkb, nvb
+            exp = exp.cpu().numpy()
+            exp = exp[np.lexsort(exp.T[::-1])]
+            torch.cuda.synchronize()
+            o = sum(counts)
+            counts.append(ta.shard_prepare((kb, ko, vb, vo, ng), None, on_device=True))
+            ta.shard_reduce(o, N)
+            nb = tb.shard_prepare(blob_b, None, on_device=True)
+            tb.shard_reduce(o, N)  # equal leaf counts per shard in both modes
+            del blob_b, v2
+            if mode == "mixed":
+                del kB, vB
+            fa.append(ta.shard_fringe())
+            fb.append(tb.shard_fringe())
+            d = None
+            for _ in range(warmup):
+                d = ta.diff_keys_view(tb)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                d = ta.diff_keys_view(tb)
+            per_ms.append((time.perf_counter() - t0) / steps * 1e3)
+            got = d.raw.reshape(-1, KLEN)
+            exact = exact and nb == ng and got.shape == exp.shape and bool((got == exp).all())
+            del d
+        ra = ta.shard_combine(b"".join(fa), nshards, N)
+        rb = tb.shard_combine(b"".join(fb), nshards, N)
+        out[mode] = {"ms_per_1b_diff": sum(per_ms), "ms_per_shard_diff": per_ms,
+                     "union_keys_per_s": N / (sum(per_ms) * 1e-3), "exact_vs_construction": exact,
+                     "root_a": ra.hex() if ra else None, "roots_differ": ra != rb,
+                     "path": "top-down from fringe roots" if mode == "value_only" else "merge-join"}
+        del ta, tb
+        torch.cuda.empty_cache()
+    del bufs
+    torch.cuda.empty_cache()
+    return out
+
+
+def configs4_sequential_block(ctx, nshards=8, per_shard=125_000_000, m=125_000, R=8, steps=5, warmup=2):
+    """configs[4] at full size on ONE GPU: the 1B-key tree as 8 key ranges x 125M, base + 7 variants, every
+    variant applying 125K value updates per shard (1M keys per variant), shard after shard. Per shard: the
+    base shard built at its global offset and cloned per variant; a step = every variant's batch through
+    one upsert_device_many (dirty path) + the base diffed against all 7 (diff_keys_many, one shared walk);
+    warmed, then timed. ms_per_1b_step = the sum over shards of the mean step (what 8 ranks do in parallel,
+    minus the fringe recombine). Afterwards every replica's global root from the seam combine of its 8
+    fringes: the base's equals the golden 1B root."""
+    torch = ctx.torch
+    from merklekv_amd import MerkleTree
+    bufs = (torch.empty(per_shard * KLEN + 64, dtype=torch.uint8, device=ctx.dev),
+            torch.empty(per_shard + 1, dtype=torch.int64, device=ctx.dev),
+            torch.empty(per_shard * VLEN + 64, dtype=torch.uint8, device=ctx.dev),
+            torch.empty(per_shard + 1, dtype=torch.int64, device=ctx.dev))
+    N = nshards * per_shard
+    fr = [[] for _ in range(R)]
+    per_ms, ok, off = [], True, 0
+    uko = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * KLEN
+    uvo = torch.arange(0, m + 1, device=ctx.dev, dtype=torch.int64) * VLEN
+    for g in range(nshards):
+        kb, ko, vb, vo, ng = _shard_blob(ctx, g, nshards, per_shard, bufs)
+        base = MerkleTree(ctx.local)
+        n_g = base.shard_prepare((kb, ko, vb, vo, ng), None, on_device=True)
+        base.shard_reduce(off, N)
+        off += n_g
+        variants = [base.clone() for _ in range(R - 1)]
+        batches, uniq = [], []
+        for r in range(R - 1):
+            gen = torch.Generator(device=ctx.dev)
+            gen.manual_seed(1000 * r + g)
+            sel = torch.randint(0, ng, (m,), device=ctx.dev, generator=gen)
+            ukb = kb[: ng * KLEN].view(ng, KLEN)[sel].contiguous().view(-1)
+            uvb = random_values(torch, m, ctx.dev, gen).contiguous().view(-1)
+            batches.append((ukb, uvb))
+            uniq.append(int(torch.unique(sel).numel()))
+        torch.cuda.synchronize()
+        ptrs = [(a.data_ptr(), uko.data_ptr(), b.data_ptr(), uvo.data_ptr(), m) for a, b in batches]
+
+        def step():
+            MerkleTree.upsert_device_many(variants, ptrs)
+            return base.diff_keys_many_view(variants)
+
+        for _ in range(warmup):
+            diffs = step()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            diffs = step()
+        per_ms.append((time.perf_counter() - t0) / steps * 1e3)
+        ok = ok and all(len(d) == u for d, u in zip(diffs, uniq))
+        for i, t in enumerate([base] + variants):
+            fr[i].append(t.shard_fringe())
+        del diffs, base, variants, batches
+        torch.cuda.empty_cache()
+    holder = MerkleTree(ctx.local)
+    roots = [holder.shard_combine(b"".join(f), nshards, N) for f in fr]
+    golden = None
+    try:
+        d = json.load(open(os.path.join(ROOT, "tests", "golden", "roots_sharded.json")))
+        golden = next((c["root"] for c in d["cases"] if c["shards"] == nshards and c["per_shard"] == per_shard
+                       and c["seed"] == SEED), None)
+    except (OSError, ValueError):
+        pass
+    total_updates = m * (R - 1) * nshards
+    out = {"keys": N, "shards": nshards, "replicas": R, "batch_per_shard": m, "updates_per_variant": m * nshards,
+           "steps": steps, "ms_per_1b_step": sum(per_ms), "ms_per_shard_step": per_ms,
+           "update_keys_per_s": total_updates / (sum(per_ms) * 1e-3),
+           "diff_sizes_match_unique_updates": ok, "base_root": roots[0].hex() if roots[0] else None,
+           "base_matches_golden": (roots[0].hex() == golden) if (roots[0] and golden) else None,
+           "distinct_replica_roots": len(set(roots)) == R,
+           "note": "per shard: 7 value batches (dirty path, one call) + 1-vs-7 diff, key lists host-visible; the "
+                   "1B step is the 8 shards in sequence; replica roots from the 8 fringes each"}
+    del bufs
     torch.cuda.empty_cache()
     return out
 
