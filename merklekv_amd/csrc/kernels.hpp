@@ -247,6 +247,7 @@ void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const Diff
                           bool host_offsets = false);
 // Batched top-down walk (one base vs up to TD_MAX_VARIANTS trees with the same level plan).
 constexpr int TD_MAX_VARIANTS = 64;
+constexpr int MKV_MAXLEV_TD = 48;  // = MKV_MAXLEV (levels of a tree)
 struct TdVariants {
     const uint8_t *nodes[TD_MAX_VARIANTS];  // each variant's node array (levels at the base's offsets)
 };
@@ -254,6 +255,21 @@ void launch_topdown_level_batch(const uint8_t *ca, const TdVariants &V, uint64_t
                                 uint64_t a_par, uint64_t a_child, uint64_t r0, uint64_t r1, uint32_t k,
                                 const uint64_t *fin, const uint32_t *nin, uint64_t *fout, uint32_t *nout,
                                 uint64_t max_frontier, hipStream_t st);
+// The top of an unsharded walk in ONE workgroup (round 6): the roots, then the jumps T[0] -> T[1] -> ...
+// -> T[nt] (every target level holding <= TD_TOP_MAX_NODES nodes) with the frontier in LDS between them;
+// the last level's divergent nodes go to fout (pair: u32 node; batch: variant << 32 | node) and its count to
+// cnt[T[nt]], every target level's count to cnt[T[q]] (walk statistics). k = variants (pair: 1, V.nodes[0] =
+// the other tree). Node (l, j) of any tree sits at 32 x (off[l] + j).
+constexpr uint64_t TD_TOP_MAX_NODES = 2048;
+constexpr uint64_t TD_TOP_MAX_FRONTIER = 8192;  // LDS frontier entries between the top's jumps
+constexpr uint64_t TD_TOP_MAX_WORK = 4096;      // descendants one jump of the top may compare (4 passes of the workgroup)
+struct TdTop {
+    uint64_t off[MKV_MAXLEV_TD], cnt[MKV_MAXLEV_TD];
+    uint32_t T[MKV_MAXLEV_TD];
+    uint32_t nt;  // jumps T[0] -> ... -> T[nt]
+};
+void launch_topdown_top(const uint8_t *na, const TdVariants &V, uint32_t k, const TdTop &P, void *fout, bool wide,
+                        uint32_t *cnt, hipStream_t st);
 // Jump k levels down from divergent parents (unsharded plans): fout gets every divergent descendant
 // at the target level (desc_count nodes there). max_desc: upper bound on parents << k (grid sizing).
 // gate: the one-wait pair diff's level-4 abort test folded into the jump from level 4 (k_td_gate's rule on

@@ -292,6 +292,7 @@ struct mkv_tree {
     bool sortctl_dirty = true;  // a sort started and did not reach its clearing launch
     bool kc_pending = false;    // the ragged key copy on st3 is not yet joined into st2
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
+    uint32_t walk_fused = 0;  // jumps of the last walk done inside the one-workgroup top launch
     // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
     std::vector<std::pair<uint32_t, uint32_t>> walk_jumps;
     uint32_t walk_L = 0, walk_k = 0;
@@ -2316,6 +2317,31 @@ static TdSeeds fringe_seeds(const mkv_tree *a, size_t l, size_t lt, bool top) {
 // node; near the leaves of a dense diff the frontier holds about one node per divergent leaf, so
 // two 2-level jumps read half the bytes of one 4-level jump (configs[4]: 7 replicas x 125K updates of
 // 125M leaves, levels 8 -> 0: ~26M -> ~13.5M digest pairs, ~380 -> ~200 us).
+// How many jumps of T the one-workgroup top (k_topdown_top) covers: targets of at most TD_TOP_MAX_NODES nodes,
+// not below TD_CHECK_LEVEL (the abort test rides on the jump from that level), every frontier it keeps in
+// LDS (k variants x the nodes of an intermediate target) within TD_TOP_MAX_FRONTIER, and at most
+// TD_TOP_MAX_WORK descendants compared per jump. 0: none.
+static size_t top_jumps(const mkv_tree *a, const std::vector<size_t> &T, uint32_t k, TdTop *P) {
+    size_t nt = 0;
+    for (size_t q = 1; q < T.size(); ++q) {
+        if (T[q] < TD_CHECK_LEVEL || a->lev_cnt[T[q]] > TD_TOP_MAX_NODES) break;
+        if (q >= 2 && (uint64_t)k * a->lev_cnt[T[q - 1]] > TD_TOP_MAX_FRONTIER) break;
+        // one CU reads ~64 KB per pass of its 1,024 threads: a heavier jump is faster as its own launch
+        // (configs[4]'s 20 -> 16 for 7 variants: 13K descendants, slower inside the top than launched)
+        if ((uint64_t)k * (q >= 2 ? a->lev_cnt[T[q - 1]] : 1) << (T[q - 1] - T[q]) > TD_TOP_MAX_WORK) break;
+        nt = q;
+    }
+    if (!nt) return 0;
+    std::memset(P, 0, sizeof *P);
+    for (size_t l = 0; l < a->lev_cnt.size() && l < (size_t)MKV_MAXLEV_TD; ++l) {
+        P->off[l] = a->lev_off[l];
+        P->cnt[l] = a->lev_cnt[l];
+    }
+    for (size_t q = 0; q <= nt; ++q) P->T[q] = (uint32_t)T[q];
+    P->nt = (uint32_t)nt;
+    return nt;
+}
+
 static std::vector<size_t> jump_targets(size_t L, bool fine = false) {
     std::vector<size_t> T{L - 1};
     for (int64_t x = (int64_t)((L - 2) / 4) * 4; x >= 0; x -= (fine && x <= 8) ? 2 : 4) T.push_back((size_t)x);
@@ -2470,26 +2496,42 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     if (!klen) blk->fill_n = 0;  // the device writes the offsets region
     blk->fill_n = std::min<uint64_t>(blk->fill_n, cap_m + 1);  // the key bytes start at kpos
     const size_t pd = prof_begin(t, "diff");  // the queued device work (the wait excluded)
-    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
-    // (one 1,024-thread workgroup zeroing and sampling in a single launch measured slower: 0.238 vs 0.231 ms)
-    launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
     const bool sh = a->sharded;  // same plan: b is sharded the same way
+    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
+    // (one 1,024-thread workgroup zeroing and sampling in a single launch measured slower: 0.238 vs 0.231 ms;
+    // round 6: inside the one-workgroup top as well, 0.187-0.194 vs 0.172 ms — one CU's few thousand random
+    // prefix reads are slower than 16 workgroups' — and the landing jump adding each divergent leaf to its
+    // position block's count, so no count pass: 0.193 vs 0.187 ms)
+    launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
     // the position bitmap is all-zero between calls; zeroed here (grown) before the jump that lands on the
     // leaves sets its bits
     if (t->td_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
     t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
-    if (!sh) {
-        launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
-                             cnt + L, fout, cnt + (L - 1), 0, t->st);
-        std::swap(fin, fout);
-    }  // sharded: the frontier at the top level starts empty (cnt[L - 1] = 0); the roots come in as seeds
     const std::vector<size_t> T = jump_targets(L);
+    TdTop P;
+    const size_t nt = sh ? 0 : top_jumps(a, T, 1, &P);
     t->walk_jumps.clear();  // mkv_tree_walk_stats describes this walk (one variant)
     t->walk_L = (uint32_t)L;
     t->walk_k = 1;
-    for (size_t q = 1; q < T.size(); ++q) {
+    t->walk_fused = 0;
+    size_t q0 = 1;
+    if (!sh) {
+        if (nt) {  // the roots and the first nt jumps in one workgroup
+            TdVariants V{};
+            V.nodes[0] = nb;
+            launch_topdown_top(na, V, 1, P, fout, false, cnt, t->st);
+            for (size_t q = 1; q <= nt; ++q) t->walk_jumps.emplace_back((uint32_t)T[q - 1], (uint32_t)T[q]);
+            t->walk_fused = (uint32_t)nt;
+            q0 = nt + 1;
+        } else {
+            launch_topdown_level(na + 32 * a->lev_off[L - 1], nb + 32 * b->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, fin,
+                                 cnt + L, fout, cnt + (L - 1), 0, t->st);
+        }
+        std::swap(fin, fout);
+    }  // sharded: the frontier at the top level starts empty (cnt[L - 1] = 0); the roots come in as seeds
+    for (size_t q = q0; q < T.size(); ++q) {
         const size_t l = T[q - 1], lt = T[q];
         const int k = (int)(l - lt);
         t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
@@ -2826,12 +2868,23 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         t->tb_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
     }
     const size_t pwalk = prof_begin(t, "walk");
+    t->walk_fused = 0;
     if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
-        launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX, k,
-                                   fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
-        std::swap(fin, fout);
         const std::vector<size_t> T = jump_targets(L, true);
-        for (size_t q = 1; q < T.size(); ++q) {
+        TdTop P;
+        const size_t nt = top_jumps(a, T, k, &P);
+        size_t q0 = 1;
+        if (nt) {  // the roots and the first nt jumps in one workgroup
+            launch_topdown_top(na, V, k, P, fout, true, cnt, t->st);
+            for (size_t q = 1; q <= nt; ++q) t->walk_jumps.emplace_back((uint32_t)T[q - 1], (uint32_t)T[q]);
+            t->walk_fused = (uint32_t)nt;
+            q0 = nt + 1;
+        } else {
+            launch_topdown_level_batch(na + 32 * a->lev_off[L - 1], V, 32 * a->lev_off[L - 1], 1, 0, 0, 0, UINT64_MAX,
+                                       k, fin, cnt + L, fout, cnt + (L - 1), 0, t->st);
+        }
+        std::swap(fin, fout);
+        for (size_t q = q0; q < T.size(); ++q) {
             const size_t l = T[q - 1], lt = T[q];
             const int kk = (int)(l - lt);
             t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
@@ -3617,7 +3670,7 @@ mkv_status mkv_tree_walk_stats(const mkv_tree *t, uint64_t out[4]) {
         out[0] = entries;
         out[1] = bytes;
         out[2] = h[0];
-        out[3] = t->walk_jumps.size() + 1;
+        out[3] = t->walk_jumps.size() + 1 - t->walk_fused;  // launches (the one-workgroup top counts once)
     });
 }
 
