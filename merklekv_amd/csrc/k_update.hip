@@ -445,8 +445,21 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
             const uint64_t key = keys[s];
             t = (uint32_t)(key >> A.pbits);
             if ((s + 1 == n || keys[s + 1] != key) && t < A.k && s_miss[t] == 0) {
+                // earlier writes of the same key: the run's start by galloping back, then a binary search
+                // (a serial walk was O(run length) dependent loads on one lane: a hot key written 1e5 times
+                // stalled its wave and with it the whole climb launch)
                 lo = s;
-                while (lo > 0 && keys[lo - 1] == key) --lo;  // earlier writes of the same key
+                uint32_t step = 1;
+                while (lo >= step && keys[lo - step] == key) {
+                    lo -= step;
+                    step <<= 1;
+                }
+                uint32_t a = lo >= step ? lo - step + 1 : 0;  // keys[a - 1] != key (or a == 0); keys[lo] == key
+                while (a < lo) {
+                    const uint32_t mid = (a + lo) >> 1;
+                    if (keys[mid] == key) lo = mid;
+                    else a = mid + 1;
+                }
                 load_digest(A.bdig + 32ull * A.bidx[s], d);
                 surv = true;
             }
@@ -552,6 +565,12 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                     __hip_atomic_store(mine + 4, right ? (uint64_t)hi : (uint64_t)lo, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(mine + 5, right ? pn : pp1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // The hand-off form of MI355X_MICROARCH.md (valid forms, hand-off table row 1): the one lane
+                    // that stored its payload with agent-scope (sc1, write-through) atomic stores drains them, then
+                    // signals with an agent-scope atomic; the consumer is the lane told by its atomic's return
+                    // value and reads the payload with sc1 (agent atomic) loads. gfx950 / ROCm 7.2 behaviour, not
+                    // the C++ model's release/acquire: an ACQ_REL fetch_or (buffer_wbl2 sc1 + buffer_inv sc1 per
+                    // merge) measured climb 0.81 -> 1.42 ms at configs[4] (round 6).
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     uint32_t *bw = A.bflags + (b >> 5);
                     const uint32_t bit = 1u << (b & 31);

@@ -293,6 +293,7 @@ struct mkv_tree {
     bool kc_pending = false;    // the ragged key copy on st3 is not yet joined into st2
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
     uint32_t walk_fused = 0;  // jumps of the last walk done inside the one-workgroup top launch
+    uint64_t hix_skip_gen = 0;  // pfx_gen + 1 of a key set whose hash index did not fit (0: none)
     // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
     std::vector<std::pair<uint32_t, uint32_t>> walk_jumps;
     uint32_t walk_L = 0, walk_k = 0;
@@ -1744,7 +1745,28 @@ static const uint64_t *locate_index_of(mkv_tree *t, hipStream_t st, uint64_t *ma
     uint64_t cap = 1;
     while (cap < 2 * t->n) cap <<= 1;
     const bool fresh = t->hix_gen != t->pfx_gen || t->hix_mask != cap - 1 || t->hix.cap < cap * 8;
-    uint64_t *tab = ens<uint64_t>(t->hix, cap);
+    if (fresh && t->hix_skip_gen == t->pfx_gen + 1) return nullptr;  // no room for this key set's index
+    uint64_t *tab = nullptr;
+    if (fresh) {
+        // The index is an accelerator (2n slots of 8 B: 2 GiB at 125M keys): when the device cannot hold it,
+        // the locate keeps the sample search instead of failing the update, and the key set is
+        // not retried until it changes.
+        size_t free_b = 0, total_b = 0;
+        const bool room = hipMemGetInfo(&free_b, &total_b) == hipSuccess &&
+                          (uint64_t)free_b + t->hix.cap >= cap * 8 + (256ull << 20);
+        try {
+            if (!room) throw Error(ST_ENOMEM, "hash index does not fit");
+            tab = ens<uint64_t>(t->hix, cap);
+        } catch (const Error &) {
+            (void)hipGetLastError();  // clear a failed hipMalloc
+            t->hix.release();
+            t->hix_gen = ~0ull;
+            t->hix_skip_gen = t->pfx_gen + 1;
+            return nullptr;
+        }
+    } else {
+        tab = t->hix.as<uint64_t>();
+    }
     if (fresh) {
         MKV_HIP(hipMemsetAsync(tab, 0, cap * 8, st));
         launch_hix_build(side_of(t), tab, cap - 1, st);

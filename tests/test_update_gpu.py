@@ -755,3 +755,32 @@ def test_batched_diff_per_variant_split_each_call():
         for i, (raw, offs) in enumerate(got):
             b, o = raw.tobytes(), offs.tolist()
             assert [b[o[j]:o[j + 1]] for j in range(len(o) - 1)] == expect[i], (rnd, i)
+
+
+@pytest.mark.parametrize("run", [1, 2, 63, 64, 65, 1000, 100_000])
+def test_dirty_climb_hot_key_long_runs_vs_oracle(run):
+    """One key written `run` times in a batch (plus scattered writes before and after it): the lane holding
+    the run's LAST write finds the run's start by galloping back + a binary search over the sorted entries
+    (ADVICE r5: a serial walk back was O(run) dependent loads on one lane). The last write wins (merkle.rs:54);
+    root and every level array vs the oracle's insert-then-rebuild (merkle.rs:52-56, :73-121)."""
+    import torch
+    n = 200_003
+    kb, ko, vb, vo = coracle.gen_records(DEFAULT_SEED, 0, n)
+    keys = split_blob(kb, ko)
+    rng = np.random.default_rng(run)
+    t = MerkleTree()
+    t.build((kb, ko), (vb, vo))
+    o = coracle.OracleTree.build(kb, ko, vb, vo)
+    hot = int(rng.integers(1, n - 1))
+    idx = list(rng.integers(0, n, size=300)) + [hot] * run + list(rng.integers(0, n, size=300)) + [hot - 1, hot + 1]
+    ks, vs = _batch(keys, idx, "hot")
+    bk, bo = pack(ks)
+    bv, bvo = pack(vs)
+    d = [torch.from_numpy(bk.copy()).cuda(), torch.from_numpy(bo.astype(np.int64)).cuda(),
+         torch.from_numpy(bv.copy()).cuda(), torch.from_numpy(bvo.astype(np.int64)).cuda()]
+    torch.cuda.synchronize()
+    t.upsert_device(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(), d[3].data_ptr(), len(ks))
+    o2 = o.upsert(bk, bo, bv, bvo)
+    assert t.get_root_hash() == o2.root()
+    assert _levels(t) == _oracle_levels(o2)
+    assert sum(t.update_counts()) > 0  # the dirty path ran
