@@ -400,7 +400,7 @@ void launch_leaf_hash_multi(const LeafBatches &B, uint32_t k, uint64_t mmax, uin
     MKV_LAUNCH_CHECK();
 }
 
-size_t leaf_ctr_words(uint64_t n) { return CTR_EDGE_LIST + n + 16; }
+size_t leaf_ctr_words(uint64_t) { return CTR_LIST + LEAF_MAX_WAVES + 16; }
 
 // Waves of the fixed-shape kernel for n records (the ragged kernel needs the same number).
 
@@ -428,7 +428,8 @@ void launch_leaf_hash(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb
     // the key copy stores at the source's byte offsets: kb must share kdst's 16-B alignment
     const KeyOut K{(reinterpret_cast<uintptr_t>(kb) & 15) == 0 ? KO.kdst : nullptr, KO.odst, KO.kcap};
     launch_leaf_fixed(kb, koff, vb, voff, n, out, ctr, st, K);
-    launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st, K);  // (and the edge records it leaves)
+    launch_leaf_ragged(kb, koff, vb, voff, n, out, ctr, st, K);
+    launch_leaf_edges(kb, koff, vb, voff, n, out, st);  // the records near the blobs' ends it leaves
     if (K.kdst) launch_keycopy_ragged(kb, koff, n, ctr, K.kdst, K.kcap, st);
 }
 

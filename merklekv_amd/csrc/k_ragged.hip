@@ -119,18 +119,26 @@ __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint32_t k1, uint
     R.live = true;
 }
 
-// A record whose source dwords would reach outside the blobs (within ~128 B of a blob's ends; every record
-// of a blob of empty or tiny keys) goes to k_leaf_edges instead: no bounds checks in this kernel's loads
-// (the checked form cost ~70 VGPRs).
+// Records near the blobs' ends (every record of a blob of empty or tiny keys) go to k_leaf_edges instead:
+// no bounds checks in this kernel's loads (the checked form cost ~70 VGPRs). The split is an interval:
+// record i is hashed here iff
+//   koff[i] >= koff[0] + 67,  voff[i] >= voff[0] + 6,  koff[i+1] + 68 <= koff[n],  voff[i+1] + 136 <= voff[n]
+// — each test monotone in i, so the records left over are a prefix and a suffix that k_leaf_edges finds by
+// itself (two searches), runs on another stream beside this kernel and needs no list from it. Each test
+// implies its term of rg_take's R.safe (ka <= kmis + k0 and 4 b1 <= 4 + k; va >= vmis + v0 - 6;
+// 4 (b3 - b1) <= v + 7), which stays as a guard: a record that passed the interval test but not R.safe
+// would be left unhashed (a parity failure), never loaded out of bounds.
+struct RgSplit {
+    uint64_t kA, vA, KN, VN;  // koff[0] + 67, voff[0] + 6, koff[n], voff[n]
+};
+__device__ __forceinline__ bool rg_inner(const RgSplit &X, uint64_t k0, uint64_t k1, uint64_t v0, uint64_t v1) {
+    return k0 >= X.kA && v0 >= X.vA && k1 + 68 <= X.KN && v1 + 136 <= X.VN;
+}
 __device__ __forceinline__ void rg_take_or_leave(RgRec &R, uint64_t k0, uint32_t k1, uint64_t v0, uint32_t v1,
                                                  uint32_t r, uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi,
-                                                 int64_t vlo, int64_t vhi, uint32_t *ctr) {
-
+                                                 int64_t vlo, int64_t vhi, const RgSplit &X) {
     rg_take(R, k0, k1, v0, v1, r, kmis, vmis, klo, khi, vlo, vhi);
-    if (!R.safe) {
-        ctr[CTR_EDGE_LIST + atomicAdd(&ctr[CTR_EDGES], 1u)] = r;
-        R.live = false;
-    }
+    R.live = R.safe && rg_inner(X, k0, k0 + R.k, v0, v0 + (R.L - 8 - R.k));
 }
 
 // The block's positions of the boundary words (block-relative, may lie outside 0..15).
@@ -227,6 +235,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     const uint8_t *kbase = kb - kmis, *vbase = vb - vmis;
     const int64_t klo = (int64_t)((kmis + koff[0]) & ~3ull), khi = (int64_t)((kmis + koff[n] + 3) & ~3ull);
     const int64_t vlo = (int64_t)((vmis + voff[0]) & ~3ull), vhi = (int64_t)((vmis + voff[n] + 3) & ~3ull);
+    const RgSplit X{koff[0] + 67, voff[0] + 6, koff[n], voff[n]};
 
     Q.pnext = rg_grab(ctr, lane);
     Q.pv = Q.pe = 0;
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     // stored then, from registers that were loaded a step earlier (a store in the refill itself would wait
     // for the offsets it just requested)
     auto take = [&]() {
-        rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, ctr);
+        rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, X);
         if (KO.odst) {
             KO.odst[nrec] = nk0;
             if ((uint64_t)nrec + 1 == n) KO.odst[n] = koff[n];
@@ -371,10 +380,10 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     }
 }
 
-// The records k_leaf_ragged left (near the blobs' ends): one wave per record, lane l reads message byte l of
-// each block inside the record's fields (no load outside them), shuffles assemble the 16 words, and every
-// lane runs the compression. A handful of records normally; every record only for blobs of empty or tiny
-// keys.
+// The records k_leaf_ragged leaves (the prefix and suffix outside rg_inner's interval): one wave per record,
+// lane l reads message byte l of each block inside the record's fields (no load outside them), shuffles
+// assemble the 16 words, and every lane runs the compression. A few hundred records normally; every record
+// only for blobs of empty or tiny keys.
 __device__ __forceinline__ uint32_t edge_byte(const uint8_t *kp, const uint8_t *vp, uint32_t k, uint32_t v, uint32_t L,
                                               uint32_t nb, uint32_t p) {
     if (p < 4) return (k >> (24 - 8 * p)) & 0xFFu;
@@ -388,14 +397,46 @@ __device__ __forceinline__ uint32_t edge_byte(const uint8_t *kp, const uint8_t *
     }
     return 0u;
 }
+// First i in [0, n) with pred(i) (n if none) for a predicate monotone false -> true: a 64-ary search by
+// one wave (4 rounds for 16M records; the answer stays in [lo, hi], probes at or past hi count as true).
+template <class Pred>
+__device__ uint64_t edge_first(uint64_t n, uint32_t lane, Pred pred) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t step = (hi - lo + 63) / 64, idx = lo + lane * step;
+        const uint64_t m = __ballot(idx >= hi || pred(idx));
+        if (m == 0) {
+            lo += 63 * step + 1;
+            continue;
+        }
+        const uint32_t f = (uint32_t)__builtin_ctzll(m);
+        if (f == 0) return lo;
+        hi = std::min<uint64_t>(lo + f * step, hi);
+        lo += (uint64_t)(f - 1) * step + 1;
+    }
+    return lo;
+}
 __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ kb, const uint64_t *__restrict__ koff,
                                                    const uint8_t *__restrict__ vb, const uint64_t *__restrict__ voff,
-                                                   uint8_t *__restrict__ out, const uint32_t *__restrict__ ctr) {
-    const uint32_t m = ctr[CTR_EDGES];
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t nw = gridDim.x * (blockDim.x / 64);
-    for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < m; i += nw) {
-        const uint32_t r = ctr[CTR_EDGE_LIST + i];
+                                                   uint64_t n, uint8_t *__restrict__ out) {
+    __shared__ uint64_t s_ends[2];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave < 2) {
+        const RgSplit X{koff[0] + 67, voff[0] + 6, koff[n], voff[n]};
+        // P: first record past the prefix; S: first record of the suffix
+        const uint64_t e = wave == 0 ? edge_first(n, lane, [&](uint64_t i) { return koff[i] >= X.kA && voff[i] >= X.vA; })
+                                     : edge_first(n, lane, [&](uint64_t i) {
+                                           return !(koff[i + 1] + 68 <= X.KN && voff[i + 1] + 136 <= X.VN);
+                                       });
+        if (lane == 0) s_ends[wave] = e;
+    }
+    __syncthreads();
+    uint64_t P = s_ends[0], S = s_ends[1];
+    if (P >= S) P = S = n;  // no interval: every record is an edge one
+    const uint64_t m = P + (n - S);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave; i < m; i += nw) {
+        const uint64_t r = i < P ? i : S + (i - P);
         const uint64_t k0 = koff[r], v0 = voff[r];
         const uint32_t k = (uint32_t)(koff[r + 1] - k0), v = (uint32_t)(voff[r + 1] - v0);
         const uint32_t L = 8 + k + v, nb = (L + 72) >> 6;
@@ -465,8 +506,14 @@ void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *
     const uint64_t grid = std::min<uint64_t>((uint64_t)device_cus() * MKV_RAGGED_WGS, ceil_div(ceil_div(n, 64), RG_WAVES));
     hipLaunchKernelGGL(k_leaf_ragged<false>, dim3((uint32_t)std::max<uint64_t>(grid, 1)), dim3(64 * RG_WAVES), 0, st,
                        kb, koff, vb, voff, n, out, ctr, leaf_fixed_waves(n), KO);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_leaf_edges(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                       uint8_t *out, hipStream_t st) {
+    if (!n) return;
     hipLaunchKernelGGL(k_leaf_edges, dim3((uint32_t)std::min<uint64_t>(ceil_div(n, 256), 256)), dim3(256), 0, st, kb, koff,
-                       vb, voff, out, ctr);
+                       vb, voff, n, out);
     MKV_LAUNCH_CHECK();
 }
 

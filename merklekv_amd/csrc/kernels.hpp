@@ -27,10 +27,15 @@ uint32_t leaf_fixed_waves(uint64_t n);
 // chunk of the configs' 32/100-B shape and hands every other chunk to the ragged stage.
 void launch_leaf_fixed(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                        uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO);
-// Every chunk launch_leaf_fixed left (k_ragged.hip: any key / value lengths and alignments), then the few
-// records near the blobs' ends (k_leaf_edges). Same stream, after launch_leaf_fixed.
+// Every chunk launch_leaf_fixed left (k_ragged.hip: any key / value lengths and alignments) except the
+// records near the blobs' ends. Same stream, after launch_leaf_fixed.
 void launch_leaf_ragged(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
                         uint8_t *out_digests, uint32_t *ctr, hipStream_t st, const KeyOut &KO);
+// The records near the blobs' ends (a prefix and a suffix it finds itself; k_ragged.hip rg_inner): needs
+// nothing from the other leaf kernels, so it may run on another stream beside them (it may rehash a record
+// k_leaf_direct also hashes: the same 32 bytes).
+void launch_leaf_edges(const uint8_t *kb, const uint64_t *koff, const uint8_t *vb, const uint64_t *voff, uint64_t n,
+                       uint8_t *out_digests, hipStream_t st);
 // Key bytes of the chunks the ragged stage hashes (k_leaf_ragged stores only their offsets), 16-B
 // granules at the source offsets into kdst (<= kcap). Needs only launch_leaf_fixed's hand-off words: may
 // run on another stream once launch_leaf_fixed is done.

@@ -16,14 +16,11 @@ constexpr uint32_t LEAF_CHUNK = 64;
 //                chunk and the rest of its range in its slot); other waves go on.
 //   [CTR_RAGGED] k_leaf_ragged's hand-out counter over its virtual chunk space: the slots' chunks first
 //                (NW x LEAF_GRAIN ids, empty ones skipped), then chunks [B, nch).
-//   [CTR_EDGES]  records the ragged kernel left to k_leaf_edges (their source dwords would reach outside
-//                the blobs: records within ~128 B of a blob's ends); their ids at [CTR_EDGE_LIST ..).
 //   [CTR_LIST + w] wave w's slot: (first chunk << 5) | count (0: nothing left to the ragged stage).
 // No same-address atomics when every chunk is ragged: the waves' first chunks are static.
-constexpr uint32_t CTR_FIXED = 0, CTR_STOP = 1, CTR_RAGGED = 2, CTR_EDGES = 3, CTR_HEAD = 4, CTR_LIST = 8;
+constexpr uint32_t CTR_FIXED = 0, CTR_STOP = 1, CTR_RAGGED = 2, CTR_HEAD = 4, CTR_LIST = 8;
 constexpr uint32_t LEAF_GRAIN = 4;     // k_leaf_direct: chunks per hand-out atomic
 constexpr uint32_t LEAF_MAX_WAVES = 16384;  // slots: fixed-kernel waves (persistent grid, <= 16 per CU)
-constexpr uint32_t CTR_EDGE_LIST = CTR_LIST + LEAF_MAX_WAVES;  // n entries (every record may be an edge one)
 
 // Key ownership of a build from borrowed device blobs: the leaf kernels store the key bytes they load at
 // their source byte offsets into kdst (the tree's key buffer; kb 16-B aligned, so offsets coincide), and

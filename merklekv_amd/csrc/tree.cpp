@@ -248,7 +248,7 @@ struct mkv_tree {
     hipStream_t st2 = nullptr;  // aux stream: key ownership copy, prefix sort, ties, dedup (overlaps st)
     hipEvent_t ev_in = nullptr, ev_join = nullptr, ev_wait = nullptr;
     hipStream_t st3 = nullptr;  // build: the ragged chunks' key copy, beside the ragged hash
-    hipEvent_t ev_fixed = nullptr, ev_kc = nullptr;
+    hipEvent_t ev_fixed = nullptr, ev_kc = nullptr, ev_edge = nullptr;
 
     // ---- contents (device) ----
     uint64_t n = 0;       // local leaves
@@ -1372,6 +1372,7 @@ mkv_status mkv_tree_create(int hip_device, mkv_tree **out) {
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_wait, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_fixed, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_kc, hipEventDisableTiming);
+        if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_edge, hipEventDisableTiming);
         if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&t->ev_a, hipEventDisableTiming);
         if (e2 == hipSuccess) {
             // copy stream at the lowest priority: HIP keeps one pool of hardware queues per priority
@@ -1403,6 +1404,7 @@ void mkv_tree_destroy(mkv_tree *t) {
     if (t->ev_wait) (void)hipEventDestroy(t->ev_wait);
     if (t->ev_fixed) (void)hipEventDestroy(t->ev_fixed);
     if (t->ev_kc) (void)hipEventDestroy(t->ev_kc);
+    if (t->ev_edge) (void)hipEventDestroy(t->ev_edge);
     if (t->ev_a) (void)hipEventDestroy(t->ev_a);
     t->a_ev.reset();
     if (t->st3) (void)hipStreamDestroy(t->st3);
@@ -1522,14 +1524,23 @@ static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t
     if ((reinterpret_cast<uintptr_t>(kb) & 15) != 0) KO.kdst = nullptr;  // copies keep the source offsets
     uint32_t *ctr = ens<uint32_t>(t->leaf_ctr, leaf_ctr_words(n));
     launch_leaf_fixed(kb, koff, vb, voff, n, dig, ctr, t->st, KO);
-    if (KO.kdst && n) {  // the ragged chunks' key bytes: on st3 beside the ragged hash, joined into st2
-        MKV_HIP(hipEventRecord(t->ev_fixed, t->st));
+    if (!n) return;
+    // st3, beside the leaf kernels: the edge records from the start (inputs ready at the callers'
+    // fork_streams event; joined into st before the reduction), then the ragged chunks' key bytes once
+    // k_leaf_direct is done (joined into st2). The ragged kernel is queued right after k_leaf_direct: host
+    // calls in between delayed its start by ~13 us.
+    MKV_HIP(hipEventRecord(t->ev_fixed, t->st));
+    launch_leaf_ragged(kb, koff, vb, voff, n, dig, ctr, t->st, KO);
+    MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_in, 0));
+    launch_leaf_edges(kb, koff, vb, voff, n, dig, t->st3);
+    MKV_HIP(hipEventRecord(t->ev_edge, t->st3));
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_edge, 0));  // the reduction reads the edge digests
+    if (KO.kdst) {
         MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_fixed, 0));
         launch_keycopy_ragged(kb, koff, n, ctr, KO.kdst, KO.kcap, t->st3);
         MKV_HIP(hipEventRecord(t->ev_kc, t->st3));
         t->kc_pending = true;
     }
-    launch_leaf_ragged(kb, koff, vb, voff, n, dig, ctr, t->st, KO);
 }
 
 static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, const uint8_t *vb,

@@ -119,6 +119,45 @@ def test_ragged_device_blobs_at_every_alignment(kshift, vshift):
     assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 64, 65, 300, 5000])
+@pytest.mark.parametrize("shape", ["tiny", "big_ends", "tiny_ends"])
+def test_ragged_edge_prefix_and_suffix(n, shape):
+    """The records near the blobs' ends (k_leaf_edges: a prefix and a suffix it finds by two searches,
+    k_ragged.hip rg_inner): blobs of tiny records only (no interval: every record an edge one), long
+    records at both ends around tiny ones, tiny records at both ends around long ones; bases 1 / 3 bytes
+    past an allocation start. Root and leaves equal the oracle's."""
+    import torch
+    rng = np.random.default_rng(1000 + n)
+    def lens(i):
+        if shape == "tiny":
+            return int(rng.integers(0, 4)), int(rng.integers(0, 4))
+        end = i < 3 or i >= n - 3
+        if shape == "big_ends":
+            return (int(rng.integers(60, 300)), int(rng.integers(100, 700))) if end else (int(rng.integers(0, 5)), int(rng.integers(0, 9)))
+        return (int(rng.integers(0, 3)), int(rng.integers(0, 3))) if end else (int(rng.integers(8, 64)), int(rng.integers(16, 256)))
+    kv = [lens(i) for i in range(n)]
+    keys = [rng.integers(0, 256, size=k, dtype=np.uint8).tobytes() for k, _ in kv]
+    vals = [rng.integers(0, 256, size=v, dtype=np.uint8).tobytes() for _, v in kv]
+    (pk, pko), (pv, pvo) = pack(keys), pack(vals)
+    o = coracle.OracleTree.build(pk, pko, pv, pvo)
+    dk = torch.zeros(len(pk) + 1, dtype=torch.uint8, device="cuda")
+    dv = torch.zeros(len(pv) + 3, dtype=torch.uint8, device="cuda")
+    if len(pk):
+        dk[1:] = torch.from_numpy(pk.copy()).cuda()
+    if len(pv):
+        dv[3:] = torch.from_numpy(pv.copy()).cuda()
+    dko = torch.from_numpy(pko.astype(np.int64)).cuda()
+    dvo = torch.from_numpy(pvo.astype(np.int64)).cuda()
+    torch.cuda.synchronize()
+    t = MerkleTree()
+    t.build_device(dk.data_ptr() + 1, dko.data_ptr(), dv.data_ptr() + 3, dvo.data_ptr(), n)
+    assert t.get_root_hash() == o.root()
+    assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
+    got = leaf_digests(keys, vals)
+    for k, v, g in zip(keys, vals, got):
+        assert g == _enc_digest(k, v), (len(k), len(v))
+
+
 def test_ragged_mixed_with_fixed_chunks_and_duplicates():
     """Fixed-shape chunks (32 / 100 B, k_leaf_direct) interleaved with ragged ones, duplicate keys (last
     write wins) and empty keys / values, against the oracle."""
