@@ -784,7 +784,6 @@ __global__ __launch_bounds__(256) void k_sample_pfx(const uint64_t *__restrict__
     }
     if (bad) atomicAdd(count, bad);
 }
-
 // ---- top-down walk in jumps of k levels (unsharded plans) ----
 // A divergent node p at level l has its level-(l-k) descendants at [p << k, (p+1) << k) (clipped to the
 // level: R5 promotion keeps the implicit arrays aligned). Comparing those 2^k nodes directly — they are
@@ -867,10 +866,28 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_u(const uint8_t *__
                                                        uint64_t desc_count, int k, const uint32_t *__restrict__ fin,
                                                        const uint32_t *__restrict__ nin, uint32_t *__restrict__ fout,
                                                        uint32_t *__restrict__ nout, uint32_t *__restrict__ gate,
-                                                       uint32_t word, uint64_t level_count, uint32_t *__restrict__ bm) {
+                                                       uint32_t word, uint64_t level_count, uint32_t *__restrict__ bm,
+                                                       const uint32_t *__restrict__ scr, TdScreen SC) {
     __shared__ uint32_t sapp[17];
+    // SC.slots: this jump also takes the key-set screen (a jump before the gated one): the sampled prefix
+    // loads issue first and are counted after the walk's work, one word per slot (plain stores)
+    uint32_t sbad = 0;  // bit j: this thread's sample of the block's j-th slot differs
+    if (SC.slots) {
+        const uint32_t samples = (uint32_t)std::min<uint64_t>(SC.n, 256u * TD_SCREEN_SLOTS);
+        uint32_t j = 0;
+        for (uint32_t sl = blockIdx.x; sl < TD_SCREEN_SLOTS; sl += gridDim.x, ++j) {
+            const uint32_t q = sl * 256 + threadIdx.x;
+            if (threadIdx.x < 256 && q < samples) {
+                const uint64_t i = samples > 1 ? (uint64_t)((unsigned __int128)q * (SC.n - 1) / (samples - 1)) : 0;
+                sbad |= (uint32_t)(SC.pa[i] != SC.pb[i]) << j;
+            }
+        }
+    }
     const uint32_t cnt = *nin;
-    if (gate && (gate[word] != 0 || 2ull * cnt > level_count)) {  // the level-4 abort test of the pair walk
+    uint32_t screen = 0;  // k_sample_pfx_slots' words (scr: TD_SCREEN_SLOTS of them), else the gate word's count
+    if (gate && scr)
+        for (int i = 0; i < TD_SCREEN_SLOTS; ++i) screen |= scr[i];
+    if (gate && (screen != 0 || gate[word] != 0 || 2ull * cnt > level_count)) {  // the level-4 abort test of the pair walk
         if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(gate + word, 0x80000000u);
         return;
     }
@@ -914,6 +931,13 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_u(const uint8_t *__
                 fout[o++] = (uint32_t)c[u];
                 if (bm) atomicOr(bm + (c[u] >> 5), 1u << (c[u] & 31));  // landing on the leaves: position bitmap
             }
+        }
+    }
+    if (SC.slots) {
+        uint32_t j = 0;
+        for (uint32_t sl = blockIdx.x; sl < TD_SCREEN_SLOTS; sl += gridDim.x, ++j) {
+            const int c = __syncthreads_count((sbad >> j) & 1u);
+            if (threadIdx.x == 0) SC.slots[sl] = (uint32_t)c;
         }
     }
 }
@@ -991,13 +1015,17 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_batch_u(const uint8
 constexpr uint32_t TOP_F = (uint32_t)TD_TOP_MAX_FRONTIER;  // LDS frontier entries (the host bounds k x nodes)
 template <bool WIDE>
 __global__ __launch_bounds__(1024) void k_topdown_top(const uint8_t *__restrict__ na, TdVariants V, uint32_t k, TdTop P,
-                                                       void *__restrict__ fout_v, uint32_t *__restrict__ cnt) {
+                                                       void *__restrict__ fout_v, uint32_t *__restrict__ cnt,
+                                                       uint32_t zero_n) {
     __shared__ uint32_t fa[TOP_F], fb[TOP_F];
     __shared__ uint32_t s_n[2], sapp[17];
     __shared__ uint64_t s_vn[TD_MAX_VARIANTS];
     const uint32_t tid = threadIdx.x;
     if (tid < TD_MAX_VARIANTS) s_vn[tid] = reinterpret_cast<uint64_t>(V.nodes[tid]);
     if (tid < 2) s_n[tid] = 0;
+    // the walk's counters cnt[0 .. zero_n) zeroed here instead of by a fill launch before this one (the
+    // barrier below waits for the stores before any count is added to)
+    for (uint32_t i = tid; i < zero_n; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const u4v_t g_u4c;
@@ -1393,10 +1421,11 @@ void launch_pack_entries(const uint64_t *ent, uint64_t m, int pb, uint64_t *key,
 
 void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st,
-                         uint32_t *gate, uint32_t word, uint64_t level_count, uint32_t *bm) {
+                         uint32_t *gate, uint32_t word, uint64_t level_count, uint32_t *bm, const uint32_t *scr,
+                         const TdScreen &SC) {
     const uint64_t blocks = std::min<uint64_t>(ceil_div(max_desc ? max_desc : 1, (uint64_t)TD_THREADS * JU), 2048);
     hipLaunchKernelGGL(k_topdown_jump_u, dim3((uint32_t)blocks), dim3(TD_THREADS), 0, st, ca, cb, desc_count, k, fin, nin,
-                       fout, nout, gate, word, level_count, bm);
+                       fout, nout, gate, word, level_count, bm, scr, SC);
     MKV_LAUNCH_CHECK();
 }
 void launch_topdown_jump_sh(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, uint64_t a_par,
@@ -1418,9 +1447,9 @@ void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t 
 }
 
 void launch_topdown_top(const uint8_t *na, const TdVariants &V, uint32_t k, const TdTop &P, void *fout, bool wide,
-                        uint32_t *cnt, hipStream_t st) {
-    if (wide) hipLaunchKernelGGL(k_topdown_top<true>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt);
-    else hipLaunchKernelGGL(k_topdown_top<false>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt);
+                        uint32_t *cnt, hipStream_t st, uint32_t zero_n) {
+    if (wide) hipLaunchKernelGGL(k_topdown_top<true>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt, zero_n);
+    else hipLaunchKernelGGL(k_topdown_top<false>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt, zero_n);
     MKV_LAUNCH_CHECK();
 }
 
@@ -1540,6 +1569,42 @@ __global__ void k_tail_fixed_dev(const uint64_t *__restrict__ refs, const uint32
     }
 }
 
+// The same for the mapped pinned block, one thread per 16-B granule of the output: every store
+// instruction of a wave covers 1 KiB of consecutive host addresses (a thread per key stored 16 B at a
+// 32-B stride, twice), so the PCIe writes leave in full lines. klen % 16 == 0, out 16-B aligned.
+__global__ void k_tail_fixed_g16(const uint64_t *__restrict__ refs, const uint32_t *__restrict__ mdev, uint64_t cap_m,
+                                 uint64_t cap_b, DiffSide A, DiffSide B, int check, uint32_t *__restrict__ nbad,
+                                 uint32_t klen, uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+    const uint64_t m = *mdev;
+    const bool fits = m <= cap_m && m * klen <= cap_b;
+    const uint32_t gpk = klen >> 4;
+    const uint64_t end = m > cap_m + 1 ? m : cap_m + 1;
+    const uint64_t G = fits ? m * gpk : 0;
+    const uint64_t tot = G > end ? G : end, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += stride) {
+        if (t < end) {
+            if (t <= cap_m) off[t] = (t < m ? t : m) * klen;
+            if (t < m && check && !key_eq_at(A, B, refs[t])) atomicAdd(nbad, 1u);
+        }
+        if (t < G) {
+            const uint64_t k = t / gpk, x = t - k * gpk;
+            uint64_t len;
+            const uint8_t *src = key_at(A, refs[k], &len) + 16 * x;
+            uint4 v;
+            if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+                v = *reinterpret_cast<const uint4 *>(src);
+            } else {
+                uint32_t w[4];
+                for (int j = 0; j < 4; ++j)
+                    w[j] = (uint32_t)src[4 * j] | ((uint32_t)src[4 * j + 1] << 8) | ((uint32_t)src[4 * j + 2] << 16) |
+                           ((uint32_t)src[4 * j + 3] << 24);
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            *reinterpret_cast<uint4 *>(out + 16 * t) = v;
+        }
+    }
+}
+
 void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
                           uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen,
@@ -1549,8 +1614,13 @@ void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const Diff
         // the key bytes straight into the mapped pinned block, no device staging + copy kernel (round 6: 100M
         // value-only diff 0.185 -> 0.172 ms device; the gather's random reads now overlap the PCIe writes of
         // other workgroups instead of preceding one streaming copy)
-        hipLaunchKernelGGL(k_tail_fixed_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)), dim3(256),
-                           0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, klen, off, dkeys);
+        if (klen % 16 == 0 && klen < (1u << 20) && (reinterpret_cast<uintptr_t>(dkeys) & 15) == 0)
+            hipLaunchKernelGGL(k_tail_fixed_g16,
+                               dim3((uint32_t)std::min<uint64_t>(ceil_div(std::max(cap_m + 1, cap_m * (klen / 16)), 256), 2048)),
+                               dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, (uint32_t)klen, off, dkeys);
+        else
+            hipLaunchKernelGGL(k_tail_fixed_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)),
+                               dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, klen, off, dkeys);
         MKV_LAUNCH_CHECK();
         return;
     }

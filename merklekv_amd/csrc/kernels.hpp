@@ -229,6 +229,14 @@ void launch_topdown_level(const uint8_t *ca, const uint8_t *cb, uint64_t child_c
 // *count += sampled positions whose sorted key prefixes differ (key-set screen for the top-down walk).
 void launch_sample_pfx(const uint64_t *pa, const uint64_t *pb, uint64_t n, uint32_t samples, uint32_t *count,
                        hipStream_t st);
+// The screen inside a jump (launch_topdown_jump SC): min(n, 256 x TD_SCREEN_SLOTS) samples into
+// TD_SCREEN_SLOTS words (plain stores, so no zeroing), read by a later gated jump (scr).
+constexpr int TD_SCREEN_SLOTS = 16;
+struct TdScreen {
+    const uint64_t *pa, *pb;
+    uint64_t n;
+    uint32_t *slots;  // nullptr: no screen in this jump
+};
 // check == false: the caller knows both key sequences are equal (same key-set id): refs only.
 void launch_topdown_leaves(const uint64_t *pos, uint64_t m, const DiffSide &A, const DiffSide &B, bool check, uint64_t *refs,
                            uint32_t *nbad, hipStream_t st);
@@ -273,8 +281,9 @@ struct TdTop {
     uint32_t T[MKV_MAXLEV_TD];
     uint32_t nt;  // jumps T[0] -> ... -> T[nt]
 };
+// zero_n: cnt[0 .. zero_n) zeroed by the kernel first (no fill launch before it).
 void launch_topdown_top(const uint8_t *na, const TdVariants &V, uint32_t k, const TdTop &P, void *fout, bool wide,
-                        uint32_t *cnt, hipStream_t st);
+                        uint32_t *cnt, hipStream_t st, uint32_t zero_n = 0);
 // Jump k levels down from divergent parents (unsharded plans): fout gets every divergent descendant
 // at the target level (desc_count nodes there). max_desc: upper bound on parents << k (grid sizing).
 // gate: the one-wait pair diff's level-4 abort test folded into the jump from level 4 (k_td_gate's rule on
@@ -282,7 +291,8 @@ void launch_topdown_top(const uint8_t *na, const TdVariants &V, uint32_t k, cons
 // divergent position's bit there (zeroed bitmap; positions_sorted_bitmap_dev then skips its set pass).
 void launch_topdown_jump(const uint8_t *ca, const uint8_t *cb, uint64_t desc_count, int k, const uint32_t *fin,
                          const uint32_t *nin, uint32_t *fout, uint32_t *nout, uint64_t max_desc, hipStream_t st,
-                         uint32_t *gate = nullptr, uint32_t word = 0, uint64_t level_count = 0, uint32_t *bm = nullptr);
+                         uint32_t *gate = nullptr, uint32_t word = 0, uint64_t level_count = 0, uint32_t *bm = nullptr,
+                         const uint32_t *scr = nullptr, const TdScreen &SC = TdScreen{});
 // Sharded plans: the frontier holds local indices of level l (global = local + a_par), descendants are
 // addressed at level l - k as global - a_desc; seeds = a shard's fringe roots at levels lt..l (owned nodes
 // whose parent is not owned), each compared through its span of level-lt descendants starting at first[i].

@@ -2505,7 +2505,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     const uint64_t n = a->n;
     uint32_t *f0 = ens<uint32_t>(t->td_f0, n + 2);
     uint32_t *f1 = ens<uint32_t>(t->td_f1, n + 2);
-    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2);
+    uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2 + TD_SCREEN_SLOTS);  // + the screen's slots
     if (!t->tail_cap_m) {
         t->tail_cap_m = std::max<uint64_t>(TAIL_MIN_KEYS, n / 1024);
         t->tail_cap_b = 48 * t->tail_cap_m;
@@ -2532,19 +2532,30 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     const uint8_t *na = a->nodes.as<uint8_t>(), *nb = b->nodes.as<uint8_t>();
     uint32_t *fin = f0, *fout = f1;
     const bool sh = a->sharded;  // same plan: b is sharded the same way
-    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
-    // (one 1,024-thread workgroup zeroing and sampling in a single launch measured slower: 0.238 vs 0.231 ms;
-    // round 6: inside the one-workgroup top as well, 0.187-0.194 vs 0.172 ms — one CU's few thousand random
-    // prefix reads are slower than 16 workgroups' — and the landing jump adding each divergent leaf to its
-    // position block's count, so no count pass: 0.193 vs 0.187 ms)
-    launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
+    // below level 8 the jumps land on every second level: near the leaves the frontier holds about one node
+    // per divergent leaf, and two 2-level jumps read half the bytes of one 4-level jump (100M value-only:
+    // 0.170 -> 0.161 ms device)
+    const std::vector<size_t> T = jump_targets(L, true);
+    TdTop P;
+    const size_t nt = sh ? 0 : top_jumps(a, T, 1, &P);
+    const bool gated = L > TD_CHECK_LEVEL + 2;  // the walk has a jump from level 4 (the abort test rides on it)
+    // Unsharded, with a one-workgroup top that ends above level 4: the top zeroes the counters itself and the
+    // first jump after it takes the key-set screen, into slots the gated jump reads. Round 6: the fill and
+    // the screen had been two launches in front of the top (~12 us of the call); the screen on the aux stream
+    // beside the top measured slower (0.164 vs 0.161 ms device: the cross-stream event pair).
+    const bool fast_head = !sh && nt && gated && T[nt] > TD_CHECK_LEVEL;
+    if (!fast_head) {
+        MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
+        // (one 1,024-thread workgroup zeroing and sampling in a single launch measured slower: 0.238 vs 0.231
+        // ms; round 6: inside the one-workgroup top as well, 0.187-0.194 vs 0.172 ms — one CU's few thousand
+        // random prefix reads are slower than 16 workgroups' — and the landing jump adding each divergent
+        // leaf to its position block's count, so no count pass: 0.193 vs 0.187 ms)
+        launch_sample_pfx(A.pfx, B.pfx, n, 4096, cnt + L + 1, t->st);
+    }
     // the position bitmap is all-zero between calls; zeroed here (grown) before the jump that lands on the
     // leaves sets its bits
     if (t->td_bm_words < words) MKV_HIP(hipMemsetAsync(bm, 0, (words + 4) * 4, t->st));
     t->td_bm_words = 0;  // until the emit pass has been queued (it leaves the bitmap zero)
-    const std::vector<size_t> T = jump_targets(L);
-    TdTop P;
-    const size_t nt = sh ? 0 : top_jumps(a, T, 1, &P);
     t->walk_jumps.clear();  // mkv_tree_walk_stats describes this walk (one variant)
     t->walk_L = (uint32_t)L;
     t->walk_k = 1;
@@ -2554,7 +2565,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         if (nt) {  // the roots and the first nt jumps in one workgroup
             TdVariants V{};
             V.nodes[0] = nb;
-            launch_topdown_top(na, V, 1, P, fout, false, cnt, t->st);
+            launch_topdown_top(na, V, 1, P, fout, false, cnt, t->st, fast_head ? (uint32_t)L + 2 : 0u);
             for (size_t q = 1; q <= nt; ++q) t->walk_jumps.emplace_back((uint32_t)T[q - 1], (uint32_t)T[q]);
             t->walk_fused = (uint32_t)nt;
             q0 = nt + 1;
@@ -2570,11 +2581,12 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
         const uint64_t maxd = std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40);
         // the level-4 abort test rides on the jump from level 4 (no launch of its own)
-        const bool gate = l == TD_CHECK_LEVEL && L > TD_CHECK_LEVEL + 2;
+        const bool gate = l == TD_CHECK_LEVEL && gated;
         if (!sh) {
+            const TdScreen SC{A.pfx, B.pfx, n, fast_head && q == q0 ? cnt + L + 2 : nullptr};
             launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
                                 cnt + lt, maxd, t->st, gate ? cnt : nullptr, (uint32_t)L + 1, a->lev_cnt[l],
-                                lt == 0 ? bm : nullptr);
+                                lt == 0 ? bm : nullptr, gate && fast_head ? cnt + L + 2 : nullptr, SC);
         } else {
             if (gate) launch_td_gate(cnt, (uint32_t)L + 1, (uint32_t)l, a->lev_cnt[l], t->st);
             launch_topdown_jump_sh(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, a->lev_base[l],

@@ -526,6 +526,31 @@ def test_topdown_equal_count_key_swap_falls_back(oracle_lib):
     assert b.diff_keys_bytes(a) == ob.diff(oa)
 
 
+@pytest.mark.parametrize("n", [100, 5_000, 300_000])
+def test_topdown_screen_every_position_shifted(oracle_lib, n):
+    """Equal counts, the largest key replaced by one that sorts first: every sorted position shifts, so the
+    key-set screen (sampled prefixes, beside the walk's top) stops the walk at its gated jump — or, for
+    trees too small for one, the leaf-key check does — and the merge-join answers. Twice per handle (the
+    screen's slots are rewritten, never zeroed), then a value-only diff on the same handle."""
+    kb, ko, vb, vo = oracle_lib.gen_records(DEFAULT_SEED + 31, 0, n)
+    keys, vals = split_blob(kb, ko), split_blob(vb, vo)
+    keys2 = list(keys)
+    last = max(range(n), key=lambda i: keys[i])
+    keys2[last] = b"\x00" + keys2[last][1:]
+    a, b = MerkleTree(), MerkleTree()
+    a.build(keys, vals)
+    b.build(keys2, vals)
+    oa = oracle_lib.OracleTree.from_pairs(list(zip(keys, vals)))
+    ob = oracle_lib.OracleTree.from_pairs(list(zip(keys2, vals)))
+    for _ in range(2):
+        assert a.diff_keys_bytes(b) == oa.diff(ob)
+    vals3 = list(vals)
+    vals3[n // 3] = b"changed"
+    c = MerkleTree()
+    c.build(keys, vals3)
+    assert a.diff_keys_bytes(c) == [keys[n // 3]]
+
+
 @pytest.mark.parametrize("klen", [12, 37, 60, 64, 90])
 def test_topdown_key_tail_change_falls_back(klen):
     """Equal counts and 8-byte prefixes; one key differs only in its last byte (aligned and unaligned
