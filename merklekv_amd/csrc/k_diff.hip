@@ -878,7 +878,8 @@ __global__ __launch_bounds__(TD_THREADS) void k_topdown_jump_u(const uint8_t *__
         for (uint32_t sl = blockIdx.x; sl < TD_SCREEN_SLOTS; sl += gridDim.x, ++j) {
             const uint32_t q = sl * 256 + threadIdx.x;
             if (threadIdx.x < 256 && q < samples) {
-                const uint64_t i = samples > 1 ? (uint64_t)((unsigned __int128)q * (SC.n - 1) / (samples - 1)) : 0;
+                // 64-bit (q < 2^12, n < 2^48); the 128-bit division of k_sample_pfx cost a jump ~6 us
+                const uint64_t i = samples > 1 ? (uint64_t)q * (SC.n - 1) / (samples - 1) : 0;
                 sbad |= (uint32_t)(SC.pa[i] != SC.pb[i]) << j;
             }
         }
@@ -1574,9 +1575,18 @@ __global__ void k_tail_fixed_dev(const uint64_t *__restrict__ refs, const uint32
 // 32-B stride, twice), so the PCIe writes leave in full lines. klen % 16 == 0, out 16-B aligned.
 __global__ void k_tail_fixed_g16(const uint64_t *__restrict__ refs, const uint32_t *__restrict__ mdev, uint64_t cap_m,
                                  uint64_t cap_b, DiffSide A, DiffSide B, int check, uint32_t *__restrict__ nbad,
-                                 uint32_t klen, uint64_t *__restrict__ off, uint8_t *__restrict__ out) {
+                                 uint32_t klen, uint64_t *__restrict__ off, uint8_t *__restrict__ out,
+                                 uint64_t *__restrict__ hsmall) {
     const uint64_t m = *mdev;
     const bool fits = m <= cap_m && m * klen <= cap_b;
+    // hsmall: the call's scalars go to the host from here, no copy launch after this one — the count, the key
+    // bytes and the walk's screen / abort word are final when it starts (block 0 stores them); a leaf-key
+    // mismatch found here stores 1 into hsmall[3] (zeroed by the host before the call)
+    if (hsmall && blockIdx.x == 0 && threadIdx.x == 0) {
+        hsmall[0] = m;
+        hsmall[1] = *nbad;
+        hsmall[2] = (m < cap_m ? m : cap_m) * klen;
+    }
     const uint32_t gpk = klen >> 4;
     const uint64_t end = m > cap_m + 1 ? m : cap_m + 1;
     const uint64_t G = fits ? m * gpk : 0;
@@ -1584,7 +1594,10 @@ __global__ void k_tail_fixed_g16(const uint64_t *__restrict__ refs, const uint32
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += stride) {
         if (t < end) {
             if (t <= cap_m) off[t] = (t < m ? t : m) * klen;
-            if (t < m && check && !key_eq_at(A, B, refs[t])) atomicAdd(nbad, 1u);
+            if (t < m && check && !key_eq_at(A, B, refs[t])) {
+                atomicAdd(nbad, 1u);
+                if (hsmall) hsmall[3] = 1;
+            }
         }
         if (t < G) {
             const uint64_t k = t / gpk, x = t - k * gpk;
@@ -1605,24 +1618,26 @@ __global__ void k_tail_fixed_g16(const uint64_t *__restrict__ refs, const uint32
     }
 }
 
-void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
+bool launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
                           uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen,
-                          bool host_offsets) {
+                          bool host_offsets, uint64_t *hsmall) {
     const dim3 g((uint32_t)std::min<uint64_t>(ceil_div(cap_m, 256), 2048));
     if (klen && host_offsets) {
         // the key bytes straight into the mapped pinned block, no device staging + copy kernel (round 6: 100M
         // value-only diff 0.185 -> 0.172 ms device; the gather's random reads now overlap the PCIe writes of
         // other workgroups instead of preceding one streaming copy)
-        if (klen % 16 == 0 && klen < (1u << 20) && (reinterpret_cast<uintptr_t>(dkeys) & 15) == 0)
+        const bool g16 = klen % 16 == 0 && klen < (1u << 20) && (reinterpret_cast<uintptr_t>(dkeys) & 15) == 0;
+        if (g16)
             hipLaunchKernelGGL(k_tail_fixed_g16,
                                dim3((uint32_t)std::min<uint64_t>(ceil_div(std::max(cap_m + 1, cap_m * (klen / 16)), 256), 2048)),
-                               dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, (uint32_t)klen, off, dkeys);
+                               dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, (uint32_t)klen, off, dkeys,
+                               hsmall);
         else
             hipLaunchKernelGGL(k_tail_fixed_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)),
                                dim3(256), 0, st, refs, mdev, cap_m, cap_b, A, B, (int)check, nbad, klen, off, dkeys);
         MKV_LAUNCH_CHECK();
-        return;
+        return g16 && hsmall;
     }
     if (klen) {  // every key of both trees has length klen: check, offsets and key bytes in one launch
         hipLaunchKernelGGL(k_tail_fixed_dev, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap_m + 1, 256), 2048)), dim3(256),
@@ -1637,6 +1652,7 @@ void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const Diff
     hipLaunchKernelGGL(k_tail_copy_dev, dim3((uint32_t)cb), dim3(256), 0, st, off, kout, mdev, cap_m, cap_b, doff, dkeys,
                        (int)!(klen && host_offsets));
     MKV_LAUNCH_CHECK();
+    return false;
 }
 
 }  // namespace mkv

@@ -254,10 +254,13 @@ void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const
 // (fixed-length keys): the host writes the offsets k x klen into doff's block itself; only the key bytes
 // cross PCIe.
 void launch_td_gate(uint32_t *cnt, uint32_t word, uint32_t level, uint64_t level_count, hipStream_t st);
-void launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
+// hsmall (optional, mapped pinned): the fixed-length form into host memory also stores the call's scalars —
+// hsmall[0] = count, [1] = *nbad as it stands before the key check, [2] = key bytes, [3] = 1 on a leaf-key
+// mismatch (the caller zeroes [3] first). Returns whether it did.
+bool launch_diff_tail_dev(const uint64_t *refs, const uint32_t *mdev, const DiffSide &A, const DiffSide &B, bool check,
                           uint32_t *nbad, uint64_t cap_m, uint64_t cap_b, uint64_t *lens, uint64_t *off, void *scan_scr,
                           uint8_t *kout, uint8_t *doff, uint8_t *dkeys, hipStream_t st, uint64_t klen = 0,
-                          bool host_offsets = false);
+                          bool host_offsets = false, uint64_t *hsmall = nullptr);
 // Batched top-down walk (one base vs up to TD_MAX_VARIANTS trees with the same level plan).
 constexpr int TD_MAX_VARIANTS = 64;
 constexpr int MKV_MAXLEV_TD = 48;  // = MKV_MAXLEV (levels of a tree)

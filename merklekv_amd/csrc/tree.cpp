@@ -2540,9 +2540,13 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     const size_t nt = sh ? 0 : top_jumps(a, T, 1, &P);
     const bool gated = L > TD_CHECK_LEVEL + 2;  // the walk has a jump from level 4 (the abort test rides on it)
     // Unsharded, with a one-workgroup top that ends above level 4: the top zeroes the counters itself and the
-    // first jump after it takes the key-set screen, into slots the gated jump reads. Round 6: the fill and
-    // the screen had been two launches in front of the top (~12 us of the call); the screen on the aux stream
-    // beside the top measured slower (0.164 vs 0.161 ms device: the cross-stream event pair).
+    // jump landing on level 4 (a full grid: 16 of its workgroups sample beside their walk work) takes the
+    // key-set screen, into slots the gated jump reads. Round 6: the fill and the screen had been two launches
+    // in front of the top (~12 us of the call); the screen on the aux stream beside the top measured slower
+    // (0.164 vs 0.161 ms device: the cross-stream event pair), inside the first jump after the top (12
+    // workgroups) it added ~3 us to that jump. (Also tried: the key tail's last workgroup writing the call's
+    // scalars instead of k_copy_small_many — a device-scope fence + arrival atomic per workgroup, 0.177 vs
+    // 0.153 ms; its first workgroup stores them instead, below.)
     const bool fast_head = !sh && nt && gated && T[nt] > TD_CHECK_LEVEL;
     if (!fast_head) {
         MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2) * 4, t->st));
@@ -2583,7 +2587,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         // the level-4 abort test rides on the jump from level 4 (no launch of its own)
         const bool gate = l == TD_CHECK_LEVEL && gated;
         if (!sh) {
-            const TdScreen SC{A.pfx, B.pfx, n, fast_head && q == q0 ? cnt + L + 2 : nullptr};
+            const TdScreen SC{A.pfx, B.pfx, n, fast_head && lt == TD_CHECK_LEVEL ? cnt + L + 2 : nullptr};
             launch_topdown_jump(na + 32 * a->lev_off[lt], nb + 32 * b->lev_off[lt], a->lev_cnt[lt], k, fin, cnt + l, fout,
                                 cnt + lt, maxd, t->st, gate ? cnt : nullptr, (uint32_t)L + 1, a->lev_cnt[l],
                                 lt == 0 ? bm : nullptr, gate && fast_head ? cnt + L + 2 : nullptr, SC);
@@ -2597,9 +2601,11 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     }
     positions_sorted_bitmap_dev(fin, cnt, n, bm, bc, refs, t->st, !sh);  // side-A refs = sorted positions
     t->td_bm_words = words;
-    launch_diff_tail_dev(refs, cnt, A, B, !same_keyset(a, b), cnt + L + 1, cap_m, cap_b, lens, off, scr, kout, blk->dp,
-                         blk->dp + kpos, t->st, klen, klen != 0);
-    {  // one launch: divergent positions, screen / abort / leaf-key mismatches, key bytes (when m <= cap_m)
+    t->h_small[3] = 0;  // the key tail's mismatch flag (its kernels of earlier calls have completed)
+    const bool scalars = launch_diff_tail_dev(refs, cnt, A, B, !same_keyset(a, b), cnt + L + 1, cap_m, cap_b, lens, off,
+                                              scr, kout, blk->dp, blk->dp + kpos, t->st, klen, klen != 0,
+                                              reinterpret_cast<uint64_t *>(t->h_small_dev));
+    if (!scalars) {  // one launch: divergent positions, screen / abort / leaf-key mismatches, key bytes (when m <= cap_m)
         SmallCopies SC{};
         const uint8_t *srcs[3] = {reinterpret_cast<const uint8_t *>(cnt), reinterpret_cast<const uint8_t *>(cnt + L + 1),
                                   reinterpret_cast<const uint8_t *>(off + cap_m)};
@@ -2617,7 +2623,7 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
     if (klen) blk->fill_offsets(klen, cap_m + 1);  // while the device works
     sync(t);
     const uint64_t m = (uint32_t)t->h_small[0];
-    const uint32_t word = (uint32_t)t->h_small[1];
+    const uint32_t word = (uint32_t)t->h_small[1] | (t->h_small[3] ? 1u : 0u);
     const uint64_t bytes = t->h_small[2];
     if (word != 0) {
         *fallback = 1;
