@@ -497,7 +497,10 @@ __global__ void k_widen_positions(const uint32_t *__restrict__ f, uint64_t m, ui
 // bitmap that is all-zero between calls; per-block popcounts over POS_BLOCK_WORDS words; each emitting
 // block finds its output base by summing the counts of the blocks before it (at most a few thousand
 // u32, L2-resident), scans its own words and writes the positions, clearing the words it read.
-constexpr uint32_t POS_BLOCK_WORDS = 1024;  // 256 threads x 4 words
+// Round 6: 16 consecutive words per thread (4 uint4 loads in flight; 4x fewer blocks for the base sums):
+// 100M value-only diff 0.151 -> 0.149 ms device (interleaved A/B)
+constexpr uint32_t POS_TW = 16;                         // words per thread
+constexpr uint32_t POS_BLOCK_WORDS = 256 * POS_TW;
 constexpr uint64_t POS_MAX_BLOCKS = 8192;   // beyond this the O(blocks^2) base sums lose to the sort
 
 __global__ void k_pos_setbits(const uint32_t *__restrict__ f, uint64_t m, uint32_t *__restrict__ bm) {
@@ -532,12 +535,23 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t pos_load(const uint32_t *bm, uint64_t w0, uint64_t words, uint32_t x[POS_TW]) {
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < POS_TW / 4; ++j) {
+        const uint4 v = pos_words(bm, w0 + 4 * j, words);
+        x[4 * j] = v.x, x[4 * j + 1] = v.y, x[4 * j + 2] = v.z, x[4 * j + 3] = v.w;
+        c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+    }
+    return c;
+}
+
 __global__ __launch_bounds__(256) void k_pos_count(const uint32_t *__restrict__ bm, uint64_t words,
                                                    uint32_t *__restrict__ bc) {
     __shared__ uint32_t red[4];
-    const uint64_t w0 = (uint64_t)blockIdx.x * POS_BLOCK_WORDS + 4 * threadIdx.x;
-    const uint4 x = pos_words(bm, w0, words);
-    const uint32_t c = wave_sum(__popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w));
+    const uint64_t w0 = (uint64_t)blockIdx.x * POS_BLOCK_WORDS + POS_TW * threadIdx.x;
+    uint32_t x[POS_TW];
+    const uint32_t c = wave_sum(pos_load(bm, w0, words, x));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
     __syncthreads();
     if (threadIdx.x == 0) bc[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
@@ -550,9 +564,9 @@ __global__ __launch_bounds__(256) void k_pos_emit(uint32_t *__restrict__ bm, uin
     uint32_t s = 0;
     for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) s += bc[i];
     s = wave_sum(s);
-    const uint64_t w0 = (uint64_t)blockIdx.x * POS_BLOCK_WORDS + 4 * threadIdx.x;
-    const uint4 x = pos_words(bm, w0, words);
-    const uint32_t c = __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    const uint64_t w0 = (uint64_t)blockIdx.x * POS_BLOCK_WORDS + POS_TW * threadIdx.x;
+    uint32_t x[POS_TW];
+    const uint32_t c = pos_load(bm, w0, words, x);
     uint32_t v = c;  // inclusive scan over the wave
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -565,20 +579,23 @@ __global__ __launch_bounds__(256) void k_pos_emit(uint32_t *__restrict__ bm, uin
     uint64_t o = (uint64_t)base_w[0] + base_w[1] + base_w[2] + base_w[3] + (v - c);
     for (uint32_t w = 0; w < wave; ++w) o += tot_w[w];
     if (!c) return;
-    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        uint32_t b = xs[q];
+    for (uint32_t q = 0; q < POS_TW; ++q) {
+        uint32_t b = x[q];
         while (b) {
             out[o++] = (w0 + q) * 32 + (uint32_t)(__ffs(b) - 1);
             b &= b - 1;
         }
     }
-    if (w0 + 3 < words) {
-        *reinterpret_cast<uint4 *>(bm + w0) = make_uint4(0, 0, 0, 0);
-    } else {
-        for (int q = 0; q < 4; ++q)
-            if (w0 + q < words) bm[w0 + q] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < POS_TW / 4; ++j) {
+        const uint64_t wj = w0 + 4 * j;
+        if (wj + 3 < words) {
+            *reinterpret_cast<uint4 *>(bm + wj) = make_uint4(0, 0, 0, 0);
+        } else {
+            for (int q = 0; q < 4; ++q)
+                if (wj + q < words) bm[wj + q] = 0;
+        }
     }
 }
 
@@ -2835,7 +2852,7 @@ static mkv_keylist *diff_pair(const mkv_tree *a, const mkv_tree *b, DevKeys *dev
     bool done = false;
     const uint64_t nwords = (A.n + 31) / 32;
     if (!dev && A.n > 0 && same_plan(a, b) && !keysets_differ(a, b) && a->sharded == b->sharded && a->lev_S.size() > 1 &&
-        ceil_div(nwords, 1024) <= 8192) {
+        ceil_div(nwords, POS_BLOCK_WORDS) <= POS_MAX_BLOCKS) {
         int fb = 0;
         mkv_keylist *l = topdown_pair_onewait(t, a, b, A, B, refs, &fb, &m);
         HTRACE("topdown-done");

@@ -1,4 +1,4 @@
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py tests/test_update_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r06x_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r06x_pytest.log; [ $rc -eq 0 ] || exit $rc
-LIBS="head=abl/head/lib/libmerklekv_hip.so new= fine=abl/fine/lib/libmerklekv_hip.so" REPS=3 TAILC=120 CMD="python tools/ab_diff.py" bash scripts/gpu_ab.sh > /dev/null
+LIBS="prev=abl/prev/lib/libmerklekv_hip.so new=" REPS=3 TAILC=120 CMD="python tools/ab_diff.py" bash scripts/gpu_ab.sh > /dev/null
 grep -H "vo-diff" gpurun_out/ab/*_[123].log
