@@ -793,7 +793,7 @@ void plan_levels(mkv_tree *t, uint64_t o, uint64_t n, uint64_t N) {
         t->lev_cnt.push_back(c);
         t->lev_off.push_back(off);
         t->lev_S.push_back(S);
-        off += c;
+        off = (off + c + 3) & ~uint64_t(3);  // every level 128-B aligned: a 2- or 4-child group is whole lines
         if (S == 1) break;
         uint64_t a2 = (a + 1) / 2;
         uint64_t e2 = (e == S) ? (e + 1) / 2 : e / 2;
@@ -803,11 +803,12 @@ void plan_levels(mkv_tree *t, uint64_t o, uint64_t n, uint64_t N) {
     }
 }
 
+// Node slots the level plan spans (levels start 128-B aligned, so a few pad slots between them).
 uint64_t total_nodes(const mkv_tree *t) {
-    uint64_t s = 0;
-    for (auto c : t->lev_cnt) s += c;
-    return s;
+    return t->lev_off.empty() ? 0 : t->lev_off.back() + t->lev_cnt.back();
 }
+// Node slots to allocate for an unsharded tree of n leaves: 2n - 1 nodes + up to 3 pad slots per level.
+static uint64_t node_slots(uint64_t n) { return 2 * n + 4 * MKV_MAXLEV + 66; }
 
 // gperm/gdig: fuse the sorted-leaf gather (nodes[c] = dig[perm[c]]) into the first launch. Leaves whose
 // parent is not owned (at most the first and the last of a shard) are gathered directly; a plan without
@@ -1198,7 +1199,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     }
     // leaf level = nodes[0 .. n). Every level is stored, promoted nodes included, so the tree holds
     // sum_l ceil(n/2^l) <= 2n + L nodes (L <= 64 levels).
-    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * (2 * n + 66));
+    uint8_t *nodes = ens<uint8_t>(t->nodes, 32 * node_slots(n));
     t->gather_pending = defer_gather;
     if (!defer_gather) {
         size_t pg = prof_begin(t, "gather");
@@ -1496,7 +1497,7 @@ mkv_status mkv_tree_clone(const mkv_tree *src, mkv_tree *dst) {
         uint32_t *pm = ens<uint32_t>(dst->perm, src->n + 1);
         uint64_t *pf = ens<uint64_t>(dst->pfx, src->n + 1);
         ++dst->pfx_gen;
-        uint8_t *nd = ens<uint8_t>(dst->nodes, 32 * (2 * src->n + 66));
+        uint8_t *nd = ens<uint8_t>(dst->nodes, 32 * std::max(node_slots(src->n), total_nodes(src) + 2));
         if (src->kbytes) MKV_HIP(hipMemcpyAsync(kb, src->kb.p, src->kbytes, hipMemcpyDeviceToDevice, dst->st));
         if (src->koff.p)
             MKV_HIP(hipMemcpyAsync(ko, src->koff.p, (src->nstore + 1) * 8, hipMemcpyDeviceToDevice, dst->st));
@@ -1684,7 +1685,7 @@ static void merge_batch(mkv_tree *t, const mkv_blob &keys, const mkv_blob *value
     if (t->nstore + nb >= 0xFFFFFFF0ull) throw Error(ST_EINVAL, "too many stored key records");
     uint64_t *npfx = ens<uint64_t>(t->m_pfx, M + 1);
     uint32_t *nperm = ens<uint32_t>(t->m_perm, M + 1);
-    uint8_t *nnodes = ens<uint8_t>(t->m_nodes, 32 * (2 * M + 66));
+    uint8_t *nnodes = ens<uint8_t>(t->m_nodes, 32 * node_slots(M));
     uint64_t *cnt = ens<uint64_t>(t->m_cnt, 4);
     void *scr = t->d_diffscr.ensure(umerge_scratch_bytes(M));
     size_t pm = prof_begin(t, "merge");
