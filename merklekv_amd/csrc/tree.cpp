@@ -2917,11 +2917,15 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     const uint64_t cap = (L > TD_CHECK_LEVEL + 2 ? k * n / 2 : k * n) + 2ull * k + 64;
     uint64_t *f0 = ens<uint64_t>(t->tb_f0, cap), *f1 = ens<uint64_t>(t->tb_f1, cap);
     uint32_t *cnt = ens<uint32_t>(t->td_cnt, L + 2 + 2 * k);  // per level; then nbad[k], count[k]
-    MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2 + 2 * k) * 4, t->st));
     const uint8_t *na = a->nodes.as<uint8_t>();
     uint64_t *fin = f0, *fout = f1;
     bool sharded = a->sharded;
     for (auto *v : vs) sharded |= v->sharded;
+    const std::vector<size_t> T = jump_targets(L, true);
+    TdTop P;
+    const size_t nt = !sharded && L > 1 ? top_jumps(a, T, k, &P) : 0;
+    // with a one-workgroup top the counters are zeroed by it (no fill launch in front of the walk)
+    if (!nt) MKV_HIP(hipMemsetAsync(cnt, 0, (L + 2 + 2 * k) * 4, t->st));
     t->walk_jumps.clear();
     t->walk_L = (uint32_t)L;
     t->walk_k = k;
@@ -2939,12 +2943,9 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     const size_t pwalk = prof_begin(t, "walk");
     t->walk_fused = 0;
     if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
-        const std::vector<size_t> T = jump_targets(L, true);
-        TdTop P;
-        const size_t nt = top_jumps(a, T, k, &P);
         size_t q0 = 1;
         if (nt) {  // the roots and the first nt jumps in one workgroup
-            launch_topdown_top(na, V, k, P, fout, true, cnt, t->st);
+            launch_topdown_top(na, V, k, P, fout, true, cnt, t->st, (uint32_t)(L + 2 + 2 * k));
             for (size_t q = 1; q <= nt; ++q) t->walk_jumps.emplace_back((uint32_t)T[q - 1], (uint32_t)T[q]);
             t->walk_fused = (uint32_t)nt;
             q0 = nt + 1;
