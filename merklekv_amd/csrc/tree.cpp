@@ -1578,11 +1578,15 @@ static void build_from_staged(mkv_tree *t, const uint8_t *kb, const uint64_t *ko
     uint64_t kcap = 0;
     bool ko_fused = false;
     leaf_hash_owning_keys(t, kb, koff, vb, voff, n, dig, staged, &kcap, &ko_fused);
+    HTRACE("leaf-queued");
     prof_end(t, pl);
     sort_dedup_gather(t, kb, koff, n, nullptr, staged, staged_kbytes, true, kcap, ko_fused);
+    HTRACE("ordered");
     finish_unsharded(t);
+    HTRACE("reduce-queued");
     prof_end(t, ptot);
     sync(t);
+    HTRACE("synced");
 }
 
 mkv_status mkv_tree_build(mkv_tree *t, mkv_blob keys, mkv_blob values) {
@@ -1630,6 +1634,7 @@ mkv_status mkv_tree_build_digests(mkv_tree *t, mkv_blob keys, const uint8_t *dig
 }
 
 mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
+    g_trace.reset();
     MKV_TRY({
         NEED(t, "tree is null");
         NEED(keys.n == values.n, "keys.n != values.n");
@@ -1638,6 +1643,7 @@ mkv_status mkv_tree_build_device(mkv_tree *t, mkv_blob keys, mkv_blob values) {
         DevGuard g(t->dev);
         need_device_blob(keys, "keys");
         need_device_blob(values, "values");
+        HTRACE("validated");
         build_from_staged(t, keys.bytes, keys.offsets, values.bytes, values.offsets, keys.n, false, 0);
     });
 }
