@@ -83,15 +83,13 @@ struct RgRec {
     uint32_t hc;          // head mask of word b1's key bytes (k & 3 of them)
     uint32_t vhl, vtl;    // u32_be(v) split across words b1 / b1 + 1
     uint32_t he, term;    // word b3: kept bytes (L & 3), 0x80 terminator
-    bool live, safe;
+    bool live;
 };
 
 // kmis / vmis: byte misalignment of the key / value blob pointers (the bases are the blobs rounded down to
-// a dword); klo .. vhi: the blobs' dword ranges as offsets from those bases.
-// k1, v1: the low words of the record's end offsets (a record is shorter than 4 GiB).
+// a dword). k1, v1: the low words of the record's end offsets (a record is shorter than 4 GiB).
 __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint32_t k1, uint64_t v0, uint32_t v1, uint32_t r,
-                                        uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi, int64_t vlo,
-                                        int64_t vhi) {
+                                        uint32_t kmis, uint32_t vmis) {
     const uint32_t k = k1 - (uint32_t)k0, v = v1 - (uint32_t)v0;
     const uint32_t c4 = k & 3;
     R.k = k;
@@ -112,10 +110,6 @@ __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint32_t k1, uint
     const uint32_t e4 = R.L & 3;
     R.he = ~(0xFFFFFFFFu >> (8 * e4));
     R.term = 0x80000000u >> (8 * e4);
-    // every source dword a block can load (key run: [ka - 60, ka + 4 b1 + 4], value run:
-    // [va, va + 4 (b3 - b1) + 64)) lies inside the blobs' dword ranges
-    R.safe = R.ka >= klo + 64 && R.ka + 4 * (int64_t)R.b1 + 64 <= khi && R.va >= vlo &&
-             R.va + 4 * (int64_t)(R.b3 - R.b1) + 128 <= vhi;
     R.live = true;
 }
 
@@ -124,10 +118,14 @@ __device__ __forceinline__ void rg_take(RgRec &R, uint64_t k0, uint32_t k1, uint
 // record i is hashed here iff
 //   koff[i] >= koff[0] + 67,  voff[i] >= voff[0] + 6,  koff[i+1] + 68 <= koff[n],  voff[i+1] + 136 <= voff[n]
 // — each test monotone in i, so the records left over are a prefix and a suffix that k_leaf_edges finds by
-// itself (two searches), runs on another stream beside this kernel and needs no list from it. Each test
-// implies its term of rg_take's R.safe (ka <= kmis + k0 and 4 b1 <= 4 + k; va >= vmis + v0 - 6;
-// 4 (b3 - b1) <= v + 7), which stays as a guard: a record that passed the interval test but not R.safe
-// would be left unhashed (a parity failure), never loaded out of bounds.
+// itself (two searches), runs on another stream beside this kernel and needs no list from it. The test
+// keeps every source dword a block loads (key run: [ka - 60, ka + 4 b1 + 4], value run: [va, va + 4 (b3 -
+// b1) + 64), ka / va the dword-aligned starts) inside the blobs' dword ranges [klo, khi) / [vlo, vhi):
+//   ka >= kmis + k0 - 3 >= klo + 64;   ka + 4 b1 + 64 <= kmis + k0 + (4 + k) + 64 = kmis + k1 + 68 <= khi;
+//   va >= vmis + v0 - (k & 3) - 3 >= vmis + voff[0] >= vlo;
+//   va + 4 (b3 - b1) + 128 <= vmis + v0 + (v + 7) + 128 < vmis + v1 + 136 <= vhi
+// (4 b1 <= 4 + k, 4 b1 >= k + 1, 4 b3 <= 8 + k + v). Round 6: this replaced a per-record bounds test kept
+// beside it as a guard (~10 VALU instructions per step: a take runs in most steps of a wave).
 struct RgSplit {
     uint64_t kA, vA, KN, VN;  // koff[0] + 67, voff[0] + 6, koff[n], voff[n]
 };
@@ -135,10 +133,9 @@ __device__ __forceinline__ bool rg_inner(const RgSplit &X, uint64_t k0, uint64_t
     return k0 >= X.kA && v0 >= X.vA && k1 + 68 <= X.KN && v1 + 136 <= X.VN;
 }
 __device__ __forceinline__ void rg_take_or_leave(RgRec &R, uint64_t k0, uint32_t k1, uint64_t v0, uint32_t v1,
-                                                 uint32_t r, uint32_t kmis, uint32_t vmis, int64_t klo, int64_t khi,
-                                                 int64_t vlo, int64_t vhi, const RgSplit &X) {
-    rg_take(R, k0, k1, v0, v1, r, kmis, vmis, klo, khi, vlo, vhi);
-    R.live = R.safe && rg_inner(X, k0, k0 + R.k, v0, v0 + (R.L - 8 - R.k));
+                                                 uint32_t r, uint32_t kmis, uint32_t vmis, const RgSplit &X) {
+    rg_take(R, k0, k1, v0, v1, r, kmis, vmis);
+    R.live = rg_inner(X, k0, k0 + R.k, v0, v0 + (R.L - 8 - R.k));
 }
 
 // The block's positions of the boundary words (block-relative, may lie outside 0..15).
@@ -233,8 +230,6 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     // bases): no source load leaves them
     const uint32_t kmis = (uint32_t)(reinterpret_cast<uintptr_t>(kb) & 3), vmis = (uint32_t)(reinterpret_cast<uintptr_t>(vb) & 3);
     const uint8_t *kbase = kb - kmis, *vbase = vb - vmis;
-    const int64_t klo = (int64_t)((kmis + koff[0]) & ~3ull), khi = (int64_t)((kmis + koff[n] + 3) & ~3ull);
-    const int64_t vlo = (int64_t)((vmis + voff[0]) & ~3ull), vhi = (int64_t)((vmis + voff[n] + 3) & ~3ull);
     const RgSplit X{koff[0] + 67, voff[0] + 6, koff[n], voff[n]};
 
     Q.pnext = rg_grab(ctr, lane);
@@ -291,7 +286,7 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     // stored then, from registers that were loaded a step earlier (a store in the refill itself would wait
     // for the offsets it just requested)
     auto take = [&]() {
-        rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, klo, khi, vlo, vhi, X);
+        rg_take_or_leave(R, nk0, nk1, nv0, nv1, nrec, kmis, vmis, X);
         if (KO.odst) {
             KO.odst[nrec] = nk0;
             if ((uint64_t)nrec + 1 == n) KO.odst[n] = koff[n];
