@@ -291,7 +291,6 @@ struct mkv_tree {
     uint32_t lb_epoch = 0;
     bool sortctl_dirty = true;  // a sort started and did not reach its clearing launch
     bool kc_pending = false;    // the ragged key copy on st3 is not yet joined into st2
-    bool edge_pending = false;  // the edge-record hash on st3 is not yet joined into st2 (before ev_join)
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
     uint32_t walk_fused = 0;  // jumps of the last walk done inside the one-workgroup top launch
     uint64_t hix_skip_gen = 0;  // pfx_gen + 1 of a key set whose hash index did not fit (0: none)
@@ -1172,12 +1171,7 @@ void sort_dedup_gather(mkv_tree *t, const uint8_t *kb, const uint64_t *koff, uin
     // a readback there would hold the host until the gather finishes and delay the reduce launches)
     const uint64_t kbytes = staged_inputs ? staged_kbytes : kb_total;
     const bool keys_done = !staged_inputs && fused_kcap && kbytes + 16 <= fused_kcap;
-    // The reduction on st needs only the sorted order (and the edge records' digests): join here, before
-    // the key copy.
-    if (t->edge_pending) {
-        MKV_HIP(hipStreamWaitEvent(st, t->ev_edge, 0));
-        t->edge_pending = false;
-    }
+    // The reduction on st needs only the sorted order: join here, before the key copy.
     MKV_HIP(hipEventRecord(t->ev_join, st));
     MKV_HIP(hipStreamWaitEvent(t->st, t->ev_join, 0));
     if (t->kc_pending) {  // the ragged key copy (st3) completes before st2 does: the call's sync covers it
@@ -1558,9 +1552,7 @@ static void leaf_hash_owning_keys(mkv_tree *t, const uint8_t *kb, const uint64_t
     MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_in, 0));
     launch_leaf_edges(kb, koff, vb, voff, n, dig, t->st3);
     MKV_HIP(hipEventRecord(t->ev_edge, t->st3));
-    // the reduction reads the edge digests: st2 waits for them after the sort (sort_dedup_gather), so
-    // the tree's stream keeps its one cross-stream wait (ev_join; a second one cost ~5 us there)
-    t->edge_pending = true;
+    MKV_HIP(hipStreamWaitEvent(t->st, t->ev_edge, 0));  // the reduction reads the edge digests
     if (KO.kdst) {
         MKV_HIP(hipStreamWaitEvent(t->st3, t->ev_fixed, 0));
         launch_keycopy_ragged(kb, koff, n, ctr, KO.kdst, KO.kcap, t->st3);
