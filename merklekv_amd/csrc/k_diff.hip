@@ -1017,7 +1017,7 @@ constexpr uint32_t TOP_F = (uint32_t)TD_TOP_MAX_FRONTIER;  // LDS frontier entri
 template <bool WIDE>
 __global__ __launch_bounds__(1024) void k_topdown_top(const uint8_t *__restrict__ na, TdVariants V, uint32_t k, TdTop P,
                                                        void *__restrict__ fout_v, uint32_t *__restrict__ cnt,
-                                                       uint32_t zero_n) {
+                                                       uint32_t zero_n, uint32_t ff_from) {
     __shared__ uint32_t fa[TOP_F], fb[TOP_F];
     __shared__ uint32_t s_n[2], sapp[17];
     __shared__ uint64_t s_vn[TD_MAX_VARIANTS];
@@ -1026,7 +1026,8 @@ __global__ __launch_bounds__(1024) void k_topdown_top(const uint8_t *__restrict_
     if (tid < 2) s_n[tid] = 0;
     // the walk's counters cnt[0 .. zero_n) zeroed here instead of by a fill launch before this one (the
     // barrier below waits for the stores before any count is added to)
-    for (uint32_t i = tid; i < zero_n; i += blockDim.x) cnt[i] = 0;
+    // (words [ff_from, zero_n) get 0xFFFFFFFF instead: the batched walk's per-variant segment starts)
+    for (uint32_t i = tid; i < zero_n; i += blockDim.x) cnt[i] = i < ff_from ? 0u : 0xFFFFFFFFu;
     __syncthreads();
     typedef uint32_t u4v_t __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const u4v_t g_u4c;
@@ -1193,19 +1194,33 @@ __global__ __launch_bounds__(256) void k_vpos_count(const uint32_t *__restrict__
     __syncthreads();
     if (threadIdx.x == 0) bc[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
+// DIRECT: boff holds the per-block counts and each block sums those before it itself (no scan launches;
+// at most VP_DIRECT_BLOCKS blocks, a few thousand L2-resident words each); else boff = their exclusive scan.
+constexpr uint64_t VP_DIRECT_BLOCKS = 8192;
+template <bool DIRECT>
 __global__ __launch_bounds__(256) void k_vpos_emit(uint32_t *__restrict__ bm, uint64_t words,
                                                    const uint32_t *__restrict__ boff, uint64_t n, int pb,
                                                    uint64_t *__restrict__ out) {
-    if (boff[blockIdx.x + 1] == boff[blockIdx.x]) return;  // no entry in this block (its words are zero)
-    __shared__ uint32_t tot_w[4];
+    if (DIRECT ? boff[blockIdx.x] == 0 : boff[blockIdx.x + 1] == boff[blockIdx.x]) return;  // no entry here
+    __shared__ uint32_t tot_w[4], base_w[4];
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t base = 0;
+    if (DIRECT) {
+        uint32_t sb = 0;
+        for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) sb += boff[i];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) sb += __shfl_xor(sb, d);
+        if (lane == 0) base_w[wave] = sb;
+    }
     const uint64_t w0 = (uint64_t)blockIdx.x * VP_WORDS + VP_TW * threadIdx.x;
     uint32_t x[VP_TW];
     const uint32_t c = vp_load(bm, w0, words, x);
     const uint32_t v = wave_incl_scan<uint32_t>(c);
     if (lane == 63) tot_w[wave] = v;
     __syncthreads();
-    uint64_t o = boff[blockIdx.x] + (v - c);
+    if (DIRECT) base = (uint64_t)base_w[0] + base_w[1] + base_w[2] + base_w[3];
+    else base = boff[blockIdx.x];
+    uint64_t o = base + (v - c);
     for (uint32_t w = 0; w < wave; ++w) o += tot_w[w];
     if (!c) return;
     // the thread's 512 bits span at most two variants (n >= 512) or any number (tiny n: divide per bit)
@@ -1423,8 +1438,12 @@ void launch_vpos_sorted_dev(const uint64_t *f, const uint32_t *mdev, uint64_t ca
     if (!bits_set) hipLaunchKernelGGL(k_vpos_setbits, dim3((uint32_t)std::min<uint64_t>(ceil_div(cap ? cap : 1, 256), 2048)), dim3(256),
                        0, st, f, mdev, n, bm);
     hipLaunchKernelGGL(k_vpos_count, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc);
-    exclusive_scan_u32(bc, boff, nb, boff + nb, scan_scr, st);
-    hipLaunchKernelGGL(k_vpos_emit, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, boff, n, pb, out);
+    if (nb <= VP_DIRECT_BLOCKS) {  // round 6: configs[4]'s 6.7K blocks without the 3-launch scan (~15 us)
+        hipLaunchKernelGGL(k_vpos_emit<true>, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, bc, n, pb, out);
+    } else {
+        exclusive_scan_u32(bc, boff, nb, boff + nb, scan_scr, st);
+        hipLaunchKernelGGL(k_vpos_emit<false>, dim3((uint32_t)nb), dim3(256), 0, st, bm, words, boff, n, pb, out);
+    }
     MKV_LAUNCH_CHECK();
 }
 
@@ -1470,9 +1489,10 @@ void launch_topdown_jump_batch(const uint8_t *ca, const TdVariants &V, uint64_t 
 }
 
 void launch_topdown_top(const uint8_t *na, const TdVariants &V, uint32_t k, const TdTop &P, void *fout, bool wide,
-                        uint32_t *cnt, hipStream_t st, uint32_t zero_n) {
-    if (wide) hipLaunchKernelGGL(k_topdown_top<true>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt, zero_n);
-    else hipLaunchKernelGGL(k_topdown_top<false>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt, zero_n);
+                        uint32_t *cnt, hipStream_t st, uint32_t zero_n, uint32_t ff_from) {
+    ff_from = std::min(ff_from, zero_n);
+    if (wide) hipLaunchKernelGGL(k_topdown_top<true>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt, zero_n, ff_from);
+    else hipLaunchKernelGGL(k_topdown_top<false>, dim3(1), dim3(1024), 0, st, na, V, k, P, fout, cnt, zero_n, ff_from);
     MKV_LAUNCH_CHECK();
 }
 

@@ -284,9 +284,10 @@ struct TdTop {
     uint32_t T[MKV_MAXLEV_TD];
     uint32_t nt;  // jumps T[0] -> ... -> T[nt]
 };
-// zero_n: cnt[0 .. zero_n) zeroed by the kernel first (no fill launch before it).
+// zero_n: cnt[0 .. zero_n) initialised by the kernel first (no fill launch before it): 0 below ff_from,
+// 0xFFFFFFFF from ff_from on.
 void launch_topdown_top(const uint8_t *na, const TdVariants &V, uint32_t k, const TdTop &P, void *fout, bool wide,
-                        uint32_t *cnt, hipStream_t st, uint32_t zero_n = 0);
+                        uint32_t *cnt, hipStream_t st, uint32_t zero_n = 0, uint32_t ff_from = ~0u);
 // Jump k levels down from divergent parents (unsharded plans): fout gets every divergent descendant
 // at the target level (desc_count nodes there). max_desc: upper bound on parents << k (grid sizing).
 // gate: the one-wait pair diff's level-4 abort test folded into the jump from level 4 (k_td_gate's rule on

@@ -292,6 +292,8 @@ struct mkv_tree {
     bool sortctl_dirty = true;  // a sort started and did not reach its clearing launch
     bool kc_pending = false;    // the ragged key copy on st3 is not yet joined into st2
     DevBuf rd_arrive;  // k_reduce_top's arrival counter (zeroed once; every launch leaves it 0)
+    std::vector<DiffSide> tb_sides_host;  // what tb_sides holds (the batched walk's variant sides)
+    const void *tb_sides_dev = nullptr;
     uint32_t walk_fused = 0;  // jumps of the last walk done inside the one-workgroup top launch
     uint64_t hix_skip_gen = 0;  // pfx_gen + 1 of a key set whose hash index did not fit (0: none)
     // introspection of the last batched walk (mkv_tree_walk_stats): (from level, to level) per launch
@@ -2951,7 +2953,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     if (!sharded && L > 1) {  // seed with every variant's root, then jump 4 levels per launch
         size_t q0 = 1;
         if (nt) {  // the roots and the first nt jumps in one workgroup
-            launch_topdown_top(na, V, k, P, fout, true, cnt, t->st, (uint32_t)(L + 2 + 2 * k));
+            launch_topdown_top(na, V, k, P, fout, true, cnt, t->st, (uint32_t)(L + 2 + 2 * k), (uint32_t)(L + 2 + k));
             for (size_t q = 1; q <= nt; ++q) t->walk_jumps.emplace_back((uint32_t)T[q - 1], (uint32_t)T[q]);
             t->walk_fused = (uint32_t)nt;
             q0 = nt + 1;
@@ -3003,6 +3005,18 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
     std::vector<DiffSide> hs(k);
     for (uint32_t i = 0; i < k; ++i) hs[i] = side_of(vs[i]);
     DiffSide *ds = reinterpret_cast<DiffSide *>(t->tb_sides.ensure(k * sizeof(DiffSide)));
+    // the variants' sides on the device: uploaded only when they changed (a value-only update keeps every
+    // array of a tree where it is; the upload is a staged copy of ~15 us on the walk's stream)
+    const bool sides_fresh = t->tb_sides_dev != (void *)ds || t->tb_sides_host.size() != hs.size() ||
+                             std::memcmp(t->tb_sides_host.data(), hs.data(), hs.size() * sizeof(DiffSide)) != 0;
+    auto upload_sides = [&] {
+        if (!sides_fresh) return;
+        MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
+        t->tb_sides_host = hs;
+        t->tb_sides_dev = ds;
+    };
+    // per-variant segment starts: 0xFFFFFFFF, set by the one-workgroup top when it ran
+    const bool vcount_set = !sharded && L > 1 && nt;
     uint64_t check = 0;  // variants whose key set may differ from the base's
     for (uint32_t i = 0; i < k; ++i)
         if (!same_keyset(vs[i], a)) check |= 1ull << i;
@@ -3016,12 +3030,21 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         void *scr = t->d_diffscr.ensure(scan_scratch_bytes(sw));
         launch_vpos_sorted_dev(fin, cnt, cap, n, k, pb, bm, bc, scr, fout, t->st, bits_set);
         t->tb_bm_words = words;
-        MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
-        MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
+        upload_sides();
+        if (!vcount_set) MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
         refs = fin;  // the level-0 frontier is consumed: its buffer holds the refs
         launch_topdown_leaves_batch(fout, cap, pb, A, ds, check, refs, nbad, vcount, t->st, cnt);
-        small_d2h(t, t->h_small, cnt, 4ull * (L + 2), t->st);
-        small_d2h(t, hb, nbad, 2 * k * 4, t->st);
+        {  // the walk's counters and the per-variant words in one readback launch
+            SmallCopies SC{};
+            SC.src[0] = reinterpret_cast<const uint8_t *>(cnt);
+            SC.dst[0] = t->h_small_dev;
+            SC.bytes[0] = (uint32_t)(4 * (L + 2));
+            SC.src[1] = reinterpret_cast<const uint8_t *>(nbad);
+            SC.dst[1] = t->h_small_dev + (reinterpret_cast<uint8_t *>(hb) - reinterpret_cast<uint8_t *>(t->h_small));
+            SC.bytes[1] = (uint32_t)(2 * k * 4);
+            hipLaunchKernelGGL(k_copy_small_many, dim3(2), dim3(64), 0, t->st, SC);
+            MKV_LAUNCH_CHECK();
+        }
         wait_stream(t, t->st);
         const uint32_t *hc = reinterpret_cast<const uint32_t *>(t->h_small);
         if (hc[L + 1] != 0) return false;  // the gate stopped the walk: not worth finishing
@@ -3038,8 +3061,8 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
             void *radix = t->s_radix.ensure(std::max(radix_scratch_bytes(m), scan_scratch_bytes(m + 1)));
             launch_pack_entries(fin, m, pb, k1, v1, t->st);
             const bool swp = radix_sort_pairs(k1, v1, k2, v2, m, 0, pb + vb, radix, t->st);
-            MKV_HIP(hipMemcpyAsync(ds, hs.data(), k * sizeof(DiffSide), hipMemcpyHostToDevice, t->st));
-            MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
+            upload_sides();
+            if (!vcount_set) MKV_HIP(hipMemsetAsync(vcount, 0xFF, k * 4, t->st));
             launch_topdown_leaves_batch(swp ? k2 : k1, m, pb, A, ds, check, refs, nbad, vcount, t->st);
             small_d2h(t, hb, nbad, 2 * k * 4, t->st);
         }
