@@ -2963,7 +2963,15 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         }
         std::swap(fin, fout);
         for (size_t q = q0; q < T.size(); ++q) {
-            const size_t l = T[q - 1], lt = T[q];
+            const size_t l = T[q - 1];
+            // Jumps whose target level is small for all variants together (<= 2^18 nodes: <= ~17 MB of
+            // digest pairs even if every node were compared) are merged with the jump before them: the
+            // frontier above such a level is dense, so one deeper jump compares the same descendants and
+            // saves a launch (configs[4]: 20 -> 16 -> 12 becomes 20 -> 12). Never across the level-4 gate.
+            while (q + 1 < T.size() && T[q + 1] > TD_CHECK_LEVEL && l - T[q + 1] <= 12 &&
+                   (uint64_t)k * a->lev_cnt[T[q + 1]] <= (1ull << 18))
+                ++q;
+            const size_t lt = T[q];
             const int kk = (int)(l - lt);
             t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
             const bool land = bitmap && lt == 0;
