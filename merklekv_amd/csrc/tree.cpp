@@ -2401,6 +2401,18 @@ static size_t top_jumps(const mkv_tree *a, const std::vector<size_t> &T, uint32_
     return nt;
 }
 
+// Jumps whose target level is small for all variants together (k x nodes <= 2^19: <= ~34 MB of digest
+// pairs even if every node were compared) are merged with the jump before them: the frontier above such a
+// level is dense, so one deeper jump compares the same descendants and saves a launch (~6 us). Never
+// across the level-4 gate, at most 12 levels per jump. Returns the index in T of the merged jump's target
+// (the jump from T[q - 1]).
+static size_t merge_small_jumps(const mkv_tree *a, const std::vector<size_t> &T, size_t q, uint64_t k) {
+    const size_t l = T[q - 1];
+    while (q + 1 < T.size() && T[q + 1] > TD_CHECK_LEVEL && l - T[q + 1] <= 12 && k * a->lev_cnt[T[q + 1]] <= (1ull << 19))
+        ++q;
+    return q;
+}
+
 static std::vector<size_t> jump_targets(size_t L, bool fine = false) {
     std::vector<size_t> T{L - 1};
     for (int64_t x = (int64_t)((L - 2) / 4) * 4; x >= 0; x -= (fine && x <= 8) ? 2 : 4) T.push_back((size_t)x);
@@ -2606,7 +2618,9 @@ static mkv_keylist *topdown_pair_onewait(mkv_tree *t, const mkv_tree *a, const m
         std::swap(fin, fout);
     }  // sharded: the frontier at the top level starts empty (cnt[L - 1] = 0); the roots come in as seeds
     for (size_t q = q0; q < T.size(); ++q) {
-        const size_t l = T[q - 1], lt = T[q];
+        const size_t l = T[q - 1];
+        if (!sh) q = merge_small_jumps(a, T, q, 1);  // (100M: 16 -> 12 -> 8 becomes 16 -> 8)
+        const size_t lt = T[q];
         const int k = (int)(l - lt);
         t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
         const uint64_t maxd = std::min<uint64_t>(a->lev_cnt[l] << k, 1ull << 40);
@@ -2964,13 +2978,7 @@ static bool topdown_batch(mkv_tree *t, const mkv_tree *a, const std::vector<cons
         std::swap(fin, fout);
         for (size_t q = q0; q < T.size(); ++q) {
             const size_t l = T[q - 1];
-            // Jumps whose target level is small for all variants together (<= 2^18 nodes: <= ~17 MB of
-            // digest pairs even if every node were compared) are merged with the jump before them: the
-            // frontier above such a level is dense, so one deeper jump compares the same descendants and
-            // saves a launch (configs[4]: 20 -> 16 -> 12 becomes 20 -> 12). Never across the level-4 gate.
-            while (q + 1 < T.size() && T[q + 1] > TD_CHECK_LEVEL && l - T[q + 1] <= 12 &&
-                   (uint64_t)k * a->lev_cnt[T[q + 1]] <= (1ull << 18))
-                ++q;
+            q = merge_small_jumps(a, T, q, k);  // (configs[4]: 20 -> 16 -> 12 becomes 20 -> 12)
             const size_t lt = T[q];
             const int kk = (int)(l - lt);
             t->walk_jumps.emplace_back((uint32_t)l, (uint32_t)lt);
