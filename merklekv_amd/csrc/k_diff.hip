@@ -714,6 +714,32 @@ __global__ void k_diff_keys(const uint64_t *__restrict__ refs, uint64_t m, DiffS
     }
 }
 
+// Fixed-length keys (klen % 16 == 0): one 16-B granule of the list per thread, key k at out + k x klen
+// (the offsets are arithmetic: no offset array is read or written). Every wave's store covers 1 KiB of
+// consecutive bytes and twice as many gathers are in flight as with a thread per key.
+__global__ void k_diff_keys_g16(const uint64_t *__restrict__ refs, uint64_t m, DiffSide A, DiffSide B, uint32_t klen,
+                                uint8_t *__restrict__ out) {
+    const uint32_t gpk = klen >> 4;
+    const uint64_t G = m * gpk;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < G; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = gpk == 2 ? t >> 1 : t / gpk, x = t - k * gpk;  // (32-B keys: a shift)
+        const uint64_t r = refs[k];
+        uint64_t len;
+        const uint8_t *src = key_at((r >> 63) ? B : A, r & ~(1ull << 63), &len) + 16 * x;
+        uint4 v;
+        if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+            v = *reinterpret_cast<const uint4 *>(src);
+        } else {
+            uint32_t w[4];
+            for (int j = 0; j < 4; ++j)
+                w[j] = (uint32_t)src[4 * j] | ((uint32_t)src[4 * j + 1] << 8) | ((uint32_t)src[4 * j + 2] << 16) |
+                       ((uint32_t)src[4 * j + 3] << 24);
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *reinterpret_cast<uint4 *>(out + 16 * t) = v;
+    }
+}
+
 // lohi[0] = lower_bound(prefix), lohi[1] = first index >= lo whose key does not start with prefix.
 __global__ void k_prefix_bounds(DiffSide A, const uint8_t *__restrict__ prefix, uint32_t plen,
                                 uint64_t *__restrict__ lohi) {
@@ -1552,6 +1578,15 @@ void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, co
                          hipStream_t st) {
     if (!m) return;
     hipLaunchKernelGGL(k_diff_keylens, grid1d(m), dim3(256), 0, st, refs, m, A, B, lens);
+    MKV_LAUNCH_CHECK();
+}
+
+void launch_diff_keys_fixed(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t klen,
+                            uint8_t *out, hipStream_t st) {
+    if (!m) return;
+    const uint64_t G = m * (klen / 16);
+    hipLaunchKernelGGL(k_diff_keys_g16, dim3((uint32_t)std::min<uint64_t>(ceil_div(G, 256), 8192)), dim3(256), 0, st, refs, m,
+                       A, B, (uint32_t)klen, out);
     MKV_LAUNCH_CHECK();
 }
 

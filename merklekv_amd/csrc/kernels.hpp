@@ -246,6 +246,9 @@ void launch_diff_keylens(const uint64_t *refs, uint64_t m, const DiffSide &A, co
 void launch_fill_stride_u64(uint64_t *off, uint64_t m, uint64_t stride, hipStream_t st);
 void launch_diff_keys(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, const uint64_t *off,
                       uint8_t *out, hipStream_t st);
+// Fixed-length keys (klen % 16 == 0, klen < 2^20): key k at out + k x klen, one 16-B granule per thread.
+void launch_diff_keys_fixed(const uint64_t *refs, uint64_t m, const DiffSide &A, const DiffSide &B, uint64_t klen,
+                            uint8_t *out, hipStream_t st);
 // One-wait tail of the unsharded top-down pair diff: k_td_gate after the landing on level 4 (screen word
 // cnt[word] != 0 or a frontier over half the level: bit 31 set there, frontier emptied); then from the
 // sorted side-A refs (count *mdev on the device): leaf-key check (nbad), key lengths padded to cap_m,

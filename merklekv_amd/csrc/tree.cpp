@@ -2815,8 +2815,9 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
             size_t pk = prof_begin(t, "diff");
             uint64_t *off = ens<uint64_t>(t->a_outoff, m + 1);
             uint64_t bytes = m * klen;
+            const bool g16 = klen && klen % 16 == 0 && klen < (1u << 20);  // granule gather, offsets implicit
             if (klen) {  // fixed-length keys: offsets k * klen, no length gather / scan / readback
-                launch_fill_stride_u64(off, m, klen, t->st);
+                if (!g16) launch_fill_stride_u64(off, m, klen, t->st);
                 prof_end(t, pk);
             } else {
                 uint64_t *lens = ens<uint64_t>(t->a_lens, m + 1);
@@ -2829,7 +2830,8 @@ static mkv_keylist *keylist_from_refs_async(mkv_tree *t, const uint64_t *refs, u
                 bytes = t->h_small[0];
             }
             uint8_t *ob = ens<uint8_t>(t->a_out, bytes + 16);
-            launch_diff_keys(refs, m, A, B, off, ob, t->st);
+            if (g16) launch_diff_keys_fixed(refs, m, A, B, klen, ob, t->st);
+            else launch_diff_keys(refs, m, A, B, off, ob, t->st);
             l->n = m;
             const uint64_t kpos = (8 * (m + 1) + 15) & ~uint64_t(15);
             l->blk = std::make_shared<PinnedBlock>(kpos + bytes + 16, klen != 0);
