@@ -38,7 +38,8 @@ namespace {
 constexpr int RG_WAVES = 4;                             // waves per workgroup
 // Lane stride 34 dwords: slots 8-B aligned, read back as 8-B words — lanes 0-31 (and 32-63) of a
 // ds_read_b64 then start on 32 distinct even banks of 64 (34 / 2 = 17 is odd), conflict-free — and a
-// 4-wave workgroup takes 34.3 KiB: three of them (12 waves per CU) leave room for a 56.5-KiB sort tile.
+// 4-wave workgroup takes 34.3 KiB: three of them (12 waves per CU) leave room for a 56.5-KiB sort tile,
+// two of them (the default since round 6) for the sort's tiles to co-run at full width.
 constexpr uint32_t RG_STRIDE = 34;                      // dwords per lane
 constexpr uint32_t RG_FRONT = 16;                       // trash below lane 0's slot
 constexpr uint32_t RG_WAVE_DW = RG_FRONT + 64 * RG_STRIDE;  // lane 63 reaches dword 16 + 63 x 34 + 30
@@ -48,7 +49,10 @@ static_assert(RG_STRIDE >= 31 && RG_STRIDE % 2 == 0 && (RG_STRIDE / 2) % 2 == 1,
 constexpr uint32_t RG_GRAIN = 4;                        // virtual chunks per hand-out atomic
 constexpr uint32_t RG_INV = 0xFFFFFFFFu;
 #ifndef MKV_RAGGED_WGS
-#define MKV_RAGGED_WGS 3                                // workgroups per CU (persistent grid)
+// workgroups per CU (persistent grid). Round 6: 2 instead of 3 — with the faster leaf stage the radix
+// passes beside it had become the ragged build's critical path (sort 2.0 vs hash 1.8 ms); at 2 the hash
+// runs ~5 % slower but the sort ~0.25 ms faster: build 2.92-2.96 -> 2.80-2.85 ms (interleaved A/B, 4 reps)
+#define MKV_RAGGED_WGS 2
 #endif
 
 typedef uint32_t rg4 __attribute__((ext_vector_type(4), aligned(4)));
