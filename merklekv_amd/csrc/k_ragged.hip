@@ -379,10 +379,9 @@ __global__ __launch_bounds__(64 * RG_WAVES) __attribute__((amdgpu_waves_per_eu(4
     }
 }
 
-// The records k_leaf_ragged leaves (the prefix and suffix outside rg_inner's interval): one wave per record,
-// lane l reads message byte l of each block inside the record's fields (no load outside them), shuffles
-// assemble the 16 words, and every lane runs the compression. A few hundred records normally; every record
-// only for blobs of empty or tiny keys.
+// The records k_leaf_ragged leaves (the prefix and suffix outside rg_inner's interval): one record per lane,
+// every message byte read inside the record's fields (no load outside them). A few hundred records
+// normally; every record for blobs whose values (or keys) are all empty or tiny.
 __device__ __forceinline__ uint32_t edge_byte(const uint8_t *kp, const uint8_t *vp, uint32_t k, uint32_t v, uint32_t L,
                                               uint32_t nb, uint32_t p) {
     if (p < 4) return (k >> (24 - 8 * p)) & 0xFFu;
@@ -433,26 +432,29 @@ __global__ __launch_bounds__(256) void k_leaf_edges(const uint8_t *__restrict__ 
     uint64_t P = s_ends[0], S = s_ends[1];
     if (P >= S) P = S = n;  // no interval: every record is an edge one
     const uint64_t m = P + (n - S);
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / 64) + wave; i < m; i += nw) {
+    // one record per lane (round 6; it had been one wave per record, every lane assembling one byte): a
+    // blob of empty values makes EVERY record an edge one (voff never moves off voff[0]), and 10M such
+    // records then took ~30 ms through one wave each
+    const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += nt) {
         const uint64_t r = i < P ? i : S + (i - P);
         const uint64_t k0 = koff[r], v0 = voff[r];
         const uint32_t k = (uint32_t)(koff[r + 1] - k0), v = (uint32_t)(voff[r + 1] - v0);
         const uint32_t L = 8 + k + v, nb = (L + 72) >> 6;
+        const uint8_t *kp = kb + k0, *vp = vb + v0;
         uint32_t st[8];
         sha_init(st);
         for (uint32_t b = 0; b < nb; ++b) {
-            const uint32_t byte = edge_byte(kb + k0, vb + v0, k, v, L, nb, 64 * b + lane);
-            const uint32_t mine = (byte << (24 - 8 * (lane & 3)));  // this byte's place in its BE word
-            uint32_t word = mine;
-            word |= __shfl_xor(word, 1);
-            word |= __shfl_xor(word, 2);  // every lane of a 4-lane group now holds the group's word
             uint32_t w[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) w[j] = __shfl(word, 4 * j);
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t p = 64 * b + 4 * j;
+                w[j] = (edge_byte(kp, vp, k, v, L, nb, p) << 24) | (edge_byte(kp, vp, k, v, L, nb, p + 1) << 16) |
+                       (edge_byte(kp, vp, k, v, L, nb, p + 2) << 8) | edge_byte(kp, vp, k, v, L, nb, p + 3);
+            }
             sha_compress<false>(st, w);
         }
-        if (lane == 0) store_digest(out + 32 * (uint64_t)r, st);
+        store_digest(out + 32 * r, st);
     }
 }
 

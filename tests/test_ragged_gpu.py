@@ -158,6 +158,31 @@ def test_ragged_edge_prefix_and_suffix(n, shape):
         assert g == _enc_digest(k, v), (len(k), len(v))
 
 
+@pytest.mark.parametrize("klen", [3, 32])
+def test_ragged_empty_values_every_record_an_edge_one(klen):
+    """Empty values everywhere: voff never moves off voff[0], so every record is an edge one (k_leaf_edges,
+    one record per lane) — 300K records at key lengths 3 (duplicates: last write wins) and 32, device blobs
+    at an unaligned base; root and leaves equal the oracle's."""
+    import torch
+    rng = np.random.default_rng(4242 + klen)
+    n = 300_000
+    pk = rng.integers(0, 256, size=n * klen, dtype=np.uint8)
+    pko = np.arange(0, n + 1, dtype=np.uint64) * klen
+    pv = np.zeros(0, np.uint8)
+    pvo = np.zeros(n + 1, np.uint64)
+    o = coracle.OracleTree.build(pk, pko, pv, pvo)
+    dk = torch.zeros(len(pk) + 1, dtype=torch.uint8, device="cuda")
+    dk[1:] = torch.from_numpy(pk.copy()).cuda()
+    dv = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    dko = torch.from_numpy(pko.astype(np.int64)).cuda()
+    dvo = torch.from_numpy(pvo.astype(np.int64)).cuda()
+    torch.cuda.synchronize()
+    t = MerkleTree()
+    t.build_device(dk.data_ptr() + 1, dko.data_ptr(), dv.data_ptr(), dvo.data_ptr(), n)
+    assert t.get_root_hash() == o.root()
+    assert b"".join(t.level_digests(0)) == o.level(0).tobytes()
+
+
 def test_ragged_mixed_with_fixed_chunks_and_duplicates():
     """Fixed-shape chunks (32 / 100 B, k_leaf_direct) interleaved with ragged ones, duplicate keys (last
     write wins) and empty keys / values, against the oracle."""
