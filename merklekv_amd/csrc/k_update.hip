@@ -338,7 +338,12 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
 // (mkv_tree_update_counts) are kept in LDS and added to the trees' counters once per workgroup.
 // ---------------------------------------------------------------------------------------------------
 constexpr int CW_THREADS = 256;  // four independent waves
-constexpr uint32_t CW_MAX_BLOCKS = 1024;  // 4 waves per SIMD x 1,024 SIMDs / 4 waves per block (3: climb 0.82-0.84 ms, 4: 0.81, 5 spills: 0.82-0.83)
+// Launch cap: 2,048 workgroups (two per resident slot at 4 waves per SIMD), so a wave whose batches merge
+// early leaves its slot to a later workgroup instead of taking a fixed share of a grid-stride loop (round 6,
+// configs[4] climb: 1,024 resident workgroups 0.78 ms, 2,048 0.75-0.76, one batch per wave 0.75-0.75; 5 waves
+// per SIMD, 95 VGPRs since the level state moved to LDS: 0.75-0.77. Round 5 with the register-carried
+// state: 3 waves 0.82-0.84, 4 waves 0.81, 5 spilled).
+constexpr uint32_t CW_MAX_BLOCKS = 2048;
 
 // Tree node arrays are addressed through GLOBAL-address-space pointers: a pointer read back from LDS is a
 // generic (flat) pointer, and a flat load also counts in lgkmcnt — every LDS wait of the level would then
@@ -432,130 +437,123 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
     const uint32_t n = A.M;
     const uint64_t *__restrict__ keys = A.pos;
     const uint32_t nb_cap = (n + 63) / 64, nwaves = gridDim.x * (CW_THREADS / 64);
-    for (uint32_t bt = blockIdx.x * (CW_THREADS / 64) + (tid >> 6); bt < nb_cap; bt += nwaves) {
-        // ---- the batch's entries / survivors that climb ----
-        const uint32_t s = bt * 64 + lane;
-        bool surv = false;
-        uint32_t t = 0, lo = 0, hi = 0, have = 0;
-        uint64_t x = 0, pn = 0, pp1 = 0;
-        uint32_t d[8];
-        uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
-        int l = 0;
-        if (s < n) {
-            const uint64_t key = keys[s];
-            t = (uint32_t)(key >> A.pbits);
-            if ((s + 1 == n || keys[s + 1] != key) && t < A.k && s_miss[t] == 0) {
-                // earlier writes of the same key: the run's start by galloping back, then a binary search
-                // (a serial walk was O(run length) dependent loads on one lane: a hot key written 1e5 times
-                // stalled its wave and with it the whole climb launch)
-                lo = s;
-                uint32_t step = 1;
-                while (lo >= step && keys[lo - step] == key) {
-                    lo -= step;
-                    step <<= 1;
-                }
-                uint32_t a = lo >= step ? lo - step + 1 : 0;  // keys[a - 1] != key (or a == 0); keys[lo] == key
-                while (a < lo) {
-                    const uint32_t mid = (a + lo) >> 1;
-                    if (keys[mid] == key) lo = mid;
-                    else a = mid + 1;
-                }
-                load_digest(A.bdig + 32ull * A.bidx[s], d);
-                surv = true;
-            }
-            if (surv) {
-                hi = s;
-                pn = s + 1 < n ? keys[s + 1] : ~0ull;
-                pp1 = lo > 0 ? keys[lo - 1] + 1 : 0;
-                x = (P.goff + (key & pmask)) >> l;
-                uint64_t sib = 0;
-                if (classify(P, t, l, x, pn, pp1, &sib) == CL_CLEAN) {
-                    g_load_raw(gptr(s_nodes[t]) + 32 * sib, n0, n1);
-                    have = 1;
-                }
-            }
-        }
-        for (;; ++l) {
-            // ---- compaction: survivor k -> slot k / lane k (key order kept), through the wave's LDS ----
-            const uint64_t m = __ballot(surv);
-            const uint32_t c = (uint32_t)__popcll(m);
-            if (c == 0) break;
-            if (surv) {
-                const uint32_t k = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-                q_x[k] = x;
-                q_pn[k] = pn;
-                q_pp[k] = pp1;
-                q_lo[k] = lo;
-                q_hi[k] = hi;
-                q_t[k] = t | (have << 31);
+    // Survivor k -> slot k (key order kept): the level's state lives in the wave's LDS slots, read back
+    // whole at the top of every level. No per-lane state crosses a level in registers, so the level body
+    // needs no register copies to merge its branches (round 6: ~80 v_mov per level before).
+    auto compact = [&](bool sv, uint32_t t_, int cls_, uint64_t x_, uint64_t pn_, uint64_t pp_, uint32_t lo_,
+                       uint32_t hi_, const uint32_t *d_, const uint4 &a_, const uint4 &b_) -> uint32_t {
+        const uint64_t m = __ballot(sv);
+        if (sv) {
+            const uint32_t k = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+            q_x[k] = x_;
+            q_pn[k] = pn_;
+            q_pp[k] = pp_;
+            q_lo[k] = lo_;
+            q_hi[k] = hi_;
+            q_t[k] = t_ | ((uint32_t)cls_ << 30);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) q_d[i][k] = d[i];
-                q_s[0][k] = n0.x; q_s[1][k] = n0.y; q_s[2][k] = n0.z; q_s[3][k] = n0.w;
-                q_s[4][k] = n1.x; q_s[5][k] = n1.y; q_s[6][k] = n1.z; q_s[7][k] = n1.w;
+            for (int i = 0; i < 8; ++i) q_d[i][k] = d_[i];
+            uint32_t w[8];
+            raw_to_words(a_, b_, w);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) q_s[i][k] = w[i];
+        }
+        return (uint32_t)__popcll(m);
+    };
+    for (uint32_t bt = blockIdx.x * (CW_THREADS / 64) + (tid >> 6); bt < nb_cap; bt += nwaves) {
+        // ---- the batch's entries: the last write of each key starts a climb ----
+        uint32_t c;
+        int l = 0;
+        {
+            const uint32_t s = bt * 64 + lane;
+            bool surv = false;
+            uint32_t t = 0, lo = 0, hi = 0;
+            int cls = CL_TOP;
+            uint64_t x = 0, pn = 0, pp1 = 0;
+            uint32_t d[8];
+            uint4 n0 = make_uint4(0, 0, 0, 0), n1 = n0;
+            if (s < n) {
+                const uint64_t key = keys[s];
+                t = (uint32_t)(key >> A.pbits);
+                if ((s + 1 == n || keys[s + 1] != key) && t < A.k && s_miss[t] == 0) {
+                    // earlier writes of the same key: the run's start by galloping back, then a binary search
+                    // (a serial walk was O(run length) dependent loads on one lane: a hot key written 1e5 times
+                    // stalled its wave and with it the whole climb launch)
+                    lo = s;
+                    uint32_t step = 1;
+                    while (lo >= step && keys[lo - step] == key) {
+                        lo -= step;
+                        step <<= 1;
+                    }
+                    uint32_t a = lo >= step ? lo - step + 1 : 0;  // keys[a - 1] != key (or a == 0); keys[lo] == key
+                    while (a < lo) {
+                        const uint32_t mid = (a + lo) >> 1;
+                        if (keys[mid] == key) lo = mid;
+                        else a = mid + 1;
+                    }
+                    load_digest(A.bdig + 32ull * A.bidx[s], d);
+                    surv = true;
+                }
+                if (surv) {
+                    hi = s;
+                    pn = s + 1 < n ? keys[s + 1] : ~0ull;
+                    pp1 = lo > 0 ? keys[lo - 1] + 1 : 0;
+                    x = P.goff + (key & pmask);
+                    uint64_t sib = 0;
+                    cls = classify(P, t, 0, x, pn, pp1, &sib);
+                    if (cls == CL_CLEAN) g_load_raw(gptr(s_nodes[t]) + 32 * sib, n0, n1);
+                }
             }
+            c = compact(surv, t, cls, x, pn, pp1, lo, hi, d, n0, n1);
+        }
+        for (; c != 0; ++l) {
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            // ---- this level: lane k holds dirty node k (slots >= c are stale; every use is under act) ----
             const bool act = lane < c;
-            if (act) {
-                x = q_x[lane];
-                pn = q_pn[lane];
-                pp1 = q_pp[lane];
-                lo = q_lo[lane];
-                hi = q_hi[lane];
-                const uint32_t tq = q_t[lane];
-                t = tq & 0x7FFFFFFFu;
-                have = tq >> 31;
+            uint64_t x = q_x[lane], pn = q_pn[lane], pp1 = q_pp[lane];
+            uint32_t lo = q_lo[lane], hi = q_hi[lane];
+            const uint32_t tq = q_t[lane];
+            const uint32_t t = tq & 0x3FFFFFFFu;
+            int cls = (int)(tq >> 30);  // classified one level ahead (with the sibling read)
+            uint32_t d[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) d[i] = q_d[i][lane];
-            }
+            for (int i = 0; i < 8; ++i) d[i] = q_d[i][lane];
+            g_u8 *const nodes = gptr(s_nodes[act ? t : 0]);
             if (l == A.lstop) {  // dense from here: the reduction rehashes the levels above whole
                 if (act) {
-                    g_store_digest(gptr(s_nodes[t]) + 32 * (P.off[l] + (x - P.base[l])), d);
+                    g_store_digest(nodes + 32 * (P.off[l] + (x - P.base[l])), d);
                     atomicAdd(&s_lc[t * L + l], 1u);
                 }
                 break;
             }
-            // ---- this level: lane k holds dirty node k ----
-            uint64_t sib = 0;
-            const int cls = act ? classify(P, t, l, x, pn, pp1, &sib) : CL_TOP;
-            surv = false;
-            bool hash = false;
-            uint32_t sg[8];
+            bool surv = false, hash = false;
+            // the sibling's words for the hash: slots q_s of this lane (clean sibling read one level ahead,
+            // or a rendezvous partner's digest) or the digest slots of lane - 1 (dirty sibling in the wave);
+            // one read path, so no sibling registers are carried between branches or levels
+            const uint32_t *sp = &q_s[0][lane];
+            g_u8 *ra = nodes;  // the next level's read: the parent's sibling when it is clean, else any valid line
             if (act) {
-                g_u8 *np = gptr(s_nodes[t]) + 32 * (P.off[l] + (x - P.base[l]));
-                atomicAdd(&s_lc[t * L + l], 1u);  // node (l, x) is dirty: stored below in every branch
+                g_u8 *np = nodes + 32 * (P.off[l] + (x - P.base[l]));
+                atomicAdd(&s_lc[t * L + l], 1u);  // node (l, x) is dirty: stored in every case
+                g_store_digest(np, d);
                 if (cls == CL_TOP) {
-                    g_store_digest(np, d);
+                    // parent not owned: done
                 } else if (cls == CL_PROMO) {
-                    g_store_digest(np, d);
                     surv = true;
-                } else if (cls == CL_CLEAN) {
-                    if (have) {
-                        const uint4 a = make_uint4(q_s[0][lane], q_s[1][lane], q_s[2][lane], q_s[3][lane]);
-                        const uint4 b = make_uint4(q_s[4][lane], q_s[5][lane], q_s[6][lane], q_s[7][lane]);
-                        raw_to_words(a, b, sg);
-                    }
-                    else {  // (not expected: read one level ahead)
-                        uint4 a, b;
-                        g_load_raw(gptr(s_nodes[t]) + 32 * sib, a, b);
-                        raw_to_words(a, b, sg);
-                    }
-                    g_store_digest(np, d);
+                } else if (cls == CL_CLEAN) {  // the sibling was read one level ahead (slots q_s)
                     hash = surv = true;
                 } else if ((x & 1) && lane > 0) {  // right sibling of lane - 1, which stops: merge here
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) sg[i] = q_d[i][lane - 1];
+                    sp = &q_d[0][lane - 1];
                     lo = q_lo[lane - 1];
                     pp1 = q_pp[lane - 1];
-                    g_store_digest(np, d);
                     hash = surv = true;
                 } else if (!(x & 1) && lane + 1 < c) {
-                    g_store_digest(np, d);  // left sibling of lane + 1, which goes on
+                    // left sibling of lane + 1, which goes on
                 } else {
                     // the sibling's entries belong to another batch: rendezvous at entry boundary b
                     const bool right = x & 1;
                     const uint64_t b = right ? lo : (uint64_t)hi + 1;
-                    g_store_digest(np, d);
                     uint64_t *mb = reinterpret_cast<uint64_t *>(A.mbox) + b * MBOX_WORDS;
                     uint64_t *mine = mb + (right ? MBOX_SIDE_WORDS : 0), *other = mb + (right ? 0 : MBOX_SIDE_WORDS);
 #pragma unroll
@@ -579,10 +577,10 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                         __hip_atomic_fetch_and(bw, ~bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the atomic
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
+                        for (int i = 0; i < 4; ++i) {  // into this lane's own sibling slots (sp)
                             const uint64_t v = __hip_atomic_load(other + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            sg[2 * i] = (uint32_t)v;
-                            sg[2 * i + 1] = (uint32_t)(v >> 32);
+                            q_s[2 * i][lane] = (uint32_t)v;
+                            q_s[2 * i + 1][lane] = (uint32_t)(v >> 32);
                         }
                         const uint64_t oi = __hip_atomic_load(other + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         const uint64_t ok = __hip_atomic_load(other + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -596,29 +594,33 @@ __global__ __launch_bounds__(CW_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4
                         hash = surv = true;
                     }
                 }
-                // the parent's clean sibling, read now: it lands while this level hashes
-                have = 0;
-                if (surv) {
+                // the parent's class and, when its sibling is clean, the sibling itself (below), read now: it
+                // lands while this level hashes (the next level's stop needs neither)
+                cls = CL_TOP;
+                if (surv && l + 1 != A.lstop) {
                     uint64_t sib2 = 0;
-                    if (l + 1 != A.lstop && classify(P, t, l + 1, x >> 1, pn, pp1, &sib2) == CL_CLEAN) {
-                        g_load_raw(gptr(s_nodes[t]) + 32 * sib2, n0, n1);
-                        have = 1;
-                    }
+                    cls = classify(P, t, l + 1, x >> 1, pn, pp1, &sib2);
+                    if (cls == CL_CLEAN) ra = nodes + 32 * sib2;
                 }
-                if (hash) {
-                    const bool right = x & 1;
-                    uint32_t lw[8], rw[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        lw[i] = right ? sg[i] : d[i];
-                        rw[i] = right ? d[i] : sg[i];
-                    }
-                    sha_node<false>(lw, rw, d);
-                }
-                if (surv) x >>= 1;
             }
-            __builtin_amdgcn_wave_barrier();  // this level's slot reads come before the next level's writes
+            // issued by every lane (a valid line where the sibling is not clean), so no branch merges n0 / n1
+            uint4 n0, n1;
+            g_load_raw(ra, n0, n1);
+            if (hash) {
+                const bool right = x & 1;
+                uint32_t lw[8], rw[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t sw = sp[64 * i];
+                    lw[i] = right ? sw : d[i];
+                    rw[i] = right ? d[i] : sw;
+                }
+                sha_node<false>(lw, rw, d);
+            }
+            x >>= 1;
+            __builtin_amdgcn_wave_barrier();  // this level's slot reads come before the compaction's writes
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            c = compact(surv, t, cls, x, pn, pp1, lo, hi, d, n0, n1);
         }
     }
     // ---- level counts: the last wave of the workgroup adds them to the trees' counters ----
