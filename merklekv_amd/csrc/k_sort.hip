@@ -212,6 +212,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_os_pass(const uint64_t *__restri
                                                        uint64_t n, int shift, const uint32_t *__restrict__ gcount,
                                                        uint64_t *__restrict__ lookback, uint32_t *__restrict__ ctl,
                                                        uint32_t epoch) {
+    static_assert(IPT % 4 == 0, "the local reorder packs 4 output digits per word (dig[IPT / 4])");
     sort_prio();
     // The scan scratch and the tile id live in the first 260 B of the key tile (written only by the local
     // sort, after the barrier that follows them): 56,320 B at IPT 24 = 55 KiB, so one tile fits beside
