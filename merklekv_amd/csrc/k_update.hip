@@ -312,23 +312,26 @@ __global__ __launch_bounds__(256) void k_locate_multi(LeafBatches B, LocateMulti
 // Entries: the batch positions sorted by (tree << pbits | leaf) — a run of equal keys is one leaf written
 // several times; its LAST entry is the last write (merkle.rs:54). Lane k of a wave holds the batch's k-th
 // dirty node (l, x) in key order: tree, the index range [lo, hi] of the entries under it with the
-// neighbouring entries pn = key[hi + 1], pp = key[lo - 1], its digest (registers) and its sibling's digest
-// read one level ahead. Per level (classify):
+// neighbouring entries pn = key[hi + 1], pp = key[lo - 1], its digest and its sibling's digest read one
+// level ahead, kept in the wave's LDS slots between levels (round 6: read whole at the top of a level, so
+// no register state crosses the level's branches) together with the node's class, computed with that
+// read-ahead. Per level (classify):
 //   * parent not owned (root, or a shard's seam): store the digest, done;
 //   * x is an odd level's last node: store it, the parent is the digest unchanged (R5 promotion);
 //   * sibling clean (no entry inside its leaf range: one compare of pn or pp): store the digest, parent =
 //     SHA-256(left || right) (R4) with the sibling's 32 B, read one level ahead (it lands while the
 //     previous level hashes): 32 B read + 32 B written per rehashed node, the dirty child is never re-read;
 //   * sibling dirty and held by lane k +/- 1 (the entries are sorted, so a dirty sibling's entries are the
-//     neighbouring lane's): the left lane stores and stops, the right one reads its digest from the wave's
-//     LDS slots and hashes the parent — no memory round trip, no barrier;
+//     neighbouring lane's): the left lane stores and stops, the right one hashes the parent with the left
+//     lane's digest slots — no memory round trip, no barrier;
 //   * sibling dirty beyond the batch (first / last lane only): a rendezvous with the other wave through a
 //     mailbox per entry boundary — both sides publish {digest, outer entry bound, its neighbour}
 //     write-through (sc1), drain, then fetch_or the boundary's bit at agent scope; the first arriver stops,
 //     the second clears the bit, reads the other side with sc1 loads (the hand-off form of
 //     MI355X_MICROARCH.md: sc1 payload -> vmcnt(0) -> atomic; consumer: returned atomic -> sc1 loads) and
-//     goes on. The bits are all-zero again when the launch ends.
-// After each level the survivors are compacted into the low lanes through the wave's LDS slots. A wave's
+//     goes on (the partner's digest goes into its own sibling slots). The bits are all-zero again when the
+//     launch ends.
+// After each level the survivors are compacted into the low slots (lane k of the next level = slot k). A wave's
 // lanes thin out as its batch merges, so the climb stops at level `lstop`, the first level whose nodes span
 // the mean gap between dirty leaves (about half of its nodes are dirty): it stores its dirty nodes there,
 // and every level above is rehashed whole by the build's reduction kernels (run_reduce from lstop, all k
